@@ -1,0 +1,265 @@
+/*
+ * rtkv.h — C ABI of the MI355X (gfx950) streaming prefill KV-cache compression path.
+ *
+ * This library replaces the PyTorch eager hot path of the reference
+ * (EvelynHung-79/RealTime-KV-cache-Compression):
+ *
+ *   RealTimePrefillCompressor.compress_layer_kv_cache      src/compression/unified_compressor.py:95-172
+ *     ├─ PromptGuidedImportanceScorer.*                    src/compression/token_importance.py:21-176
+ *     ├─ DynamicPrecisionQuantizer.*                       src/compression/dynamic_quantization.py:21-196
+ *     └─ SelectiveTokenPropagator.*                        src/compression/selective_propagation.py:68-244
+ *
+ * Conventions
+ *   - Every pointer argument named *_dev is a device pointer (hipMalloc / torch CUDA tensor).
+ *   - All work is stream-ordered on `stream` (a hipStream_t passed as void*; NULL = default stream).
+ *     No entry point allocates, frees or synchronises; scratch comes from a caller-owned workspace
+ *     sized by rtkv_workspace_size().  Inputs are never mutated.
+ *   - Return value: 0 on success, a negative RTKV_ERR_* code otherwise; rtkv_last_error() returns a
+ *     human-readable message for the calling thread.  Errors that depend on device data (e.g. the
+ *     fp16 16-bit overflow) are reported through rtkv_layer_stats.error_flags after the stream syncs.
+ *   - dtype codes: RTKV_F32 / RTKV_F16 / RTKV_BF16.  Arithmetic follows the reference's PyTorch CPU
+ *     semantics: every elementwise op is computed in fp32 and rounded to the tensor dtype
+ *     (round-to-nearest-even), division is IEEE, no FMA contraction.
+ *   - Token precision classes ("labels") are 0 = LOW, 1 = MEDIUM, 2 = HIGH
+ *     (dynamic_quantization.py:41-45), stored as uint8.
+ */
+#ifndef RTKV_H
+#define RTKV_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RTKV_ABI_VERSION 1
+
+enum rtkv_dtype { RTKV_F32 = 0, RTKV_F16 = 1, RTKV_BF16 = 2 };
+
+enum rtkv_status {
+  RTKV_OK = 0,
+  RTKV_ERR_INVALID = -1,     /* bad shape / stride / parameter */
+  RTKV_ERR_UNSUPPORTED = -2, /* configuration outside the implemented envelope */
+  RTKV_ERR_HIP = -3,         /* a HIP runtime call failed */
+  RTKV_ERR_WORKSPACE = -4    /* workspace too small */
+};
+
+/* rtkv_layer_stats.error_flags bits (device-detected, read after the stream syncs) */
+enum rtkv_error_flag {
+  /* A populated class uses a bit width whose qmax = 2^b-1 overflows fp16 (b >= 16).  The reference
+   * raises "value cannot be converted to type c10::Half without overflow" at
+   * dynamic_quantization.py:121 in that case; the host wrapper raises the same RuntimeError. */
+  RTKV_FLAG_F16_QMAX_OVERFLOW = 1
+};
+
+/* Flags for rtkv_layer_params.flags */
+enum rtkv_layer_flag {
+  RTKV_EMIT_DEQUANT = 1,   /* write the dequantized K'/V' (the reference's return value) */
+  RTKV_EMIT_PACKED = 2,    /* write bit-packed integer codes + per-row scale/zero-point */
+  RTKV_NO_SELECTION = 4    /* keep every token (quantization only, BASELINE config 2) */
+};
+
+/* ------------------------------------------------------------------------------------------------
+ * Parameter block.  Field-by-field mirror of configs/base_config.py:4-56 as consumed on the path.
+ * The host fills the float fields with the float32 rounding of the config's Python floats, exactly
+ * as PyTorch casts a Python scalar against an fp32 tensor.
+ * ---------------------------------------------------------------------------------------------- */
+typedef struct rtkv_layer_params {
+  float alpha;             /* token_importance.py:163  (config.alpha) */
+  float beta;              /* token_importance.py:167  (config.beta) */
+  float gamma;             /* token_importance.py:171  (config.gamma) */
+  float layer_weight;      /* token_importance.py:162  (config.layer_weights[layer_idx]) */
+  float theta_h;           /* dynamic_quantization.py:41 */
+  float theta_m;           /* dynamic_quantization.py:42 */
+  int32_t bits[3];         /* bits by class {LOW, MEDIUM, HIGH}: dynamic_quantization.py:169-174 */
+  int32_t prompt_len;      /* P = max(1, min(S // 5, 128)): unified_compressor.py:55 */
+  double propagation_ratio;/* selective_propagation.py:23-38 for this layer */
+  int32_t flags;           /* RTKV_EMIT_* | RTKV_NO_SELECTION */
+  int32_t reserved;
+} rtkv_layer_params;
+
+/* Attention input.  W[b, h, i, c] at w + b*stride_b + h*stride_h + i*stride_s + c (elements);
+ * only columns c < prompt_len are read (token_importance.py:41 reads W[..., prompt_indices] with
+ * prompt_indices = arange(P)).  Either the reference's full [B,H,S,S] matrix or a [B,H,S,P] prompt
+ * slice can be passed: both give bit-identical results. */
+typedef struct rtkv_attn_desc {
+  const void* w_dev;
+  int32_t dtype;
+  int32_t reserved;
+  int64_t B, H, S, cols;               /* cols >= prompt_len */
+  int64_t stride_b, stride_h, stride_s;
+} rtkv_attn_desc;
+
+/* Key/value states.  x[b, i, h, d] at base + b*stride_b + i*stride_s + h*stride_h + d.
+ * The reference layout [B, S, Hkv*D] (modified_llama.py:105-108) is stride_s = Hkv*D, stride_h = D;
+ * the model's native [B, Hkv, S, D] layout is stride_h = S*D, stride_s = D (no transpose copy). */
+typedef struct rtkv_kv_desc {
+  const void* k_dev;
+  const void* v_dev;
+  int32_t dtype;
+  int32_t reserved;
+  int64_t B, S, H, D;
+  int64_t stride_b, stride_s, stride_h;
+} rtkv_kv_desc;
+
+/* Per-batch-row statistics (device-resident; one entry per batch row after the header). */
+typedef struct rtkv_batch_stats {
+  int64_t class_count[3];    /* tokens per class, dynamic_quantization.py:50-57 */
+  int64_t kept;              /* selected tokens S'_b */
+  int64_t kept_class[3];     /* selected tokens per class (selective_propagation.py:126-133) */
+  int64_t cost_units;        /* Σ bits of the selected tokens = 8 * current_cost (:122-131) */
+  int64_t packed_bytes;      /* bytes of packed codes per tensor for this row */
+  int32_t fallback;          /* 1 if the top-10% emergency fallback ran (:205-211) */
+  int32_t reserved;
+  double kept_score_sum;     /* Σ scores of selected tokens (avg_importance, :139) */
+} rtkv_batch_stats;
+
+typedef struct rtkv_layer_stats {
+  int64_t max_kept;          /* S'_max = max_b S'_b: rows of the padded output (:183) */
+  int64_t total_packed_bytes;/* bytes used in each packed code buffer */
+  double score_sum;          /* Σ scores over B*S   (unified_compressor.py:159) */
+  double score_m2;           /* Σ (s - mean)^2      (unified_compressor.py:160, unbiased std) */
+  float score_min;           /* unified_compressor.py:161 */
+  float score_max;           /* unified_compressor.py:162 */
+  int32_t error_flags;       /* RTKV_FLAG_* */
+  int32_t B;
+  /* followed by B x rtkv_batch_stats */
+} rtkv_layer_stats;
+
+static inline size_t rtkv_stats_bytes(int64_t B) {
+  return sizeof(rtkv_layer_stats) + (size_t)B * sizeof(rtkv_batch_stats);
+}
+
+/* Outputs of one layer.  Any pointer may be NULL to skip that output (scores/labels/mask/kept_index
+ * /stats are always needed by the fused driver and must be non-NULL there).
+ *
+ * Output rows are the selected tokens in ascending original index (selective_propagation.py:224-232),
+ * zero-padded per batch row up to S'_max (:214-222).
+ *
+ * Packed codes: for output row r of batch row b with class c, bits w = rtkv_field_width(dtype,
+ * bits[c]) per element; the row's F = H*D codes form a little-endian bit stream (element f at stream
+ * bits [f*w, f*w + w), stream bit k = bit (k & 7) of byte k >> 3) of ceil(F*w/8) bytes stored at
+ * packed_{k,v}_dev + row_offset[b*row_capacity + r].  The same offsets serve K and V.
+ * scale_zp[(b*row_capacity + r)*4 + {0,1,2,3}] = {k_scale, k_zero_point, v_scale, v_zero_point}
+ * (values exactly representable in the K/V dtype, stored as fp32). */
+typedef struct rtkv_layer_out {
+  void* k_out_dev;           /* dequantized K' in the K/V dtype, [B, row_capacity, H, D] via strides */
+  void* v_out_dev;
+  int64_t o_stride_b, o_stride_s, o_stride_h;
+  int64_t row_capacity;      /* rows available per batch row (>= S'_max; S is always enough) */
+  float* scores_dev;         /* [B, S] fp32 importance scores */
+  uint8_t* labels_dev;       /* [B, S] precision classes */
+  uint8_t* mask_dev;         /* [B, S] 1 = selected */
+  int32_t* kept_index_dev;   /* [B, row_capacity] original token index per output row, -1 = pad */
+  uint8_t* packed_k_dev;     /* packed code buffers (capacity packed_capacity bytes each) */
+  uint8_t* packed_v_dev;
+  int64_t packed_capacity;
+  int64_t* row_offset_dev;   /* [B, row_capacity] byte offset of each row's codes */
+  float* scale_zp_dev;       /* [B, row_capacity, 4] */
+  rtkv_layer_stats* stats_dev;
+} rtkv_layer_out;
+
+/* ------------------------------------------------------------------------------------------------
+ * Library / sizing
+ * ---------------------------------------------------------------------------------------------- */
+const char* rtkv_version(void);
+const char* rtkv_last_error(void);
+
+/* Bits per packed element for a class of `bits` on `dtype`: bits, or bits+1 when the clamp bound
+ * qmax = 2^bits-1 is not representable in dtype (then PyTorch's clamp rounds it up to 2^bits and a
+ * code can equal 2^bits; dynamic_quantization.py:121).  0 if unsupported (bits outside 1..16, or
+ * fp16 with bits = 16, which the reference rejects). */
+int rtkv_field_width(int dtype, int bits);
+
+/* Scratch bytes needed by the entry points below for B batch rows of S tokens. */
+size_t rtkv_workspace_size(int64_t B, int64_t S);
+
+/* Upper bound of packed bytes per tensor for B*S rows of F elements at the widest class. */
+int64_t rtkv_packed_capacity(int64_t B, int64_t S, int64_t F, int dtype, const int32_t bits[3]);
+
+/* ------------------------------------------------------------------------------------------------
+ * Stage entry points (each replaces one reference method; used by the Python mirror classes)
+ * ---------------------------------------------------------------------------------------------- */
+
+/* A[b,i] = Σ_{p<P} mean_h W[b,h,i,p], rounded to W's dtype and stored as fp32.
+ * Replaces PromptGuidedImportanceScorer.compute_attention_aggregation (token_importance.py:21-47).
+ * The summation order reproduces PyTorch's CPU cascade sum (AVX2 kernels), so results are
+ * bit-identical to the reference's CPU path. */
+int rtkv_attention_aggregation(const rtkv_attn_desc* w, int32_t prompt_len, float* A_dev,
+                               void* workspace_dev, size_t workspace_bytes, void* stream);
+
+/* Per-row min-max normalisation of x[B,S] (dtype), output in the same dtype.
+ * Replaces PromptGuidedImportanceScorer.normalize_attention_scores (token_importance.py:49-85). */
+int rtkv_minmax_normalize(const void* x_dev, int dtype, int64_t B, int64_t S, void* out_dev,
+                          void* stream);
+
+/* pos[i] = log(i+1)/log(S) in fp32 (0 if S <= 1), bit-identical to torch.log on CPU.
+ * Replaces PromptGuidedImportanceScorer.compute_position_bias (token_importance.py:87-110). */
+int rtkv_position_bias(int64_t S, float* pos_dev, void* stream);
+
+/* scores[b,i] from A (values rounded to a_dtype): α·N·w_l + β·pos + γ·min(1, P/S).
+ * Replaces compute_importance_scores given its aggregation (token_importance.py:134-176). */
+int rtkv_importance_scores(const float* A_dev, int a_dtype, int64_t B, int64_t S,
+                           const rtkv_layer_params* p, float* scores_dev,
+                           void* workspace_dev, size_t workspace_bytes, void* stream);
+
+/* labels[b,i] ∈ {0,1,2} from thresholds; per-class counts into stats (class_count).
+ * Replaces DynamicPrecisionQuantizer.assign_precision_levels (dynamic_quantization.py:21-60). */
+int rtkv_assign_precision(const float* scores_dev, int64_t B, int64_t S, const rtkv_layer_params* p,
+                          uint8_t* labels_dev, rtkv_layer_stats* stats_dev,
+                          void* workspace_dev, size_t workspace_bytes, void* stream);
+
+/* Budgeted greedy selection + emergency fallback + ordered compaction map.
+ * Replaces SelectiveTokenPropagator.select_tokens_with_budget (selective_propagation.py:68-161) and
+ * the selection half of apply_token_selection (:163-211).  Tie order among equal scores is
+ * (score desc, index asc). */
+int rtkv_select_tokens(const float* scores_dev, const uint8_t* labels_dev, int64_t B, int64_t S,
+                       const rtkv_layer_params* p, uint8_t* mask_dev, int32_t* kept_index_dev,
+                       int64_t row_capacity, int64_t* row_offset_dev, int64_t F, int kv_dtype,
+                       rtkv_layer_stats* stats_dev, void* workspace_dev, size_t workspace_bytes,
+                       void* stream);
+
+/* Quantize/dequantize/pack the rows listed in kept_index (or every token when kept_index_dev is
+ * NULL: output row r = token r), with per-row class from labels.  Row count per batch row is read
+ * from stats_dev->batch[b].kept (or S when kept_index_dev is NULL).
+ * Replaces DynamicPrecisionQuantizer.apply_mixed_precision_quantization
+ * (dynamic_quantization.py:128-196) fused with the gather of apply_token_selection (:214-232). */
+int rtkv_quantize_rows(const rtkv_kv_desc* kv, const uint8_t* labels_dev,
+                       const int32_t* kept_index_dev, const rtkv_layer_params* p,
+                       const rtkv_layer_out* out, void* stream);
+
+/* Fused driver: aggregation → scores → labels → selection → quantize+pack+compact for one layer.
+ * Replaces RealTimePrefillCompressor.compress_layer_kv_cache (unified_compressor.py:95-172).
+ * Three kernel launches, no host synchronisation; read out->stats_dev after the stream syncs. */
+int rtkv_compress_layer(const rtkv_kv_desc* kv, const rtkv_attn_desc* w, const rtkv_layer_params* p,
+                        const rtkv_layer_out* out, void* workspace_dev, size_t workspace_bytes,
+                        void* stream);
+
+/* Reconstruct dequantized rows from packed codes (+ scale/zp, labels of the kept rows); bit-identical
+ * to the RTKV_EMIT_DEQUANT output.  rows_per_batch[b] rows of batch row b are decoded.
+ * Consumer side of the packed format (compression_layers.py:7-45 CompressedKVCache). */
+int rtkv_unpack_dequant(const uint8_t* packed_dev, const int64_t* row_offset_dev,
+                        const float* scale_zp_dev, int which /*0=K,1=V*/,
+                        const int32_t* kept_index_dev, const uint8_t* labels_dev /*[B,S]*/,
+                        int64_t B, int64_t S, int64_t row_capacity, const int64_t* rows_dev,
+                        int64_t H, int64_t D, int dtype, const int32_t bits[3], void* out_dev,
+                        int64_t o_stride_b, int64_t o_stride_s, int64_t o_stride_h, void* stream);
+
+/* Whole-tensor helpers (single scale/zero-point over n elements):
+ *   rtkv_tensor_quant_params: DynamicPrecisionQuantizer.get_quantization_params
+ *     (dynamic_quantization.py:62-95) → scale_zp_dev[0..1] (fp32 storage of dtype values);
+ *   rtkv_tensor_fake_quant: DynamicPrecisionQuantizer.quantize_tensor (:97-126) with that pair.
+ * Optional element mask (uint8, NULL = all) selects the elements that take part and get written
+ * (compression_layers.py:150-175 AdaptiveQuantization.forward applies one pair per class). */
+int rtkv_tensor_quant_params(const void* x_dev, int dtype, int64_t n, const uint8_t* mask_dev,
+                             int32_t mask_value, int bits, float* scale_zp_dev, void* workspace_dev,
+                             size_t workspace_bytes, void* stream);
+int rtkv_tensor_fake_quant(const void* x_dev, int dtype, int64_t n, const uint8_t* mask_dev,
+                           int32_t mask_value, int bits, const float* scale_zp_dev, void* out_dev,
+                           void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* RTKV_H */
