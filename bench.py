@@ -1,0 +1,264 @@
+#!/usr/bin/env python3
+"""Benchmark of the MI355X streaming prefill KV-cache compression path.
+
+Metric (BASELINE.json): prefill KV-compress GB/s + TTFT, Llama-2-7B, S = 16k, 1 GPU.
+
+One *step* = the compression of all 32 layers of one prefill (BASELINE config 3: B=1, S=16384,
+32 heads × 128, fp16 K/V, prompt P=128, full importance → quantization → selective propagation)
+through the C ABI's fused driver (rtkv_compress_layer: 3 kernels per layer, no host sync inside
+the step).  Inputs are synthetic (seeded, resident in HBM before timing).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+
+N > 1 (launched by torch.distributed.run): sequence-chunk sharding with weak scaling (every rank
+owns S tokens of an N·S-token prefill; RCCL all-gather of per-token attention mass, global
+selection on every rank, local quantization, RCCL all-gather of the packed KV).
+
+Rank 0 prints ONE JSON line.  ``value`` = algorithmic bytes of the whole job ÷ wall time (GB/s);
+``ttft_ms`` = Σ per-layer compress time (the reference's TTFT, longbench_eval.py:160);
+``roofline`` = the dominant kernel (K4 quantize+pack+compact) timed with HIP events inside this
+run; ``cpu_baseline`` = the C oracle (single-thread restatement of the reference) on a bounded
+sample of the same workload.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(REPO, "realtime-kv-cache-compression_amd"))
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--layers", type=int, default=32)
+    ap.add_argument("--seq", type=int, default=16384, help="tokens per rank")
+    ap.add_argument("--heads", type=int, default=32)
+    ap.add_argument("--head-dim", type=int, default=128)
+    ap.add_argument("--dtype", default="float16", choices=["float16", "bfloat16", "float32"])
+    ap.add_argument("--no-packed", action="store_true", help="skip the packed-code output")
+    ap.add_argument("--cpu-baseline-layers", type=int, default=2, help="layers of the oracle sample (0 = skip)")
+    ap.add_argument("--quiet", action="store_true")
+    return ap.parse_args()
+
+
+def synth_layer(l: int, S: int, H: int, D: int, P: int, dtype, device, gen):
+    """K, V [1,S,H*D] ~ N(0,1); W prompt slice [1,H,S,P] = u^4 row-normalised × U(0,1), causal in
+    the prompt."""
+    F = H * D
+    K = torch.randn(1, S, F, generator=gen, device=device, dtype=torch.float32).to(dtype)
+    V = torch.randn(1, S, F, generator=gen, device=device, dtype=torch.float32).to(dtype)
+    u = torch.rand(1, H, S, P, generator=gen, device=device, dtype=torch.float32)
+    raw = (u * u) ** 2 + 1e-6
+    causal = torch.arange(P, device=device)[None, :] <= torch.arange(S, device=device)[:, None]
+    raw = raw * causal
+    W = raw / raw.sum(-1, keepdim=True) * torch.rand(1, H, S, 1, generator=gen, device=device)
+    return K, V, W.to(dtype)
+
+
+class Job:
+    """Per-rank state: inputs and outputs of every layer, resident in HBM."""
+
+    def __init__(self, args, device, rank, world):
+        import rtkv
+        from rtkv import _lib as L
+        self.args, self.device, self.rank, self.world = args, device, rank, world
+        self.dtype = getattr(torch, args.dtype)
+        self.S, self.H, self.D = args.seq, args.heads, args.head_dim
+        self.F = self.H * self.D
+        self.S_total = self.S * world
+        self.P = rtkv.prompt_length(self.S_total)
+        self.cfg = rtkv.CompressionConfig(alpha=0.8, beta=0.1, gamma=0.1, theta_h=0.4, theta_m=0.25,
+                                          high_precision_bits=8, medium_precision_bits=4, low_precision_bits=2,
+                                          early_layer_ratio=0.8, middle_layer_ratio=0.6, later_layer_ratio=0.4,
+                                          num_hidden_layers=args.layers)
+        self.bits = (2, 4, 8)
+        self.emit_packed = not args.no_packed
+        flags = L.EMIT_DEQUANT | (0 if args.no_packed else L.EMIT_PACKED)
+        prop = rtkv.SelectiveTokenPropagator(self.cfg)
+        gen = torch.Generator(device=device)
+        gen.manual_seed(1234 + 7919 * rank)
+        self.inputs, self.bufs, self.params = [], [], []
+        for l in range(args.layers):
+            self.inputs.append(synth_layer(l, self.S, self.H, self.D, self.P, self.dtype, device, gen))
+            self.bufs.append(rtkv.LayerBuffers(1, self.S, self.F, self.dtype, device, self.bits,
+                                               emit_dequant=True, emit_packed=self.emit_packed))
+            self.params.append(rtkv.params_from_config(self.cfg, l, self.P, prop.get_layer_propagation_ratio(l), flags))
+        self.ws = rtkv.Workspace(device)
+        self.ws.get(1, self.S)
+        torch.cuda.synchronize(device)
+
+    def step(self, events=None):
+        """Compress every layer (single GPU); events: list of 4-tuples of raw hipEvent_t or None."""
+        import rtkv
+        from rtkv import _lib as L
+        import ctypes
+        for l in range(self.args.layers):
+            K, V, W = self.inputs[l]
+            if events is None:
+                rtkv.compress_layer(K, V, W, self.params[l], self.bufs[l], self.ws)
+            else:
+                kd, wd = rtkv.engine.kv_desc(K, V), rtkv.engine.attn_desc(W)
+                out = self.bufs[l].out_struct()
+                ev = (ctypes.c_void_p * 4)(*[e.cuda_event for e in events[l]])
+                L.check(L.lib().rtkv_compress_layer_events(ctypes.byref(kd), ctypes.byref(wd),
+                                                           ctypes.byref(self.params[l]), ctypes.byref(out),
+                                                           self.ws.buf.data_ptr(), self.ws.buf.numel(),
+                                                           L.stream_ptr(self.device), ev), "compress_layer_events")
+
+    def layer_bytes(self):
+        """Algorithmic HBM bytes per layer: total and the K4 (quantize+pack+compact) part."""
+        from rtkv.engine import decode_stats
+        e = torch.tensor([], dtype=self.dtype).element_size()
+        tot, k4 = [], []
+        for l in range(self.args.layers):
+            st = decode_stats(self.bufs[l].stats.cpu().numpy().tobytes(), 1)
+            Sp, pk = st.max_kept, st.total_packed_bytes
+            w_read = self.H * self.S * self.P * e               # prompt columns of W
+            kv_read = 2 * Sp * self.F * e                        # kept rows of K and V, read once
+            deq = 2 * Sp * self.F * e                            # dequantized K', V'
+            packed = (2 * pk + Sp * 16) if self.emit_packed else 0   # codes + scale/zp
+            meta = self.S * (4 + 4 + 4 + 1 + 1) + Sp * (4 + 8 + 1)   # A, scores, labels, mask / index, offset
+            k4.append(kv_read + deq + packed + Sp * (4 + 8 + 1))
+            tot.append(w_read + kv_read + deq + packed + meta)
+        return tot, k4
+
+
+def cpu_baseline(args, job):
+    """The C oracle (single thread, a literal restatement of the reference) on a bounded sample:
+    the first `cpu_baseline_layers` layers of the same workload, same inputs."""
+    if args.cpu_baseline_layers <= 0:
+        return None
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import numpy as np
+    import rtkv_oracle as orc
+    code = {torch.float32: 0, torch.float16: 1, torch.bfloat16: 2}[job.dtype]
+    n = min(args.cpu_baseline_layers, args.layers)
+    nbytes, secs = 0.0, 0.0
+    tot, _ = job.layer_bytes()
+    for l in range(n):
+        K, V, W = job.inputs[l]
+        as_np = (lambda t: t.cpu().numpy()) if job.dtype == torch.float32 else \
+            (lambda t: t.cpu().view(torch.int16).numpy().view(np.uint16))
+        Kn, Vn, Wn = as_np(K), as_np(V), as_np(W)
+        p = job.params[l]
+        t0 = time.perf_counter()
+        orc.compress_layer(Kn, Vn, code, Wn, code, job.P, p.alpha, p.beta, p.gamma, p.layer_weight, p.theta_h,
+                           p.theta_m, job.bits, p.propagation_ratio, packed=job.emit_packed)
+        secs += time.perf_counter() - t0
+        nbytes += tot[l]
+    return {"value": round(nbytes / secs / 1e9, 4), "unit": "GB/s", "cores": 1, "kind": "port",
+            "ms_per_layer": round(secs / n * 1e3, 1),
+            "sample": f"{n} of {args.layers} layers (S={job.S}, {job.H}x{job.D}, {args.dtype}), C oracle "
+                      f"oracle/rtkv_oracle.c single-threaded on the host"}
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.gpus != world and world > 1:
+        print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
+    torch.cuda.set_device(local)
+    device = torch.device("cuda", local)
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=device)
+        from rtkv.sharded import ShardedJob
+        job = ShardedJob(args, device, rank, world, Job)
+    else:
+        dist = None
+        job = Job(args, device, rank, world)
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+        torch.cuda.synchronize(device)
+
+    for _ in range(args.warmup):
+        job.step()
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        job.step()
+    barrier()
+    elapsed = time.perf_counter() - t0
+    if dist is not None:
+        t = torch.tensor([elapsed], device=device, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    ms_per_step = elapsed / args.steps * 1e3
+
+    # per-kernel timing of the fused path (HIP events on the launch stream), outside the timed loop
+    events = [[torch.cuda.Event(enable_timing=True) for _ in range(4)] for _ in range(args.layers)]
+    for evs in events:
+        for e in evs:
+            e.record()  # materialise the hipEvent_t
+    torch.cuda.synchronize(device)
+    reps = 3
+    k_ms = [0.0, 0.0, 0.0]
+    for _ in range(reps):
+        job.step(events=events) if world == 1 else job.step()
+        torch.cuda.synchronize(device)
+        if world == 1:
+            for evs in events:
+                for k in range(3):
+                    k_ms[k] += evs[k].elapsed_time(evs[k + 1])
+    tot_bytes, k4_bytes = job.layer_bytes()
+    step_bytes = sum(tot_bytes)
+    if dist is not None:
+        b = torch.tensor([float(step_bytes)], device=device, dtype=torch.float64)
+        dist.all_reduce(b)
+        step_bytes = float(b.item())
+    value = step_bytes / (ms_per_step / 1e3) / 1e9
+
+    if rank == 0:
+        line = {
+            "metric": "prefill KV-compress GB/s + TTFT, Llama-2-7B S=16k, 1 GPU",
+            "value": round(value, 2),
+            "unit": "GB/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms_per_step, 4),
+            "ttft_ms": round(ms_per_step, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": {"float16": "f16", "bfloat16": "bf16", "float32": "f32"}[args.dtype],
+            "data": "synthetic (seeded torch RNG; K,V ~ N(0,1), W = causal u^4-softmax-like prompt slice)",
+            "config": {"workload": f"Llama-2-7B prefill KV compression, {args.layers} layers, "
+                                   f"S={job.S * world} ({job.S}/rank), {args.heads}x{args.head_dim}, "
+                                   f"P={job.P}, bits 8/4/2, ratios .8/.6/.4, dequant+packed outputs",
+                       "model": "Llama-2-7B (KV shapes only)", "global_batch": 1, "seq_len": job.S * world,
+                       "parallelism": f"sequence-shard x{world}" if world > 1 else "single GPU"},
+        }
+        if world == 1:
+            per_launch_ms = k_ms[2] / (reps * args.layers)
+            achieved = sum(k4_bytes) / args.layers / (per_launch_ms / 1e3) / 1e9
+            line["roofline"] = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+                                "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                                "kernel": "quant_rows_kernel (K4)", "avg_launch_us": round(per_launch_ms * 1e3, 2)}
+            line["kernel_us_per_layer"] = {"K1_aggregation": round(k_ms[0] / (reps * args.layers) * 1e3, 2),
+                                           "K2_finalize": round(k_ms[1] / (reps * args.layers) * 1e3, 2),
+                                           "K4_quant_pack": round(per_launch_ms * 1e3, 2)}
+            line["cpu_baseline"] = cpu_baseline(args, job)
+        print(json.dumps(line), flush=True)
+    if dist is not None:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

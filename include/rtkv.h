@@ -57,7 +57,8 @@ enum rtkv_error_flag {
 enum rtkv_layer_flag {
   RTKV_EMIT_DEQUANT = 1,   /* write the dequantized K'/V' (the reference's return value) */
   RTKV_EMIT_PACKED = 2,    /* write bit-packed integer codes + per-row scale/zero-point */
-  RTKV_NO_SELECTION = 4    /* keep every token (quantization only, BASELINE config 2) */
+  RTKV_NO_SELECTION = 4,   /* keep every token (quantization only, BASELINE config 2) */
+  RTKV_NO_FALLBACK = 8     /* skip the top-10% emergency fallback (select_tokens_with_budget alone) */
 };
 
 /* ------------------------------------------------------------------------------------------------
@@ -144,7 +145,10 @@ static inline size_t rtkv_stats_bytes(int64_t B) {
  * scale_zp[(b*row_capacity + r)*4 + {0,1,2,3}] = {k_scale, k_zero_point, v_scale, v_zero_point}
  * (values exactly representable in the K/V dtype, stored as fp32). */
 typedef struct rtkv_layer_out {
-  void* k_out_dev;           /* dequantized K' in the K/V dtype, [B, row_capacity, H, D] via strides */
+  /* dequantized K' in the K/V dtype, [B, rows, H, D] via strides.  o_stride_b = -1 packs batch rows
+   * back to back at the RUNTIME row count: batch stride = S'_max * o_stride_s, so a contiguous
+   * [B, S'_max, H*D] result needs no host round trip before the launch. */
+  void* k_out_dev;
   void* v_out_dev;
   int64_t o_stride_b, o_stride_s, o_stride_h;
   int64_t row_capacity;      /* rows available per batch row (>= S'_max; S is always enough) */
@@ -236,6 +240,14 @@ int rtkv_compress_layer(const rtkv_kv_desc* kv, const rtkv_attn_desc* w, const r
                         const rtkv_layer_out* out, void* workspace_dev, size_t workspace_bytes,
                         void* stream);
 
+/* rtkv_compress_layer that also records hipEvent_t events[0..3] on `stream` before K1, after K1
+ * (aggregation), after K2 (scores/classes/selection) and after K4 (quantize+pack+compact), so a
+ * caller can time each kernel of the fused path without changing it (bench.py's roofline). */
+int rtkv_compress_layer_events(const rtkv_kv_desc* kv, const rtkv_attn_desc* w,
+                               const rtkv_layer_params* p, const rtkv_layer_out* out,
+                               void* workspace_dev, size_t workspace_bytes, void* stream,
+                               void* const events[4]);
+
 /* Reconstruct dequantized rows from packed codes (+ scale/zp, labels of the kept rows); bit-identical
  * to the RTKV_EMIT_DEQUANT output.  rows_per_batch[b] rows of batch row b are decoded.
  * Consumer side of the packed format (compression_layers.py:7-45 CompressedKVCache). */
@@ -246,18 +258,32 @@ int rtkv_unpack_dequant(const uint8_t* packed_dev, const int64_t* row_offset_dev
                         int64_t H, int64_t D, int dtype, const int32_t bits[3], void* out_dev,
                         int64_t o_stride_b, int64_t o_stride_s, int64_t o_stride_h, void* stream);
 
-/* Whole-tensor helpers (single scale/zero-point over n elements):
+/* Copy the kept rows of a row-major tensor (row r of batch b = src row kept_index[b*cap + r]), zero
+ * rows for r in [kept_b, S'_max), rows of row_bytes bytes, into dst (batch stride dst_stride_b bytes,
+ * or S'_max*row_bytes when -1).  The pure gather of apply_token_selection (selective_propagation.py
+ * :224-232) for tensors the caller did not quantize (K/V, scores, labels). */
+int rtkv_gather_rows(const void* src_dev, int64_t B, int64_t S, int64_t row_bytes,
+                     const int32_t* kept_index_dev, int64_t row_capacity, int64_t src_stride_b,
+                     void* dst_dev, int64_t dst_stride_b, int64_t src_stride_s,
+                     const rtkv_layer_stats* stats_dev, void* stream);
+
+/* Whole-tensor helpers (one scale/zero-point over all elements of the selected rows of an
+ * [n_rows, row_len] tensor; row_labels_dev = NULL selects every row, otherwise the rows whose
+ * label equals label_value):
  *   rtkv_tensor_quant_params: DynamicPrecisionQuantizer.get_quantization_params
  *     (dynamic_quantization.py:62-95) → scale_zp_dev[0..1] (fp32 storage of dtype values);
- *   rtkv_tensor_fake_quant: DynamicPrecisionQuantizer.quantize_tensor (:97-126) with that pair.
- * Optional element mask (uint8, NULL = all) selects the elements that take part and get written
- * (compression_layers.py:150-175 AdaptiveQuantization.forward applies one pair per class). */
-int rtkv_tensor_quant_params(const void* x_dev, int dtype, int64_t n, const uint8_t* mask_dev,
-                             int32_t mask_value, int bits, float* scale_zp_dev, void* workspace_dev,
-                             size_t workspace_bytes, void* stream);
-int rtkv_tensor_fake_quant(const void* x_dev, int dtype, int64_t n, const uint8_t* mask_dev,
-                           int32_t mask_value, int bits, const float* scale_zp_dev, void* out_dev,
-                           void* stream);
+ *     workspace >= 8 KiB;
+ *   rtkv_tensor_fake_quant: DynamicPrecisionQuantizer.quantize_tensor (:97-126) with that pair,
+ *     writing only the selected rows of out_dev.
+ * AdaptiveQuantization.forward (compression_layers.py:150-175) is one params + fake_quant pair per
+ * precision class. */
+int rtkv_tensor_quant_params(const void* x_dev, int dtype, int64_t n_rows, int64_t row_len,
+                             const uint8_t* row_labels_dev, int32_t label_value, int bits,
+                             float* scale_zp_dev, void* workspace_dev, size_t workspace_bytes,
+                             void* stream);
+int rtkv_tensor_fake_quant(const void* x_dev, int dtype, int64_t n_rows, int64_t row_len,
+                           const uint8_t* row_labels_dev, int32_t label_value, int bits,
+                           const float* scale_zp_dev, void* out_dev, void* stream);
 
 #ifdef __cplusplus
 }

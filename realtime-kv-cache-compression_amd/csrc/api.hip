@@ -1,0 +1,272 @@
+// api.hip — the C ABI of include/rtkv.h: argument validation, workspace carving, host-side scalar
+// preparation (the Python-float → fp32 casts the reference performs) and stream-ordered launches.
+#include <cmath>
+#include <cstring>
+#include <string>
+
+#include "common.h"
+
+namespace rtkv {
+
+static thread_local std::string g_last_error;
+void set_error(const std::string& msg) { g_last_error = msg; }
+
+static inline size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
+
+// Workspace layout: [A: B*S fp32][labels scratch: B*S u8][stats scratch][tensor partials: 8 KiB]
+struct Workspace {
+  float* A;
+  uint8_t* labels;
+  rtkv_layer_stats* stats;
+  float* partial;
+};
+static size_t ws_bytes(int64_t B, int64_t S) {
+  return align_up((size_t)(B * S) * 4, 256) + align_up((size_t)(B * S), 256) + align_up(rtkv_stats_bytes(B), 256) +
+         8192;
+}
+static int carve(void* ws, size_t bytes, int64_t B, int64_t S, Workspace& w) {
+  if (!ws || bytes < ws_bytes(B, S)) {
+    set_error("rtkv: workspace too small (need rtkv_workspace_size(B, S) bytes)");
+    return RTKV_ERR_WORKSPACE;
+  }
+  char* p = static_cast<char*>(ws);
+  w.A = reinterpret_cast<float*>(p);
+  p += align_up((size_t)(B * S) * 4, 256);
+  w.labels = reinterpret_cast<uint8_t*>(p);
+  p += align_up((size_t)(B * S), 256);
+  w.stats = reinterpret_cast<rtkv_layer_stats*>(p);
+  p += align_up(rtkv_stats_bytes(B), 256);
+  w.partial = reinterpret_cast<float*>(p);
+  return RTKV_OK;
+}
+
+static int check_params(const rtkv_layer_params* p) {
+  RTKV_REQUIRE(p != nullptr, "null params");
+  for (int g = 0; g < 3; ++g) RTKV_REQUIRE(p->bits[g] >= 1 && p->bits[g] <= 16, "bits must be in [1, 16]");
+  return RTKV_OK;
+}
+
+static FinalizeArgs finalize_args(const rtkv_layer_params* p, int64_t B, int64_t S) {
+  FinalizeArgs a;
+  std::memset(&a, 0, sizeof(a));
+  a.p = *p;
+  a.B = B;
+  a.S = S;
+  a.kv_dtype = -1;
+  a.a_dtype = RTKV_F32;
+  // compute_position_bias divides by math.log(seq_len) (a C double log), cast to fp32 against the
+  // fp32 tensor; compute_context_relevance is torch.full((S,), min(1.0, P/S)) in fp32.
+  a.logS = (float)std::log((double)S);
+  const double rel = (double)p->prompt_len / (double)S;
+  a.ctx = (float)(rel < 1.0 ? rel : 1.0);
+  return a;
+}
+
+}  // namespace rtkv
+
+using namespace rtkv;
+
+extern "C" {
+
+const char* rtkv_version(void) { return "rtkv 0.1.0 (gfx950, HIP)"; }
+const char* rtkv_last_error(void) { return g_last_error.c_str(); }
+int rtkv_field_width(int dtype, int bits) { return field_width(dtype, bits); }
+size_t rtkv_workspace_size(int64_t B, int64_t S) { return ws_bytes(B, S); }
+
+int64_t rtkv_packed_capacity(int64_t B, int64_t S, int64_t F, int dtype, const int32_t bits[3]) {
+  int w = 0;
+  for (int g = 0; g < 3; ++g) {
+    const int fw = field_width(dtype, bits[g]);
+    if (fw > w) w = fw;
+  }
+  return B * S * ((F * w + 7) / 8);
+}
+
+int rtkv_attention_aggregation(const rtkv_attn_desc* w, int32_t prompt_len, float* A_dev, void* workspace_dev,
+                               size_t workspace_bytes, void* stream) {
+  (void)workspace_dev;
+  (void)workspace_bytes;
+  RTKV_REQUIRE(w != nullptr, "null attention descriptor");
+  return launch_aggregation(*w, prompt_len, A_dev, (hipStream_t)stream);
+}
+
+int rtkv_minmax_normalize(const void* x_dev, int dtype, int64_t B, int64_t S, void* out_dev, void* stream) {
+  return launch_minmax_normalize(x_dev, dtype, B, S, out_dev, (hipStream_t)stream);
+}
+
+int rtkv_position_bias(int64_t S, float* pos_dev, void* stream) {
+  return launch_position_bias(S, pos_dev, (hipStream_t)stream);
+}
+
+int rtkv_importance_scores(const float* A_dev, int a_dtype, int64_t B, int64_t S, const rtkv_layer_params* p,
+                           float* scores_dev, void* workspace_dev, size_t workspace_bytes, void* stream) {
+  RTKV_REQUIRE(p != nullptr, "null params");
+  RTKV_REQUIRE(B >= 1 && S >= 1, "empty shape");
+  Workspace ws;
+  int rc = carve(workspace_dev, workspace_bytes, B, S, ws);
+  if (rc) return rc;
+  FinalizeArgs a = finalize_args(p, B, S);
+  a.A = A_dev;
+  a.a_dtype = a_dtype;
+  a.scores = scores_dev;
+  a.labels = ws.labels;
+  a.stats = ws.stats;
+  a.mode_scores = 1;
+  a.mode_labels = 1;
+  a.mode_select = 0;
+  return launch_finalize(a, (hipStream_t)stream);
+}
+
+int rtkv_assign_precision(const float* scores_dev, int64_t B, int64_t S, const rtkv_layer_params* p,
+                          uint8_t* labels_dev, rtkv_layer_stats* stats_dev, void* workspace_dev,
+                          size_t workspace_bytes, void* stream) {
+  RTKV_REQUIRE(p != nullptr && labels_dev && stats_dev, "null argument");
+  RTKV_REQUIRE(B >= 1 && S >= 1, "empty shape");
+  (void)workspace_dev;
+  (void)workspace_bytes;
+  FinalizeArgs a = finalize_args(p, B, S);
+  a.scores = const_cast<float*>(scores_dev);
+  a.labels = labels_dev;
+  a.stats = stats_dev;
+  a.mode_scores = 0;
+  a.mode_labels = 1;
+  a.mode_select = 0;
+  return launch_finalize(a, (hipStream_t)stream);
+}
+
+int rtkv_select_tokens(const float* scores_dev, const uint8_t* labels_dev, int64_t B, int64_t S,
+                       const rtkv_layer_params* p, uint8_t* mask_dev, int32_t* kept_index_dev, int64_t row_capacity,
+                       int64_t* row_offset_dev, int64_t F, int kv_dtype, rtkv_layer_stats* stats_dev,
+                       void* workspace_dev, size_t workspace_bytes, void* stream) {
+  int rc = check_params(p);
+  if (rc) return rc;
+  RTKV_REQUIRE(scores_dev && labels_dev && mask_dev && stats_dev, "null argument");
+  RTKV_REQUIRE(B >= 1 && S >= 1, "empty shape");
+  RTKV_REQUIRE(!kept_index_dev || row_capacity >= 1, "row_capacity must be >= 1");
+  (void)workspace_dev;
+  (void)workspace_bytes;
+  FinalizeArgs a = finalize_args(p, B, S);
+  a.scores = const_cast<float*>(scores_dev);
+  a.labels = const_cast<uint8_t*>(labels_dev);
+  a.mask = mask_dev;
+  a.kept_index = kept_index_dev;
+  a.row_offset = row_offset_dev;
+  a.row_capacity = kept_index_dev ? row_capacity : 0;
+  a.F = F;
+  a.kv_dtype = kv_dtype;
+  a.stats = stats_dev;
+  a.mode_scores = 0;
+  a.mode_labels = 0;
+  a.mode_select = (p->flags & RTKV_NO_SELECTION) ? 2 : 1;
+  return launch_finalize(a, (hipStream_t)stream);
+}
+
+int rtkv_quantize_rows(const rtkv_kv_desc* kv, const uint8_t* labels_dev, const int32_t* kept_index_dev,
+                       const rtkv_layer_params* p, const rtkv_layer_out* out, void* stream) {
+  int rc = check_params(p);
+  if (rc) return rc;
+  RTKV_REQUIRE(kv && out, "null descriptor");
+  QuantArgs q;
+  std::memset(&q, 0, sizeof(q));
+  q.kv = *kv;
+  q.labels = labels_dev;
+  q.kept_index = kept_index_dev;
+  q.stats = out->stats_dev;
+  for (int g = 0; g < 3; ++g) q.bits[g] = p->bits[g];
+  q.out = *out;
+  if (!(p->flags & RTKV_EMIT_DEQUANT)) { q.out.k_out_dev = nullptr; q.out.v_out_dev = nullptr; }
+  if (!(p->flags & RTKV_EMIT_PACKED)) { q.out.packed_k_dev = nullptr; q.out.packed_v_dev = nullptr; }
+  return launch_quant(q, (hipStream_t)stream);
+}
+
+int rtkv_compress_layer_events(const rtkv_kv_desc* kv, const rtkv_attn_desc* w, const rtkv_layer_params* p,
+                               const rtkv_layer_out* out, void* workspace_dev, size_t workspace_bytes, void* stream,
+                               void* const events[4]) {
+  int rc = check_params(p);
+  if (rc) return rc;
+  RTKV_REQUIRE(kv && w && out, "null descriptor");
+  RTKV_REQUIRE(kv->B == w->B && kv->S == w->S, "K/V and attention weights disagree on B or S");
+  RTKV_REQUIRE(out->scores_dev && out->labels_dev && out->mask_dev && out->kept_index_dev && out->stats_dev,
+               "compress_layer needs scores, labels, mask, kept_index and stats outputs");
+  RTKV_REQUIRE(out->row_capacity >= kv->S, "row_capacity must be >= S (every token may be kept)");
+  if (p->flags & RTKV_EMIT_PACKED) {
+    RTKV_REQUIRE(out->packed_k_dev && out->packed_v_dev && out->row_offset_dev && out->scale_zp_dev,
+                 "EMIT_PACKED needs packed_k, packed_v, row_offset and scale_zp outputs");
+    for (int g = 0; g < 3; ++g)
+      RTKV_REQUIRE(field_width(kv->dtype, p->bits[g]) > 0, "packed codes unsupported for this dtype/bits");
+    RTKV_REQUIRE(out->packed_capacity >= rtkv_packed_capacity(kv->B, out->row_capacity < kv->S ? out->row_capacity : kv->S,
+                                                             kv->H * kv->D, kv->dtype, p->bits),
+                 "packed_capacity too small");
+  }
+  if (p->flags & RTKV_EMIT_DEQUANT) RTKV_REQUIRE(out->k_out_dev && out->v_out_dev, "EMIT_DEQUANT needs k_out and v_out");
+  Workspace ws;
+  rc = carve(workspace_dev, workspace_bytes, kv->B, kv->S, ws);
+  if (rc) return rc;
+  hipStream_t st = (hipStream_t)stream;
+  auto mark = [&](int k) -> int {
+    if (events && events[k]) RTKV_HIP_CHECK(hipEventRecord((hipEvent_t)events[k], st));
+    return RTKV_OK;
+  };
+  if ((rc = mark(0))) return rc;
+  rc = launch_aggregation(*w, p->prompt_len, ws.A, st);
+  if (rc) return rc;
+  if ((rc = mark(1))) return rc;
+  FinalizeArgs a = finalize_args(p, kv->B, kv->S);
+  a.A = ws.A;
+  a.a_dtype = w->dtype;
+  a.scores = out->scores_dev;
+  a.labels = out->labels_dev;
+  a.mask = out->mask_dev;
+  a.kept_index = out->kept_index_dev;
+  a.row_offset = out->row_offset_dev;
+  a.row_capacity = out->row_capacity;
+  a.F = kv->H * kv->D;
+  a.kv_dtype = kv->dtype;
+  a.stats = out->stats_dev;
+  a.mode_scores = 1;
+  a.mode_labels = 1;
+  a.mode_select = (p->flags & RTKV_NO_SELECTION) ? 2 : 1;
+  rc = launch_finalize(a, st);
+  if (rc) return rc;
+  if ((rc = mark(2))) return rc;
+  rc = rtkv_quantize_rows(kv, out->labels_dev, out->kept_index_dev, p, out, stream);
+  if (rc) return rc;
+  return mark(3);
+}
+
+int rtkv_compress_layer(const rtkv_kv_desc* kv, const rtkv_attn_desc* w, const rtkv_layer_params* p,
+                        const rtkv_layer_out* out, void* workspace_dev, size_t workspace_bytes, void* stream) {
+  return rtkv_compress_layer_events(kv, w, p, out, workspace_dev, workspace_bytes, stream, nullptr);
+}
+
+int rtkv_unpack_dequant(const uint8_t* packed_dev, const int64_t* row_offset_dev, const float* scale_zp_dev,
+                        int which, const int32_t* kept_index_dev, const uint8_t* labels_dev, int64_t B, int64_t S,
+                        int64_t row_capacity, const int64_t* rows_dev, int64_t H, int64_t D, int dtype,
+                        const int32_t bits[3], void* out_dev, int64_t o_stride_b, int64_t o_stride_s,
+                        int64_t o_stride_h, void* stream) {
+  RTKV_REQUIRE(bits != nullptr, "null bits");
+  return launch_unpack(packed_dev, row_offset_dev, scale_zp_dev, which, kept_index_dev, labels_dev, B, S, row_capacity,
+                       rows_dev, H, D, dtype, bits, out_dev, o_stride_b, o_stride_s, o_stride_h, (hipStream_t)stream);
+}
+
+int rtkv_gather_rows(const void* src_dev, int64_t B, int64_t S, int64_t row_bytes, const int32_t* kept_index_dev,
+                     int64_t row_capacity, int64_t src_stride_b, void* dst_dev, int64_t dst_stride_b, int64_t src_stride_s,
+                     const rtkv_layer_stats* stats_dev, void* stream) {
+  return launch_gather(src_dev, B, S, row_bytes, kept_index_dev, row_capacity, src_stride_b, dst_dev, dst_stride_b,
+                       src_stride_s, stats_dev, (hipStream_t)stream);
+}
+
+int rtkv_tensor_quant_params(const void* x_dev, int dtype, int64_t n_rows, int64_t row_len, const uint8_t* row_labels_dev,
+                             int32_t label_value, int bits, float* scale_zp_dev, void* workspace_dev,
+                             size_t workspace_bytes, void* stream) {
+  return launch_tensor_params(x_dev, dtype, n_rows, row_len, row_labels_dev, label_value, bits, scale_zp_dev,
+                              workspace_dev, workspace_bytes, (hipStream_t)stream);
+}
+
+int rtkv_tensor_fake_quant(const void* x_dev, int dtype, int64_t n_rows, int64_t row_len, const uint8_t* row_labels_dev,
+                           int32_t label_value, int bits, const float* scale_zp_dev, void* out_dev, void* stream) {
+  return launch_tensor_fake_quant(x_dev, dtype, n_rows, row_len, row_labels_dev, label_value, bits, scale_zp_dev,
+                                  out_dev, (hipStream_t)stream);
+}
+
+}  // extern "C"

@@ -1,0 +1,191 @@
+// common.h — device helpers shared by the rtkv kernels (gfx950 / CDNA4, wave64).
+//
+// Numerics contract (see include/rtkv.h): every elementwise op of the reference is an fp32 op
+// followed by a round-to-nearest-even into the tensor dtype; the library is compiled with
+// -ffp-contract=off and IEEE fp32 division so that the device ops equal PyTorch's CPU ops bit for bit.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <string>
+
+#include "rtkv.h"
+
+namespace rtkv {
+
+constexpr int kWave = 64;
+
+// ------------------------------------------------------------------------------------ dtypes
+template <int DT> struct Dt;
+
+template <> struct Dt<RTKV_F32> {
+  using S = float;                       // storage type
+  static constexpr int kBytes = 4;
+  static constexpr int kPrecision = 24;  // significand bits incl. the hidden bit
+  __device__ __forceinline__ static float load(S v) { return v; }
+  __device__ __forceinline__ static S store(float f) { return f; }
+  __device__ __forceinline__ static float rnd(float f) { return f; }
+};
+
+template <> struct Dt<RTKV_F16> {
+  using S = uint16_t;
+  static constexpr int kBytes = 2;
+  static constexpr int kPrecision = 11;
+  __device__ __forceinline__ static float load(S v) { return (float)__builtin_bit_cast(_Float16, v); }
+  __device__ __forceinline__ static S store(float f) { return __builtin_bit_cast(uint16_t, (_Float16)f); }
+  __device__ __forceinline__ static float rnd(float f) { return (float)(_Float16)f; }
+};
+
+template <> struct Dt<RTKV_BF16> {
+  using S = uint16_t;
+  static constexpr int kBytes = 2;
+  static constexpr int kPrecision = 8;
+  __device__ __forceinline__ static float load(S v) { return __builtin_bit_cast(float, (uint32_t)v << 16); }
+  __device__ __forceinline__ static S store(float f) {
+    uint32_t u = __builtin_bit_cast(uint32_t, f);
+    if ((u & 0x7fffffffu) > 0x7f800000u) return (S)((u >> 16) | 0x40u);
+    return (S)((u + 0x7fffu + ((u >> 16) & 1u)) >> 16);
+  }
+  __device__ __forceinline__ static float rnd(float f) { return load(store(f)); }
+};
+
+__device__ __forceinline__ float rnd_dt(int dt, float x) {
+  if (dt == RTKV_F16) return Dt<RTKV_F16>::rnd(x);
+  if (dt == RTKV_BF16) return Dt<RTKV_BF16>::rnd(x);
+  return x;
+}
+
+inline int dtype_bytes(int dt) { return dt == RTKV_F32 ? 4 : 2; }
+inline int dtype_precision(int dt) { return dt == RTKV_F16 ? 11 : (dt == RTKV_BF16 ? 8 : 24); }
+
+// Bits per packed element (include/rtkv.h rtkv_field_width).
+__host__ __device__ inline int field_width(int dt, int bits) {
+  if (bits < 1 || bits > 16) return 0;
+  if (dt == RTKV_F16 && bits >= 16) return 0;
+  const int prec = dt == RTKV_F16 ? 11 : (dt == RTKV_BF16 ? 8 : 24);
+  return bits > prec ? bits + 1 : bits;
+}
+
+// ------------------------------------------------------------------------------------ keys
+// Order-preserving uint32 key of an fp32 score (larger key = larger score; -0 folded onto +0 so
+// that equal scores compare equal, as in the reference's `>` comparator).
+__device__ __forceinline__ uint32_t score_key(float s) {
+  uint32_t u = __builtin_bit_cast(uint32_t, s);
+  if (u == 0x80000000u) u = 0u;
+  return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+
+// torch.log(float(n)) on the CPU = Sleef_logf8_u10: the correctly rounded logf except at these
+// integers (measured against torch 2.10; oracle/rtkv_oracle.c carries the same table).
+static __constant__ uint32_t kSleefN[14] = {73223, 109922, 127729, 183800, 212513, 415941, 495891,
+                                     639580, 691150, 717811, 753016, 920019, 941358, 942898};
+static __constant__ uint32_t kSleefBits[14] = {0x41333861u, 0x4139b86du, 0x413c1f67u, 0x4141f217u, 0x414444a4u,
+                                        0x414f0345u, 0x4151d367u, 0x4155e5a6u, 0x41572347u, 0x4157be4fu,
+                                        0x4158826du, 0x415bb6e2u, 0x415c14ceu, 0x415c1b80u};
+
+static __device__ __forceinline__ float torch_logf(uint32_t n) {
+  if (n >= 73223u) {
+#pragma unroll
+    for (int k = 0; k < 14; ++k)
+      if (kSleefN[k] == n) return __builtin_bit_cast(float, kSleefBits[k]);
+  }
+  return (float)log((double)n);
+}
+
+// ------------------------------------------------------------------------------------ waves
+template <typename T> __device__ __forceinline__ T wave_sum(T v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, kWave);
+  return v;
+}
+__device__ __forceinline__ float wave_min(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fminf(v, __shfl_xor(v, o, kWave));
+  return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, kWave));
+  return v;
+}
+
+// Inclusive prefix sum across the wave (Hillis-Steele over shuffles).
+template <typename T> __device__ __forceinline__ T wave_inclusive_scan(T v) {
+  const int lane = threadIdx.x & (kWave - 1);
+#pragma unroll
+  for (int o = 1; o < kWave; o <<= 1) {
+    T n = __shfl_up(v, o, kWave);
+    if (lane >= o) v += n;
+  }
+  return v;
+}
+
+// ------------------------------------------------------------------------------------ errors
+void set_error(const std::string& msg);
+
+#define RTKV_HIP_CHECK(expr)                                                      \
+  do {                                                                            \
+    hipError_t _e = (expr);                                                       \
+    if (_e != hipSuccess) {                                                       \
+      ::rtkv::set_error(std::string(#expr) + ": " + hipGetErrorString(_e));       \
+      return RTKV_ERR_HIP;                                                        \
+    }                                                                             \
+  } while (0)
+
+#define RTKV_REQUIRE(cond, msg)                                                   \
+  do {                                                                            \
+    if (!(cond)) {                                                                \
+      ::rtkv::set_error(std::string("rtkv: ") + (msg));                           \
+      return RTKV_ERR_INVALID;                                                    \
+    }                                                                             \
+  } while (0)
+
+// ------------------------------------------------------------------------------------ launchers
+// (implemented in the .hip translation units; all return rtkv_status)
+int launch_aggregation(const rtkv_attn_desc& w, int P, float* A, hipStream_t st);
+int launch_position_bias(int64_t S, float* pos, hipStream_t st);
+int launch_minmax_normalize(const void* x, int dt, int64_t B, int64_t S, void* out, hipStream_t st);
+
+struct FinalizeArgs {
+  const float* A;          // aggregation (mode_scores = 1)
+  int a_dtype;
+  float* scores;           // written when mode_scores = 1, read otherwise
+  uint8_t* labels;         // written when mode_labels = 1, read otherwise
+  uint8_t* mask;           // may be null when mode_select = 0
+  int32_t* kept_index;     // may be null
+  int64_t* row_offset;     // may be null
+  int64_t row_capacity;
+  int64_t B, S, F;
+  int kv_dtype;
+  rtkv_layer_params p;
+  float logS;              // (float)log((double)S), host libm (as Python's math.log)
+  float ctx;               // (float)min(1, P/S)
+  rtkv_layer_stats* stats;
+  int mode_scores, mode_labels, mode_select;
+};
+int launch_finalize(const FinalizeArgs& a, hipStream_t st);
+
+struct QuantArgs {
+  rtkv_kv_desc kv;
+  const uint8_t* labels;          // [B,S]
+  const int32_t* kept_index;      // [B,cap] or null (all tokens)
+  const rtkv_layer_stats* stats;  // kept counts / max_kept (null when kept_index is null)
+  int32_t bits[3];
+  rtkv_layer_out out;
+};
+int launch_quant(const QuantArgs& a, hipStream_t st);
+
+int launch_gather(const void* src, int64_t B, int64_t S, int64_t row_bytes, const int32_t* kept_index, int64_t cap,
+                  int64_t ssb, void* dst, int64_t dsb, int64_t sss, const rtkv_layer_stats* stats, hipStream_t st);
+int launch_unpack(const uint8_t* packed, const int64_t* row_offset, const float* scale_zp, int which,
+                  const int32_t* kept_index, const uint8_t* labels, int64_t B, int64_t S, int64_t cap,
+                  const int64_t* rows, int64_t H, int64_t D, int dt, const int32_t bits[3], void* out,
+                  int64_t ob, int64_t os, int64_t oh, hipStream_t st);
+
+int launch_tensor_params(const void* x, int dt, int64_t n_rows, int64_t row_len, const uint8_t* row_labels,
+                         int label_value, int bits, float* scale_zp, void* ws, size_t ws_bytes, hipStream_t st);
+int launch_tensor_fake_quant(const void* x, int dt, int64_t n_rows, int64_t row_len, const uint8_t* row_labels,
+                             int label_value, int bits, const float* scale_zp, void* out, hipStream_t st);
+
+}  // namespace rtkv

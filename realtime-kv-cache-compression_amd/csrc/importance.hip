@@ -1,0 +1,359 @@
+// importance.hip — K1: prompt-attention aggregation (token_importance.py:21-47), plus the small
+// score helpers (position bias :87-110, min-max normalisation :49-85).
+//
+// K1 reads the [B,H,S,P] prompt columns of W exactly once (the dominant input of the importance
+// stage, B·H·S·P·e bytes) and reproduces PyTorch's CPU reduction order bit for bit:
+//   mean over heads  = multi_row_sum cascade (16-element blocks, 4 levels) / H   (vectorized_outer_sum)
+//   sum over prompt  = vectorized_inner_sum with 8 fp32 lanes, ilp-4 partials, lanes added last
+// Work decomposition: a 256-thread workgroup owns TT consecutive tokens of one batch row.  For each
+// head the TT×P slab is contiguous in a [B,H,S,P] slice, so the workgroup streams H slabs with one
+// 16-byte load per thread per head (16 heads in flight per thread).  Means go to LDS; 8 threads per
+// token then form the 8 vector lanes of the inner sum and one thread folds them.
+#include "common.h"
+
+namespace rtkv {
+
+// ----------------------------------------------------------------------------- reduction order
+// PyTorch multi_row_sum for one column, n < 2^20 (level_power = 4, level_step = 16).
+template <typename Get> __device__ __forceinline__ float cascade_seq(Get get, int n) {
+  float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+  int i = 0;
+  while (i + 16 <= n) {
+    for (int j = 0; j < 16; ++j, ++i) a0 += get(i);
+    a1 += a0;
+    a0 = 0.f;
+    if ((i & (15 << 4)) == 0) {
+      a2 += a1;
+      a1 = 0.f;
+      if ((i & (15 << 8)) == 0) {
+        a3 += a2;
+        a2 = 0.f;
+      }
+    }
+  }
+  for (; i < n; ++i) a0 += get(i);
+  a0 += a1;
+  a0 += a2;
+  a0 += a3;
+  return a0;
+}
+
+// PyTorch row_sum<.., ilp_factor = 4>: part k = cascade over elements 4j+k, tail into part 0.
+template <typename Get> __device__ __forceinline__ float row_sum_ilp4(Get get, int n) {
+  const int nq = n >> 2;
+  float part[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) part[k] = cascade_seq([&](int j) { return get(4 * j + k); }, nq);
+  for (int i = nq * 4; i < n; ++i) part[0] += get(i);
+  part[0] += part[1];
+  part[0] += part[2];
+  part[0] += part[3];
+  return part[0];
+}
+
+// ----------------------------------------------------------------------------- K1 aggregation
+template <int DT, int VEC> struct VecT;
+template <> struct VecT<RTKV_F32, 4> { using T = float4; };
+template <> struct VecT<RTKV_F16, 8> { using T = uint4; };
+template <> struct VecT<RTKV_BF16, 8> { using T = uint4; };
+
+template <int DT, int VEC>
+__device__ __forceinline__ void unpack_vec(const typename VecT<DT, VEC>::T& v, float (&x)[VEC]) {
+  if constexpr (DT == RTKV_F32) {
+    x[0] = v.x; x[1] = v.y; x[2] = v.z; x[3] = v.w;
+  } else {
+    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      x[2 * k] = Dt<DT>::load((uint16_t)(w[k] & 0xffffu));
+      x[2 * k + 1] = Dt<DT>::load((uint16_t)(w[k] >> 16));
+    }
+  }
+}
+
+// Fast path: P % VEC == 0, 16-byte aligned rows.  Thread → one VEC-wide chunk of one token row.
+template <int DT, int VEC>
+__global__ __launch_bounds__(256) void aggregation_vec_kernel(const typename Dt<DT>::S* __restrict__ W,
+                                                              int H, int64_t S, int P, int64_t sb,
+                                                              int64_t sh, int64_t ss, int TT, int64_t lim,
+                                                              float* __restrict__ A) {
+  using S_ = typename Dt<DT>::S;
+  using V = typename VecT<DT, VEC>::T;
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  float* means = smem;                 // [TT][P]
+  float* lanes = smem + TT * P;        // [TT][8]
+  const int b = blockIdx.y;
+  const int64_t i0 = (int64_t)blockIdx.x * TT;
+  const int cpr = P / VEC;
+  const S_* Wb = W + b * sb;
+  for (int e = threadIdx.x; e < TT * cpr; e += blockDim.x) {
+    const int tok = e / cpr, ch = e - tok * cpr;
+    const int64_t i = i0 + tok;
+    if (i >= S) continue;
+    const S_* base = Wb + i * ss + (int64_t)ch * VEC;
+    float a0[VEC], a1[VEC], a2[VEC], a3[VEC];
+#pragma unroll
+    for (int k = 0; k < VEC; ++k) a0[k] = a1[k] = a2[k] = a3[k] = 0.f;
+    int h = 0;
+    while (h + 16 <= H) {
+      V v[16];
+#pragma unroll
+      for (int j = 0; j < 16; ++j) v[j] = *reinterpret_cast<const V*>(base + (int64_t)(h + j) * sh);
+#pragma unroll
+      for (int j = 0; j < 16; ++j) {
+        float x[VEC];
+        unpack_vec<DT, VEC>(v[j], x);
+#pragma unroll
+        for (int k = 0; k < VEC; ++k) a0[k] += x[k];
+      }
+      h += 16;
+#pragma unroll
+      for (int k = 0; k < VEC; ++k) { a1[k] += a0[k]; a0[k] = 0.f; }
+      if ((h & (15 << 4)) == 0) {
+#pragma unroll
+        for (int k = 0; k < VEC; ++k) { a2[k] += a1[k]; a1[k] = 0.f; }
+        if ((h & (15 << 8)) == 0) {
+#pragma unroll
+          for (int k = 0; k < VEC; ++k) { a3[k] += a2[k]; a2[k] = 0.f; }
+        }
+      }
+    }
+    for (; h < H; ++h) {
+      float x[VEC];
+      unpack_vec<DT, VEC>(*reinterpret_cast<const V*>(base + (int64_t)h * sh), x);
+#pragma unroll
+      for (int k = 0; k < VEC; ++k) a0[k] += x[k];
+    }
+    const float fH = (float)H;
+#pragma unroll
+    for (int k = 0; k < VEC; ++k) {
+      float s = a0[k];
+      s += a1[k];
+      s += a2[k];
+      s += a3[k];
+      const int p = ch * VEC + k;
+      const int64_t col = i * P + p;
+      if (col >= lim) {  // columns past the 32-aligned block: row_sum (ilp 4) order
+        const S_* colp = Wb + i * ss + p;
+        s = row_sum_ilp4([&](int hh) { return Dt<DT>::load(colp[(int64_t)hh * sh]); }, H);
+      }
+      means[tok * P + p] = Dt<DT>::rnd(s / fH);
+    }
+  }
+  __syncthreads();
+  // inner sum over the prompt columns: 8 fp32 vector lanes per token
+  constexpr int VN = (DT == RTKV_F32) ? 8 : 16;
+  if (P >= VN) {
+    const int nv = P / VN;
+    for (int e = threadIdx.x; e < TT * 8; e += blockDim.x) {
+      const int tok = e >> 3, l = e & 7;
+      if (i0 + tok >= S) continue;
+      const float* x = means + tok * P;
+      lanes[tok * 8 + l] = row_sum_ilp4(
+          [&](int m) { return VN == 8 ? x[8 * m + l] : (x[16 * m + l] + x[16 * m + 8 + l]); }, nv);
+    }
+  }
+  __syncthreads();
+  for (int tok = threadIdx.x; tok < TT; tok += blockDim.x) {
+    const int64_t i = i0 + tok;
+    if (i >= S) continue;
+    const float* x = means + tok * P;
+    float fin;
+    if (P >= VN) {
+      const int nv = P / VN;
+      fin = 0.f;
+      for (int k = nv * VN; k < P; ++k) fin += x[k];
+#pragma unroll
+      for (int l = 0; l < 8; ++l) fin += lanes[tok * 8 + l];
+    } else {
+      fin = row_sum_ilp4([&](int k) { return x[k]; }, P);
+    }
+    A[(int64_t)b * S + i] = Dt<DT>::rnd(fin);
+  }
+}
+
+// Generic path: any P / strides / alignment (scalar loads; the cfg1 P = 102 case lands here).
+template <int DT>
+__global__ __launch_bounds__(256) void aggregation_scalar_kernel(const typename Dt<DT>::S* __restrict__ W,
+                                                                 int H, int64_t S, int P, int64_t sb,
+                                                                 int64_t sh, int64_t ss, int TT, int64_t lim,
+                                                                 float* __restrict__ A) {
+  using S_ = typename Dt<DT>::S;
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  float* means = smem;
+  float* lanes = smem + TT * P;
+  const int b = blockIdx.y;
+  const int64_t i0 = (int64_t)blockIdx.x * TT;
+  const S_* Wb = W + b * sb;
+  for (int e = threadIdx.x; e < TT * P; e += blockDim.x) {
+    const int tok = e / P, p = e - tok * P;
+    const int64_t i = i0 + tok;
+    if (i >= S) continue;
+    const S_* colp = Wb + i * ss + p;
+    auto get = [&](int hh) { return Dt<DT>::load(colp[(int64_t)hh * sh]); };
+    const int64_t col = i * P + p;
+    const float s = (col < lim) ? cascade_seq(get, H) : row_sum_ilp4(get, H);
+    means[tok * P + p] = Dt<DT>::rnd(s / (float)H);
+  }
+  __syncthreads();
+  constexpr int VN = (DT == RTKV_F32) ? 8 : 16;
+  if (P >= VN) {
+    const int nv = P / VN;
+    for (int e = threadIdx.x; e < TT * 8; e += blockDim.x) {
+      const int tok = e >> 3, l = e & 7;
+      if (i0 + tok >= S) continue;
+      const float* x = means + tok * P;
+      lanes[tok * 8 + l] = row_sum_ilp4(
+          [&](int m) { return VN == 8 ? x[8 * m + l] : (x[16 * m + l] + x[16 * m + 8 + l]); }, nv);
+    }
+  }
+  __syncthreads();
+  for (int tok = threadIdx.x; tok < TT; tok += blockDim.x) {
+    const int64_t i = i0 + tok;
+    if (i >= S) continue;
+    const float* x = means + tok * P;
+    float fin;
+    if (P >= VN) {
+      const int nv = P / VN;
+      fin = 0.f;
+      for (int k = nv * VN; k < P; ++k) fin += x[k];
+      for (int l = 0; l < 8; ++l) fin += lanes[tok * 8 + l];
+    } else {
+      fin = row_sum_ilp4([&](int k) { return x[k]; }, P);
+    }
+    A[(int64_t)b * S + i] = Dt<DT>::rnd(fin);
+  }
+}
+
+// Columns of the flattened [S*P] head-mean below this limit take the cascade order (see
+// oracle/rtkv_oracle.c outer_cascade_limit).
+static int64_t cascade_limit(int dt, int64_t M) {
+  const int64_t vec = (dt == RTKV_F32) ? 8 : 16;
+  if (M >= vec) return (M / 32) * 32;
+  return (M / 4) * 4;
+}
+
+template <int DT>
+static int launch_agg_dt(const rtkv_attn_desc& w, int P, float* A, hipStream_t st) {
+  using S_ = typename Dt<DT>::S;
+  constexpr int VEC = 16 / Dt<DT>::kBytes;
+  const S_* W = static_cast<const S_*>(w.w_dev);
+  const int64_t lim = cascade_limit(DT, w.S * (int64_t)P);
+  const bool aligned = ((uintptr_t)W % 16 == 0) && (P % VEC == 0) && (w.stride_s % VEC == 0) &&
+                       (w.stride_h % VEC == 0) && (w.stride_b % VEC == 0);
+  const int H = (int)w.H;
+  if (aligned) {
+    const int cpr = P / VEC;
+    int TT = 256 / cpr;
+    if (TT < 1) TT = 1;
+    if (TT > 64) TT = 64;
+    const size_t lds = sizeof(float) * (size_t)TT * (P + 8);
+    dim3 grid((unsigned)((w.S + TT - 1) / TT), (unsigned)w.B);
+    hipLaunchKernelGGL((aggregation_vec_kernel<DT, VEC>), grid, dim3(256), lds, st, W, H, w.S, P,
+                       w.stride_b, w.stride_h, w.stride_s, TT, lim, A);
+  } else {
+    int TT = 256 / P;
+    if (TT < 1) TT = 1;
+    const size_t lds = sizeof(float) * (size_t)TT * (P + 8);
+    dim3 grid((unsigned)((w.S + TT - 1) / TT), (unsigned)w.B);
+    hipLaunchKernelGGL((aggregation_scalar_kernel<DT>), grid, dim3(256), lds, st, W, H, w.S, P,
+                       w.stride_b, w.stride_h, w.stride_s, TT, lim, A);
+  }
+  RTKV_HIP_CHECK(hipGetLastError());
+  return RTKV_OK;
+}
+
+int launch_aggregation(const rtkv_attn_desc& w, int P, float* A, hipStream_t st) {
+  RTKV_REQUIRE(w.w_dev && A, "aggregation: null pointer");
+  RTKV_REQUIRE(w.B >= 1 && w.H >= 1 && w.S >= 1, "aggregation: empty shape");
+  RTKV_REQUIRE(w.H < (1 << 20), "aggregation: H must be < 2^20");
+  RTKV_REQUIRE(P >= 1 && P <= w.cols, "aggregation: prompt_len must be in [1, cols]");
+  RTKV_REQUIRE(P <= 8192, "aggregation: prompt_len > 8192 unsupported");
+  RTKV_REQUIRE(w.B <= 65535, "aggregation: B > 65535 unsupported");
+  switch (w.dtype) {
+    case RTKV_F32: return launch_agg_dt<RTKV_F32>(w, P, A, st);
+    case RTKV_F16: return launch_agg_dt<RTKV_F16>(w, P, A, st);
+    case RTKV_BF16: return launch_agg_dt<RTKV_BF16>(w, P, A, st);
+  }
+  RTKV_REQUIRE(false, "aggregation: bad dtype");
+}
+
+// ----------------------------------------------------------------------------- position bias
+__global__ void position_bias_kernel(int64_t S, float logS, float* pos) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= S) return;
+  pos[i] = (S <= 1) ? 0.f : torch_logf((uint32_t)(i + 1)) / logS;
+}
+
+int launch_position_bias(int64_t S, float* pos, hipStream_t st) {
+  RTKV_REQUIRE(pos != nullptr || S == 0, "position_bias: null output");
+  RTKV_REQUIRE(S < (int64_t)1 << 31, "position_bias: S too large");
+  if (S == 0) return RTKV_OK;
+  const float logS = (float)std::log((double)S);
+  hipLaunchKernelGGL(position_bias_kernel, dim3((unsigned)((S + 255) / 256)), dim3(256), 0, st, S, logS, pos);
+  RTKV_HIP_CHECK(hipGetLastError());
+  return RTKV_OK;
+}
+
+// ----------------------------------------------------------------------------- min-max normalise
+template <int DT>
+__global__ __launch_bounds__(1024) void minmax_normalize_kernel(const typename Dt<DT>::S* __restrict__ x,
+                                                                int64_t S, typename Dt<DT>::S* __restrict__ out) {
+  __shared__ float red[2][16];
+  const int b = blockIdx.x;
+  const typename Dt<DT>::S* xb = x + (int64_t)b * S;
+  float mn = INFINITY, mx = -INFINITY;
+  for (int64_t i = threadIdx.x; i < S; i += blockDim.x) {
+    const float v = Dt<DT>::load(xb[i]);
+    mn = fminf(mn, v);
+    mx = fmaxf(mx, v);
+  }
+  mn = wave_min(mn);
+  mx = wave_max(mx);
+  const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  if (lane == 0) { red[0][wid] = mn; red[1][wid] = mx; }
+  __syncthreads();
+  if (threadIdx.x < 64) {
+    const int nw = blockDim.x >> 6;
+    mn = lane < nw ? red[0][lane] : INFINITY;
+    mx = lane < nw ? red[1][lane] : -INFINITY;
+    mn = wave_min(mn);
+    mx = wave_max(mx);
+    if (lane == 0) { red[0][0] = mn; red[1][0] = mx; }
+  }
+  __syncthreads();
+  mn = red[0][0];
+  mx = red[1][0];
+  const float den = Dt<DT>::rnd(mx - mn);
+  const float eps = Dt<DT>::rnd(1e-8f);
+  for (int64_t i = threadIdx.x; i < S; i += blockDim.x) {
+    const float v = Dt<DT>::load(xb[i]);
+    const float n = (den > eps) ? Dt<DT>::rnd(Dt<DT>::rnd(v - mn) / den) : 0.f;
+    out[(int64_t)b * S + i] = Dt<DT>::store(n);
+  }
+}
+
+int launch_minmax_normalize(const void* x, int dt, int64_t B, int64_t S, void* out, hipStream_t st) {
+  RTKV_REQUIRE(x && out, "minmax_normalize: null pointer");
+  RTKV_REQUIRE(B >= 1 && S >= 1 && B <= 65535, "minmax_normalize: bad shape");
+  switch (dt) {
+    case RTKV_F32:
+      hipLaunchKernelGGL(minmax_normalize_kernel<RTKV_F32>, dim3((unsigned)B), dim3(1024), 0, st,
+                         (const float*)x, S, (float*)out);
+      break;
+    case RTKV_F16:
+      hipLaunchKernelGGL(minmax_normalize_kernel<RTKV_F16>, dim3((unsigned)B), dim3(1024), 0, st,
+                         (const uint16_t*)x, S, (uint16_t*)out);
+      break;
+    case RTKV_BF16:
+      hipLaunchKernelGGL(minmax_normalize_kernel<RTKV_BF16>, dim3((unsigned)B), dim3(1024), 0, st,
+                         (const uint16_t*)x, S, (uint16_t*)out);
+      break;
+    default:
+      RTKV_REQUIRE(false, "minmax_normalize: bad dtype");
+  }
+  RTKV_HIP_CHECK(hipGetLastError());
+  return RTKV_OK;
+}
+
+}  // namespace rtkv

@@ -1,0 +1,513 @@
+// quant.hip — K4: per-token asymmetric min-max quantization + bit-pack + ordered compaction, plus
+// the unpack (consumer) kernel and the whole-tensor quantization helpers.
+//
+// Reference: DynamicPrecisionQuantizer.get_quantization_params / quantize_tensor /
+// apply_mixed_precision_quantization (dynamic_quantization.py:62-196) followed by the gather of
+// SelectiveTokenPropagator.apply_token_selection (selective_propagation.py:214-232).  The reference
+// fake-quantizes EVERY token with ~12 tiny torch ops and then gathers the kept rows; here each kept
+// row is read from HBM once, quantized in registers and written once (dequantized row in the output
+// position + packed codes), and dropped rows are never read.
+//
+// Work decomposition: one wave64 per (kept row, tensor).  Lane l owns 8-element chunks
+// c = k*64 + l (k < NCH), so every wave-instruction moves 64 × 16 B = 1 KiB of one row (fp32: two
+// such loads).  Row min/max → wave shuffle reduction; the per-element ops are fp32 ops rounded to
+// the dtype after each op (bit-identical to PyTorch CPU).  8 codes of w bits pack into exactly w
+// bytes, so each lane writes its chunk's codes with one store at byte offset c*w.
+#include "common.h"
+
+namespace rtkv {
+
+template <int DT> struct Chunk;  // 8 elements of storage
+template <> struct Chunk<RTKV_F32> { float4 a, b; };
+template <> struct Chunk<RTKV_F16> { uint4 a; };
+template <> struct Chunk<RTKV_BF16> { uint4 a; };
+
+template <int DT> __device__ __forceinline__ void chunk_to_f32(const Chunk<DT>& c, float (&x)[8]) {
+  if constexpr (DT == RTKV_F32) {
+    x[0] = c.a.x; x[1] = c.a.y; x[2] = c.a.z; x[3] = c.a.w;
+    x[4] = c.b.x; x[5] = c.b.y; x[6] = c.b.z; x[7] = c.b.w;
+  } else {
+    const uint32_t w[4] = {c.a.x, c.a.y, c.a.z, c.a.w};
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      x[2 * k] = Dt<DT>::load((uint16_t)(w[k] & 0xffffu));
+      x[2 * k + 1] = Dt<DT>::load((uint16_t)(w[k] >> 16));
+    }
+  }
+}
+template <int DT> __device__ __forceinline__ Chunk<DT> f32_to_chunk(const float (&x)[8]) {
+  Chunk<DT> c;
+  if constexpr (DT == RTKV_F32) {
+    c.a = make_float4(x[0], x[1], x[2], x[3]);
+    c.b = make_float4(x[4], x[5], x[6], x[7]);
+  } else {
+    uint32_t w[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      w[k] = (uint32_t)Dt<DT>::store(x[2 * k]) | ((uint32_t)Dt<DT>::store(x[2 * k + 1]) << 16);
+    c.a = make_uint4(w[0], w[1], w[2], w[3]);
+  }
+  return c;
+}
+
+// Little-endian accumulation of 8 codes of w bits (w <= 17) into 3 × 64-bit words.
+__device__ __forceinline__ void pack8(const uint32_t (&q)[8], int w, uint64_t& p0, uint64_t& p1, uint64_t& p2) {
+  p0 = p1 = p2 = 0;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const int bit = e * w;
+    const uint64_t v = q[e];
+    const int word = bit >> 6, sh = bit & 63;
+    const uint64_t lo = v << sh;
+    const uint64_t hi = sh ? (v >> (64 - sh)) : 0ull;
+    if (word == 0) { p0 |= lo; p1 |= hi; }
+    else if (word == 1) { p1 |= lo; p2 |= hi; }
+    else { p2 |= lo; }
+  }
+}
+
+__device__ __forceinline__ void store_bytes(uint8_t* dst, int nbytes, uint64_t p0, uint64_t p1, uint64_t p2) {
+  const uintptr_t addr = (uintptr_t)dst;
+  if (nbytes == 16 && (addr & 15) == 0) {
+    *reinterpret_cast<uint4*>(dst) = make_uint4((uint32_t)p0, (uint32_t)(p0 >> 32), (uint32_t)p1, (uint32_t)(p1 >> 32));
+  } else if (nbytes == 8 && (addr & 7) == 0) {
+    *reinterpret_cast<uint2*>(dst) = make_uint2((uint32_t)p0, (uint32_t)(p0 >> 32));
+  } else if (nbytes == 4 && (addr & 3) == 0) {
+    *reinterpret_cast<uint32_t*>(dst) = (uint32_t)p0;
+  } else if (nbytes == 2 && (addr & 1) == 0) {
+    *reinterpret_cast<uint16_t*>(dst) = (uint16_t)p0;
+  } else {
+    for (int k = 0; k < nbytes; ++k) {
+      const uint64_t word = k < 8 ? p0 : (k < 16 ? p1 : p2);
+      dst[k] = (uint8_t)(word >> ((k & 7) * 8));
+    }
+  }
+}
+
+struct RowParams {
+  float scale, zp, qmaxT;
+};
+
+template <int DT> __device__ __forceinline__ RowParams row_params(float mn, float mx, int bits) {
+  // dynamic_quantization.py:79-93 (each op rounded to the dtype)
+  RowParams r;
+  const float qmax = (float)((1u << bits) - 1u);
+  r.qmaxT = Dt<DT>::rnd(qmax);  // clamp bound as converted by torch.clamp (:121)
+  if (mx == mn) {
+    r.scale = 1.f;
+    r.zp = 0.f;
+  } else {
+    r.scale = Dt<DT>::rnd(Dt<DT>::rnd(mx - mn) / qmax);
+    r.zp = Dt<DT>::rnd(0.f - Dt<DT>::rnd(mn / r.scale));
+  }
+  return r;
+}
+
+template <int DT> __device__ __forceinline__ float quant_code(float x, const RowParams& rp) {
+  // dynamic_quantization.py:120-121
+  const float t = Dt<DT>::rnd(Dt<DT>::rnd(x / rp.scale) + rp.zp);
+  float q = Dt<DT>::rnd(__builtin_rintf(t));
+  q = q < 0.f ? 0.f : q;
+  q = q > rp.qmaxT ? rp.qmaxT : q;
+  return q;
+}
+template <int DT> __device__ __forceinline__ float dequant(float q, const RowParams& rp) {
+  return Dt<DT>::rnd(Dt<DT>::rnd(q - rp.zp) * rp.scale);  // :124
+}
+
+// ------------------------------------------------------------------------------------ K4
+template <int DT, int NCH, bool VEC>
+__global__ __launch_bounds__(256) void quant_rows_kernel(QuantArgs a) {
+  using S_ = typename Dt<DT>::S;
+  const int lane = threadIdx.x & 63;
+  const int64_t gw = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  const int64_t nw = (int64_t)gridDim.x * (blockDim.x >> 6);
+  const int64_t B = a.kv.B, S = a.kv.S, H = a.kv.H, D = a.kv.D, F = H * D;
+  const int64_t nch = (F + 7) >> 3;
+  const int64_t cap = a.out.row_capacity;
+  int64_t R = a.kept_index ? a.stats->max_kept : S;  // rows per batch row
+  if (R > cap) R = cap;
+  const int64_t tasks = 2 * B * R;
+  const rtkv_batch_stats* bst = a.stats ? reinterpret_cast<const rtkv_batch_stats*>(a.stats + 1) : nullptr;
+  const bool emit_deq = a.out.k_out_dev != nullptr;
+  const bool emit_pk = a.out.packed_k_dev != nullptr;
+  for (int64_t t = gw; t < tasks; t += nw) {
+    const int which = (int)(t & 1);
+    const int64_t rr = t >> 1;
+    const int64_t b = rr / R, r = rr - b * R;
+    const int64_t kept_b = a.kept_index ? bst[b].kept : S;
+    S_* out = static_cast<S_*>(which ? a.out.v_out_dev : a.out.k_out_dev);
+    const int64_t osb = a.out.o_stride_b >= 0 ? a.out.o_stride_b : R * a.out.o_stride_s;
+    S_* orow = emit_deq ? out + b * osb + r * a.out.o_stride_s : nullptr;
+    const int64_t i = (r < kept_b) ? (a.kept_index ? a.kept_index[b * cap + r] : r) : 0;
+    const int lab = (r < kept_b) ? a.labels[b * S + i] : 0;
+    if (r >= kept_b || lab > 2) {  // zero padding row (selective_propagation.py:214-222)
+      if (emit_deq) {
+#pragma unroll
+        for (int k = 0; k < NCH; ++k) {
+          const int64_t c = (int64_t)k * 64 + lane;
+          if (c >= nch) break;
+          for (int e = 0; e < 8; ++e) {
+            const int64_t f = c * 8 + e;
+            if (f < F) orow[(f / D) * a.out.o_stride_h + (f % D)] = Dt<DT>::store(0.f);
+          }
+        }
+      }
+      if (a.out.scale_zp_dev && lane < 2) a.out.scale_zp_dev[(b * cap + r) * 4 + which * 2 + lane] = 0.f;
+      continue;
+    }
+    const int bits = a.bits[lab];
+    const int w = field_width(DT, bits);
+    const S_* src = static_cast<const S_*>(which ? a.kv.v_dev : a.kv.k_dev) + b * a.kv.stride_b + i * a.kv.stride_s;
+
+    // ---- load the row (one HBM read)
+    float x[NCH][8];
+    float mn = INFINITY, mx = -INFINITY;
+    if constexpr (VEC) {
+      Chunk<DT> raw[NCH];
+#pragma unroll
+      for (int k = 0; k < NCH; ++k) {
+        const int64_t c = (int64_t)k * 64 + lane;
+        if (c < nch) {
+          const int64_t f = c * 8;
+          raw[k] = *reinterpret_cast<const Chunk<DT>*>(src + (f / D) * a.kv.stride_h + (f % D));
+        }
+      }
+#pragma unroll
+      for (int k = 0; k < NCH; ++k) {
+        const int64_t c = (int64_t)k * 64 + lane;
+        if (c < nch) {
+          chunk_to_f32<DT>(raw[k], x[k]);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) { mn = fminf(mn, x[k][e]); mx = fmaxf(mx, x[k][e]); }
+        }
+      }
+    } else {
+#pragma unroll
+      for (int k = 0; k < NCH; ++k) {
+        const int64_t c = (int64_t)k * 64 + lane;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const int64_t f = c * 8 + e;
+          if (c < nch && f < F) {
+            x[k][e] = Dt<DT>::load(src[(f / D) * a.kv.stride_h + (f % D)]);
+            mn = fminf(mn, x[k][e]);
+            mx = fmaxf(mx, x[k][e]);
+          } else {
+            x[k][e] = 0.f;
+          }
+        }
+      }
+    }
+    mn = wave_min(mn);
+    mx = wave_max(mx);
+    const RowParams rp = row_params<DT>(mn, mx, bits);
+    if (a.out.scale_zp_dev && lane < 2)
+      a.out.scale_zp_dev[(b * cap + r) * 4 + which * 2 + lane] = lane == 0 ? rp.scale : rp.zp;
+    uint8_t* pk = nullptr;
+    if (emit_pk) {
+      pk = (which ? a.out.packed_v_dev : a.out.packed_k_dev) + a.out.row_offset_dev[b * cap + r];
+    }
+    // ---- quantize, pack, dequantize, store
+#pragma unroll
+    for (int k = 0; k < NCH; ++k) {
+      const int64_t c = (int64_t)k * 64 + lane;
+      if (c >= nch) break;
+      float q[8], d[8];
+      uint32_t qi[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        q[e] = quant_code<DT>(x[k][e], rp);
+        d[e] = dequant<DT>(q[e], rp);
+        qi[e] = (uint32_t)q[e];
+      }
+      const int64_t f0 = c * 8;
+      const int nvalid = (F - f0) < 8 ? (int)(F - f0) : 8;
+      if (emit_pk) {
+        if (nvalid < 8)
+          for (int e = nvalid; e < 8; ++e) qi[e] = 0u;
+        uint64_t p0, p1, p2;
+        pack8(qi, w, p0, p1, p2);
+        store_bytes(pk + c * w, (nvalid * w + 7) >> 3, p0, p1, p2);
+      }
+      if (emit_deq) {
+        if constexpr (VEC) {
+          *reinterpret_cast<Chunk<DT>*>(orow + (f0 / D) * a.out.o_stride_h + (f0 % D)) = f32_to_chunk<DT>(d);
+        } else {
+          for (int e = 0; e < nvalid; ++e) {
+            const int64_t f = f0 + e;
+            orow[(f / D) * a.out.o_stride_h + (f % D)] = Dt<DT>::store(d[e]);
+          }
+        }
+      }
+    }
+  }
+}
+
+template <int DT, bool VEC>
+static int launch_quant_vec(const QuantArgs& a, int nch_per_lane, dim3 grid, hipStream_t st) {
+#define RTKV_Q(N)                                                                            \
+  if (nch_per_lane <= N) {                                                                   \
+    hipLaunchKernelGGL((quant_rows_kernel<DT, N, VEC>), grid, dim3(256), 0, st, a);          \
+    RTKV_HIP_CHECK(hipGetLastError());                                                       \
+    return RTKV_OK;                                                                          \
+  }
+  RTKV_Q(1) RTKV_Q(2) RTKV_Q(4) RTKV_Q(8) RTKV_Q(10) RTKV_Q(16) RTKV_Q(32)
+#undef RTKV_Q
+  set_error("rtkv: row of more than 16384 elements unsupported");
+  return RTKV_ERR_UNSUPPORTED;
+}
+
+template <int DT>
+static int launch_quant_dt(const QuantArgs& a, hipStream_t st) {
+  const rtkv_kv_desc& kv = a.kv;
+  const int64_t F = kv.H * kv.D;
+  const int64_t nch = (F + 7) / 8;
+  const int per_lane = (int)((nch + 63) / 64);
+  const int64_t R = a.kept_index ? (a.out.row_capacity < kv.S ? a.out.row_capacity : kv.S) : kv.S;
+  const int64_t tasks = 2 * kv.B * R;
+  int64_t blocks = (tasks + 3) / 4;
+  if (blocks > 2048) blocks = 2048;
+  if (blocks < 1) blocks = 1;
+  const int esz = Dt<DT>::kBytes;
+  auto al16 = [](const void* p) { return p == nullptr || ((uintptr_t)p % 16) == 0; };
+  bool vec = (kv.D % 8 == 0) && al16(kv.k_dev) && al16(kv.v_dev) && (kv.stride_s * esz) % 16 == 0 &&
+             (kv.stride_h * esz) % 16 == 0 && (kv.stride_b * esz) % 16 == 0;
+  if (a.out.k_out_dev)
+    vec = vec && al16(a.out.k_out_dev) && al16(a.out.v_out_dev) && (a.out.o_stride_s * esz) % 16 == 0 &&
+          (a.out.o_stride_h * esz) % 16 == 0 && (a.out.o_stride_b * esz) % 16 == 0;
+  if (vec) return launch_quant_vec<DT, true>(a, per_lane, dim3((unsigned)blocks), st);
+  return launch_quant_vec<DT, false>(a, per_lane, dim3((unsigned)blocks), st);
+}
+
+int launch_quant(const QuantArgs& a, hipStream_t st) {
+  RTKV_REQUIRE(a.kv.k_dev && a.kv.v_dev && a.labels, "quantize_rows: null K/V/labels");
+  RTKV_REQUIRE(a.kv.B >= 1 && a.kv.S >= 1 && a.kv.H >= 1 && a.kv.D >= 1, "quantize_rows: empty shape");
+  RTKV_REQUIRE(!a.kept_index || a.stats, "quantize_rows: kept_index requires stats");
+  RTKV_REQUIRE(!a.out.k_out_dev == !a.out.v_out_dev, "quantize_rows: k_out and v_out must both be set or both null");
+  RTKV_REQUIRE(!a.out.packed_k_dev == !a.out.packed_v_dev, "quantize_rows: packed_k and packed_v must match");
+  RTKV_REQUIRE(!a.out.packed_k_dev || a.out.row_offset_dev, "quantize_rows: packed output needs row offsets");
+  RTKV_REQUIRE(a.out.row_capacity >= 1, "quantize_rows: row_capacity must be >= 1");
+  for (int g = 0; g < 3; ++g) {
+    RTKV_REQUIRE(a.bits[g] >= 1 && a.bits[g] <= 16, "quantize_rows: bits must be in [1, 16]");
+    if (a.out.packed_k_dev)
+      RTKV_REQUIRE(field_width(a.kv.dtype, a.bits[g]) > 0, "quantize_rows: packed codes unsupported for this dtype/bits");
+  }
+  switch (a.kv.dtype) {
+    case RTKV_F32: return launch_quant_dt<RTKV_F32>(a, st);
+    case RTKV_F16: return launch_quant_dt<RTKV_F16>(a, st);
+    case RTKV_BF16: return launch_quant_dt<RTKV_BF16>(a, st);
+  }
+  RTKV_REQUIRE(false, "quantize_rows: bad dtype");
+}
+
+// ------------------------------------------------------------------------------------ gather
+__global__ __launch_bounds__(256) void gather_rows_kernel(const uint8_t* __restrict__ src, int64_t B, int64_t row_bytes,
+                                                          const int32_t* __restrict__ kept_index, int64_t cap,
+                                                          int64_t ssb, int64_t sss, uint8_t* __restrict__ dst, int64_t dsb,
+                                                          const rtkv_layer_stats* __restrict__ stats) {
+  const int64_t R = stats->max_kept;
+  const rtkv_batch_stats* bst = reinterpret_cast<const rtkv_batch_stats*>(stats + 1);
+  const int64_t db = dsb >= 0 ? dsb : R * row_bytes;
+  const bool vec = ((row_bytes | ssb | sss | db) & 15) == 0 && (((uintptr_t)src | (uintptr_t)dst) & 15) == 0;
+  const int lane = threadIdx.x & 63;
+  const int64_t gw = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  const int64_t nw = (int64_t)gridDim.x * (blockDim.x >> 6);
+  for (int64_t t = gw; t < B * R; t += nw) {
+    const int64_t b = t / R, r = t - b * R;
+    uint8_t* d = dst + b * db + r * row_bytes;
+    const bool keep = r < bst[b].kept;
+    const uint8_t* s = keep ? src + b * ssb + (int64_t)kept_index[b * cap + r] * sss : nullptr;
+    if (vec) {
+      for (int64_t o = (int64_t)lane * 16; o < row_bytes; o += 64 * 16)
+        *reinterpret_cast<uint4*>(d + o) = keep ? *reinterpret_cast<const uint4*>(s + o) : make_uint4(0, 0, 0, 0);
+    } else {
+      for (int64_t o = lane; o < row_bytes; o += 64) d[o] = keep ? s[o] : (uint8_t)0;
+    }
+  }
+}
+
+int launch_gather(const void* src, int64_t B, int64_t S, int64_t row_bytes, const int32_t* kept_index, int64_t cap,
+                  int64_t ssb, void* dst, int64_t dsb, int64_t sss, const rtkv_layer_stats* stats, hipStream_t st) {
+  RTKV_REQUIRE(src && dst && kept_index && stats, "gather_rows: null pointer");
+  RTKV_REQUIRE(B >= 1 && S >= 1 && row_bytes >= 1 && cap >= 1, "gather_rows: bad shape");
+  int64_t blocks = (B * (cap < S ? cap : S) + 3) / 4;
+  if (blocks > 2048) blocks = 2048;
+  hipLaunchKernelGGL(gather_rows_kernel, dim3((unsigned)blocks), dim3(256), 0, st, static_cast<const uint8_t*>(src), B,
+                     row_bytes, kept_index, cap, ssb, sss, static_cast<uint8_t*>(dst), dsb, stats);
+  RTKV_HIP_CHECK(hipGetLastError());
+  return RTKV_OK;
+}
+
+// ------------------------------------------------------------------------------------ unpack
+template <int DT>
+__global__ __launch_bounds__(256) void unpack_kernel(const uint8_t* __restrict__ packed, const int64_t* __restrict__ row_offset,
+                                                     const float* __restrict__ scale_zp, int which,
+                                                     const int32_t* __restrict__ kept_index, const uint8_t* __restrict__ labels,
+                                                     int64_t B, int64_t S, int64_t cap, const int64_t* __restrict__ rows,
+                                                     int64_t H, int64_t D, int b0, int b1, int b2,
+                                                     typename Dt<DT>::S* __restrict__ out, int64_t ob, int64_t os, int64_t oh) {
+  const int lane = threadIdx.x & 63;
+  const int64_t gw = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  const int64_t nw = (int64_t)gridDim.x * (blockDim.x >> 6);
+  const int64_t F = H * D, nch = (F + 7) >> 3;
+  const int bitsv[3] = {b0, b1, b2};
+  for (int64_t t = gw; t < B * cap; t += nw) {
+    const int64_t b = t / cap, r = t - b * cap;
+    if (r >= rows[b]) continue;
+    const int64_t i = kept_index ? kept_index[b * cap + r] : r;
+    const int w = field_width(DT, bitsv[labels[b * S + i]]);
+    RowParams rp;
+    rp.scale = scale_zp[(b * cap + r) * 4 + which * 2];
+    rp.zp = scale_zp[(b * cap + r) * 4 + which * 2 + 1];
+    const uint8_t* src = packed + row_offset[b * cap + r];
+    for (int64_t c = lane; c < nch; c += 64) {
+      const int64_t f0 = c * 8;
+      const int nvalid = (F - f0) < 8 ? (int)(F - f0) : 8;
+      const uint8_t* p = src + c * w;
+      const int nb = (nvalid * w + 7) >> 3;
+      uint64_t wd[3] = {0, 0, 0};
+      for (int k = 0; k < nb; ++k) wd[k >> 3] |= (uint64_t)p[k] << ((k & 7) * 8);
+      const uint64_t m = (w >= 64) ? ~0ull : ((1ull << w) - 1ull);
+      for (int e = 0; e < nvalid; ++e) {
+        const int bit = e * w, word = bit >> 6, sh = bit & 63;
+        uint64_t v = wd[word] >> sh;
+        if (sh && word < 2) v |= wd[word + 1] << (64 - sh);
+        const float q = (float)(uint32_t)(v & m);
+        const int64_t f = f0 + e;
+        out[b * ob + r * os + (f / D) * oh + (f % D)] = Dt<DT>::store(dequant<DT>(q, rp));
+      }
+    }
+  }
+}
+
+int launch_unpack(const uint8_t* packed, const int64_t* row_offset, const float* scale_zp, int which,
+                  const int32_t* kept_index, const uint8_t* labels, int64_t B, int64_t S, int64_t cap,
+                  const int64_t* rows, int64_t H, int64_t D, int dt, const int32_t bits[3], void* out,
+                  int64_t ob, int64_t os, int64_t oh, hipStream_t st) {
+  RTKV_REQUIRE(packed && row_offset && scale_zp && labels && rows && out, "unpack: null pointer");
+  RTKV_REQUIRE(B >= 1 && S >= 1 && cap >= 1 && H >= 1 && D >= 1, "unpack: bad shape");
+  for (int g = 0; g < 3; ++g) RTKV_REQUIRE(field_width(dt, bits[g]) > 0, "unpack: unsupported bits");
+  int64_t blocks = (B * cap + 3) / 4;
+  if (blocks > 2048) blocks = 2048;
+  switch (dt) {
+#define RTKV_U(DT)                                                                                          \
+  case DT:                                                                                                  \
+    hipLaunchKernelGGL(unpack_kernel<DT>, dim3((unsigned)blocks), dim3(256), 0, st, packed, row_offset,     \
+                       scale_zp, which, kept_index, labels, B, S, cap, rows, H, D, bits[0], bits[1],       \
+                       bits[2], static_cast<typename Dt<DT>::S*>(out), ob, os, oh);                         \
+    break;
+    RTKV_U(RTKV_F32) RTKV_U(RTKV_F16) RTKV_U(RTKV_BF16)
+#undef RTKV_U
+    default:
+      RTKV_REQUIRE(false, "unpack: bad dtype");
+  }
+  RTKV_HIP_CHECK(hipGetLastError());
+  return RTKV_OK;
+}
+
+// ------------------------------------------------------------------------------------ whole-tensor helpers
+// get_quantization_params over all elements of the rows whose label equals label_value (or every row
+// when row_labels is null): per-block min/max partials, then one block folds them.
+template <int DT>
+__global__ __launch_bounds__(256) void tensor_minmax_kernel(const typename Dt<DT>::S* __restrict__ x, int64_t n_rows,
+                                                            int64_t row_len, const uint8_t* __restrict__ row_labels,
+                                                            int label_value, float* __restrict__ partial) {
+  __shared__ float red[2][4];
+  float mn = INFINITY, mx = -INFINITY;
+  const int64_t n = n_rows * row_len;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < n; e += (int64_t)gridDim.x * blockDim.x) {
+    if (row_labels && row_labels[e / row_len] != label_value) continue;
+    const float v = Dt<DT>::load(x[e]);
+    mn = fminf(mn, v);
+    mx = fmaxf(mx, v);
+  }
+  mn = wave_min(mn);
+  mx = wave_max(mx);
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  if (lane == 0) { red[0][wid] = mn; red[1][wid] = mx; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    mn = red[0][0];
+    mx = red[1][0];
+    for (int k = 1; k < (int)(blockDim.x >> 6); ++k) { mn = fminf(mn, red[0][k]); mx = fmaxf(mx, red[1][k]); }
+    partial[2 * blockIdx.x] = mn;
+    partial[2 * blockIdx.x + 1] = mx;
+  }
+}
+
+template <int DT>
+__global__ void tensor_params_kernel(const float* __restrict__ partial, int nblocks, int bits, float* __restrict__ scale_zp) {
+  if (threadIdx.x != 0) return;
+  float mn = INFINITY, mx = -INFINITY;
+  for (int k = 0; k < nblocks; ++k) { mn = fminf(mn, partial[2 * k]); mx = fmaxf(mx, partial[2 * k + 1]); }
+  if (!(mn <= mx)) { mn = mx = 0.f; }  // no element selected
+  const RowParams rp = row_params<DT>(mn, mx, bits);
+  scale_zp[0] = rp.scale;
+  scale_zp[1] = rp.zp;
+}
+
+template <int DT>
+__global__ __launch_bounds__(256) void tensor_fake_quant_kernel(const typename Dt<DT>::S* __restrict__ x, int64_t n_rows,
+                                                                int64_t row_len, const uint8_t* __restrict__ row_labels,
+                                                                int label_value, int bits, const float* __restrict__ scale_zp,
+                                                                typename Dt<DT>::S* __restrict__ out) {
+  const RowParams rp0 = {scale_zp[0], scale_zp[1], 0.f};
+  RowParams rp = rp0;
+  rp.qmaxT = Dt<DT>::rnd((float)((1u << bits) - 1u));
+  const int64_t n = n_rows * row_len;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < n; e += (int64_t)gridDim.x * blockDim.x) {
+    if (row_labels && row_labels[e / row_len] != label_value) continue;
+    out[e] = Dt<DT>::store(dequant<DT>(quant_code<DT>(Dt<DT>::load(x[e]), rp), rp));
+  }
+}
+
+int launch_tensor_params(const void* x, int dt, int64_t n_rows, int64_t row_len, const uint8_t* row_labels,
+                         int label_value, int bits, float* scale_zp, void* ws, size_t ws_bytes, hipStream_t st) {
+  RTKV_REQUIRE(x && scale_zp && ws, "tensor_quant_params: null pointer");
+  RTKV_REQUIRE(n_rows >= 1 && row_len >= 1, "tensor_quant_params: empty tensor");
+  RTKV_REQUIRE(bits >= 1 && bits <= 16, "tensor_quant_params: bits must be in [1, 16]");
+  int64_t nblocks = (n_rows * row_len + 255) / 256;
+  if (nblocks > 1024) nblocks = 1024;
+  RTKV_REQUIRE(ws_bytes >= (size_t)nblocks * 8, "tensor_quant_params: workspace too small");
+  float* partial = static_cast<float*>(ws);
+  switch (dt) {
+#define RTKV_T(DT)                                                                                                   \
+  case DT:                                                                                                           \
+    hipLaunchKernelGGL(tensor_minmax_kernel<DT>, dim3((unsigned)nblocks), dim3(256), 0, st,                          \
+                       static_cast<const typename Dt<DT>::S*>(x), n_rows, row_len, row_labels, label_value, partial); \
+    hipLaunchKernelGGL(tensor_params_kernel<DT>, dim3(1), dim3(64), 0, st, partial, (int)nblocks, bits, scale_zp);   \
+    break;
+    RTKV_T(RTKV_F32) RTKV_T(RTKV_F16) RTKV_T(RTKV_BF16)
+#undef RTKV_T
+    default:
+      RTKV_REQUIRE(false, "tensor_quant_params: bad dtype");
+  }
+  RTKV_HIP_CHECK(hipGetLastError());
+  return RTKV_OK;
+}
+
+int launch_tensor_fake_quant(const void* x, int dt, int64_t n_rows, int64_t row_len, const uint8_t* row_labels,
+                             int label_value, int bits, const float* scale_zp, void* out, hipStream_t st) {
+  RTKV_REQUIRE(x && scale_zp && out, "tensor_fake_quant: null pointer");
+  RTKV_REQUIRE(n_rows >= 1 && row_len >= 1, "tensor_fake_quant: empty tensor");
+  RTKV_REQUIRE(bits >= 1 && bits <= 16, "tensor_fake_quant: bits must be in [1, 16]");
+  int64_t nblocks = (n_rows * row_len + 255) / 256;
+  if (nblocks > 4096) nblocks = 4096;
+  switch (dt) {
+#define RTKV_T(DT)                                                                                          \
+  case DT:                                                                                                  \
+    hipLaunchKernelGGL(tensor_fake_quant_kernel<DT>, dim3((unsigned)nblocks), dim3(256), 0, st,             \
+                       static_cast<const typename Dt<DT>::S*>(x), n_rows, row_len, row_labels, label_value, \
+                       bits, scale_zp, static_cast<typename Dt<DT>::S*>(out));                               \
+    break;
+    RTKV_T(RTKV_F32) RTKV_T(RTKV_F16) RTKV_T(RTKV_BF16)
+#undef RTKV_T
+    default:
+      RTKV_REQUIRE(false, "tensor_fake_quant: bad dtype");
+  }
+  RTKV_HIP_CHECK(hipGetLastError());
+  return RTKV_OK;
+}
+
+}  // namespace rtkv

@@ -1,0 +1,145 @@
+"""CompressedKVCache and AdaptiveQuantization — the compression_layers API surface named by the
+north_star (reference src/models/compression_layers.py:7-45 and :96-175).
+
+CompressedKVCache keeps the reference's dict-of-tensors interface and adds the packed form of a layer
+(bit-packed integer codes + per-row scale/zero-point, as produced by rtkv_compress_layer) with an
+on-device decoder (rtkv_unpack_dequant) that reproduces the dequantized K'/V' bit for bit.
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import Dict, Optional
+
+import torch
+import torch.nn as nn
+
+from . import _lib as L
+from .token_importance import _workspace
+
+
+class CompressedKVCache:
+    """Per-layer storage of compressed K/V (compression_layers.py:7-45)."""
+
+    def __init__(self, max_batch_size: int, max_seq_len: int, head_dim: int):
+        self.max_batch_size = max_batch_size
+        self.max_seq_len = max_seq_len
+        self.head_dim = head_dim
+        self.cache_data: Dict[int, dict] = {}
+        self.compression_info: Dict[int, dict] = {}
+
+    def store_compressed_kv(self, layer_idx: int, keys: torch.Tensor, values: torch.Tensor,
+                            importance_scores: torch.Tensor, precision_labels: torch.Tensor,
+                            selection_mask: torch.Tensor):
+        self.cache_data[layer_idx] = {
+            "keys": keys.detach(),
+            "values": values.detach(),
+            "importance_scores": importance_scores.detach(),
+            "precision_labels": precision_labels.detach(),
+            "selection_mask": selection_mask.detach(),
+            "compressed_seq_len": keys.shape[1],
+        }
+
+    def get_compressed_kv(self, layer_idx: int) -> Optional[Dict]:
+        return self.cache_data.get(layer_idx)
+
+    def clear_cache(self):
+        self.cache_data.clear()
+        self.compression_info.clear()
+
+    # ------------------------------------------------------------------ packed form (extension)
+    def store_packed(self, layer_idx: int, packed: dict):
+        """Keep only the packed codes of a layer (``info['packed']`` of compress_layer_kv_cache)."""
+        self.compression_info[layer_idx] = packed
+
+    def packed_nbytes(self, layer_idx: int) -> int:
+        p = self.compression_info[layer_idx]
+        return (p["codes_k"].numel() + p["codes_v"].numel() + p["scale_zp"].numel() * 4
+                + p["kept_index"].numel() * 4)
+
+    def dequantize(self, layer_idx: int):
+        """Decode a packed layer back to dense (K', V') [B, S'_max, F] on the device."""
+        p = self.compression_info[layer_idx]
+        return unpack_layer(p)
+
+
+def unpack_layer(p: dict):
+    """Packed layer dict → dense dequantized (K', V'), bit-identical to the fused output."""
+    codes_k, codes_v = p["codes_k"], p["codes_v"]
+    L.require_device(codes_k, codes_v)
+    dev = codes_k.device
+    row_offset = p["row_offset"].contiguous()
+    scale_zp = p["scale_zp"].contiguous()
+    kept_index = p["kept_index"].contiguous()
+    labels = p["labels"].contiguous()
+    B, Sp = kept_index.shape
+    S = labels.shape[1]
+    F = int(p["feature_dim"])
+    dtype = p["dtype"]
+    rows = torch.tensor(p["rows"], dtype=torch.int64, device=dev)
+    bits = (ctypes.c_int32 * 3)(*p["bits"])
+    outs = []
+    for which, codes in ((0, codes_k), (1, codes_v)):
+        out = torch.zeros(B, Sp, F, dtype=dtype, device=dev)
+        if out.numel():
+            L.check(L.lib().rtkv_unpack_dequant(codes.data_ptr(), row_offset.data_ptr(), scale_zp.data_ptr(), which,
+                                                kept_index.data_ptr(), labels.data_ptr(), B, S, Sp, rows.data_ptr(), 1,
+                                                F, L.TORCH_DTYPE_CODE[dtype], bits, out.data_ptr(), Sp * F, F, F,
+                                                L.stream_ptr(dev)), "rtkv_unpack_dequant")
+        outs.append(out)
+    return outs[0], outs[1]
+
+
+class AdaptiveQuantization(nn.Module):
+    """One scale/zero-point per precision class over all of that class's rows; bits by class index
+    (compression_layers.py:96-175)."""
+
+    def __init__(self, feature_dim: int, num_bits_options: list = [2, 4, 8]):
+        super().__init__()
+        self.feature_dim = feature_dim
+        self.num_bits_options = num_bits_options
+        self.quantization_params = {b: {"scale": torch.ones(1), "zero_point": torch.zeros(1)}
+                                    for b in num_bits_options}
+
+    def compute_quantization_params(self, tensor: torch.Tensor, num_bits: int):
+        L.require_device(tensor)
+        x = tensor.contiguous()
+        sz = torch.empty(2, dtype=torch.float32, device=x.device)
+        ws = _workspace(x.device).get(1, 1)
+        L.check(L.lib().rtkv_tensor_quant_params(x.data_ptr(), L.dtype_code(x), 1, x.numel(), None, 0, int(num_bits),
+                                                 sz.data_ptr(), ws.data_ptr(), ws.numel(), L.stream_ptr(x.device)),
+                "rtkv_tensor_quant_params")
+        return sz[0], sz[1]
+
+    def quantize_tensor(self, tensor, num_bits, scale, zero_point):
+        L.require_device(tensor)
+        x = tensor.contiguous()
+        sz = torch.stack([torch.as_tensor(scale, device=x.device).float().reshape(()),
+                          torch.as_tensor(zero_point, device=x.device).float().reshape(())])
+        out = torch.empty_like(x)
+        L.check(L.lib().rtkv_tensor_fake_quant(x.data_ptr(), L.dtype_code(x), 1, x.numel(), None, 0, int(num_bits),
+                                               sz.data_ptr(), out.data_ptr(), L.stream_ptr(x.device)),
+                "rtkv_tensor_fake_quant")
+        return out
+
+    def forward(self, tensor: torch.Tensor, precision_labels: torch.Tensor) -> torch.Tensor:
+        L.require_device(tensor, precision_labels)
+        x = tensor.contiguous()
+        labels = precision_labels.to(torch.uint8).contiguous()
+        n_rows = labels.numel()
+        row_len = x.numel() // max(n_rows, 1)
+        out = torch.zeros_like(x)
+        dev = x.device
+        st = L.stream_ptr(dev)
+        present = torch.bincount(precision_labels.reshape(-1).long().clamp(0, 255), minlength=256).tolist()
+        for level, bits in enumerate(self.num_bits_options):
+            if level > 255 or present[level] == 0:
+                continue
+            sz = torch.empty(2, dtype=torch.float32, device=dev)
+            ws = _workspace(dev).get(1, 1)
+            L.check(L.lib().rtkv_tensor_quant_params(x.data_ptr(), L.dtype_code(x), n_rows, row_len, labels.data_ptr(),
+                                                     level, int(bits), sz.data_ptr(), ws.data_ptr(), ws.numel(), st),
+                    "rtkv_tensor_quant_params")
+            L.check(L.lib().rtkv_tensor_fake_quant(x.data_ptr(), L.dtype_code(x), n_rows, row_len, labels.data_ptr(),
+                                                   level, int(bits), sz.data_ptr(), out.data_ptr(), st),
+                    "rtkv_tensor_fake_quant")
+        return out

@@ -1,0 +1,200 @@
+"""Device-side driver of one layer's compression (the C ABI's rtkv_compress_layer) with reusable
+output buffers.  Everything here is stream-ordered and sync-free except ``LayerResult.stats()``.
+
+This is the layer the reference-mirroring classes (unified_compressor.py etc.) and bench.py use.
+"""
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass
+from typing import Optional
+
+import torch
+
+from . import _lib as L
+
+
+def params_from_config(config, layer_idx: int, prompt_len: int, ratio: float, flags: int) -> L.LayerParams:
+    """rtkv_layer_params for one layer.  ctypes.c_float performs the same double→float32 rounding
+    PyTorch applies to a Python scalar combined with an fp32 tensor."""
+    p = L.LayerParams()
+    p.alpha = float(config.alpha)
+    p.beta = float(config.beta)
+    p.gamma = float(config.gamma)
+    p.layer_weight = float(config.layer_weights[layer_idx])
+    p.theta_h = float(config.theta_h)
+    p.theta_m = float(config.theta_m)
+    p.bits[0] = int(config.low_precision_bits)
+    p.bits[1] = int(config.medium_precision_bits)
+    p.bits[2] = int(config.high_precision_bits)
+    p.prompt_len = int(prompt_len)
+    p.propagation_ratio = float(ratio)
+    p.flags = int(flags)
+    return p
+
+
+def prompt_length(seq_len: int) -> int:
+    """unified_compressor.py:55"""
+    return max(1, min(seq_len // 5, 128))
+
+
+def attn_desc(W: torch.Tensor) -> L.AttnDesc:
+    if W.dim() != 4:
+        raise ValueError(f"attention weights must be [B, H, S, cols], got {tuple(W.shape)}")
+    if W.stride(-1) != 1:
+        raise ValueError("attention weights must have unit stride along the last (key) dimension")
+    d = L.AttnDesc()
+    d.w_dev = W.data_ptr()
+    d.dtype = L.dtype_code(W)
+    d.B, d.H, d.S, d.cols = W.shape
+    d.stride_b, d.stride_h, d.stride_s = W.stride(0), W.stride(1), W.stride(2)
+    return d
+
+
+def kv_desc(K: torch.Tensor, V: torch.Tensor, layout: str = "bsf", heads: Optional[int] = None) -> L.KVDesc:
+    """layout 'bsf': [B, S, F] (the reference's compress_layer_kv_cache input);
+    layout 'bhsd': [B, H, S, D] (the model-native layout, no transpose copy)."""
+    if K.shape != V.shape or K.dtype != V.dtype or K.stride() != V.stride():
+        raise ValueError("key and value states must have identical shape, dtype and strides")
+    d = L.KVDesc()
+    d.k_dev, d.v_dev = K.data_ptr(), V.data_ptr()
+    d.dtype = L.dtype_code(K)
+    if layout == "bsf":
+        if K.dim() != 3 or K.stride(-1) != 1:
+            raise ValueError("bsf layout needs [B, S, F] with unit feature stride")
+        B, S, F = K.shape
+        d.B, d.S, d.H, d.D = B, S, 1, F
+        d.stride_b, d.stride_s, d.stride_h = K.stride(0), K.stride(1), F
+    elif layout == "bhsd":
+        if K.dim() != 4 or K.stride(-1) != 1:
+            raise ValueError("bhsd layout needs [B, H, S, D] with unit head_dim stride")
+        B, H, S, D = K.shape
+        d.B, d.S, d.H, d.D = B, S, H, D
+        d.stride_b, d.stride_s, d.stride_h = K.stride(0), K.stride(2), K.stride(1)
+    else:
+        raise ValueError(layout)
+    return d
+
+
+@dataclass
+class LayerStats:
+    max_kept: int
+    total_packed_bytes: int
+    score_sum: float
+    score_m2: float
+    score_min: float
+    score_max: float
+    error_flags: int
+    batch: list  # per batch row dicts
+
+
+def decode_stats(raw: bytes, B: int) -> LayerStats:
+    h = L.LayerStatsHeader.from_buffer_copy(raw[: ctypes.sizeof(L.LayerStatsHeader)])
+    rows = []
+    off = ctypes.sizeof(L.LayerStatsHeader)
+    for _ in range(B):
+        s = L.BatchStats.from_buffer_copy(raw[off: off + ctypes.sizeof(L.BatchStats)])
+        off += ctypes.sizeof(L.BatchStats)
+        rows.append(dict(class_count=list(s.class_count), kept=s.kept, kept_class=list(s.kept_class),
+                         cost_units=s.cost_units, packed_bytes=s.packed_bytes, fallback=bool(s.fallback),
+                         kept_score_sum=s.kept_score_sum))
+    return LayerStats(h.max_kept, h.total_packed_bytes, h.score_sum, h.score_m2, h.score_min, h.score_max,
+                      h.error_flags, rows)
+
+
+class Workspace:
+    """Caller-owned scratch for the C ABI, grown on demand (one per device)."""
+
+    def __init__(self, device):
+        self.device = torch.device(device)
+        self.buf = torch.empty(0, dtype=torch.uint8, device=self.device)
+
+    def get(self, B: int, S: int) -> torch.Tensor:
+        need = int(L.lib().rtkv_workspace_size(B, S))
+        if self.buf.numel() < need:
+            self.buf = torch.empty(need, dtype=torch.uint8, device=self.device)
+        return self.buf
+
+
+class LayerBuffers:
+    """Output buffers of one compressed layer, sized for B batch rows of S tokens (capacity = S)."""
+
+    def __init__(self, B: int, S: int, F: int, dtype: torch.dtype, device, bits, emit_dequant=True, emit_packed=True):
+        self.B, self.S, self.F, self.dtype = B, S, F, dtype
+        dev = torch.device(device)
+        self.scores = torch.empty(B, S, dtype=torch.float32, device=dev)
+        self.labels = torch.empty(B, S, dtype=torch.uint8, device=dev)
+        self.mask = torch.empty(B, S, dtype=torch.uint8, device=dev)
+        self.kept_index = torch.empty(B, S, dtype=torch.int32, device=dev)
+        self.stats = torch.empty(L.stats_bytes(B), dtype=torch.uint8, device=dev)
+        self.k_out = torch.empty(B * S * F, dtype=dtype, device=dev) if emit_dequant else None
+        self.v_out = torch.empty(B * S * F, dtype=dtype, device=dev) if emit_dequant else None
+        if emit_packed:
+            b3 = (ctypes.c_int32 * 3)(*bits)
+            cap = int(L.lib().rtkv_packed_capacity(B, S, F, L.TORCH_DTYPE_CODE[dtype], b3))
+            self.packed_k = torch.empty(max(cap, 1), dtype=torch.uint8, device=dev)
+            self.packed_v = torch.empty(max(cap, 1), dtype=torch.uint8, device=dev)
+            self.packed_capacity = cap
+            self.row_offset = torch.empty(B, S, dtype=torch.int64, device=dev)
+            self.scale_zp = torch.empty(B, S, 4, dtype=torch.float32, device=dev)
+        else:
+            self.packed_k = self.packed_v = self.row_offset = self.scale_zp = None
+            self.packed_capacity = 0
+
+    def matches(self, B, S, F, dtype, emit_dequant, emit_packed) -> bool:
+        return (self.B, self.S, self.F, self.dtype) == (B, S, F, dtype) and \
+            (self.k_out is not None) == emit_dequant and (self.packed_k is not None) == emit_packed
+
+    def out_struct(self, packed_batch_rows: bool = True) -> L.LayerOut:
+        o = L.LayerOut()
+        o.k_out_dev, o.v_out_dev = L.ptr(self.k_out), L.ptr(self.v_out)
+        # dequant rows packed back to back at the runtime row count: a contiguous [B, S', F] view
+        o.o_stride_b = -1 if packed_batch_rows else self.S * self.F
+        o.o_stride_s, o.o_stride_h = self.F, self.F
+        o.row_capacity = self.S
+        o.scores_dev, o.labels_dev, o.mask_dev = L.ptr(self.scores), L.ptr(self.labels), L.ptr(self.mask)
+        o.kept_index_dev = L.ptr(self.kept_index)
+        o.packed_k_dev, o.packed_v_dev = L.ptr(self.packed_k), L.ptr(self.packed_v)
+        o.packed_capacity = self.packed_capacity
+        o.row_offset_dev, o.scale_zp_dev = L.ptr(self.row_offset), L.ptr(self.scale_zp)
+        o.stats_dev = L.ptr(self.stats)
+        return o
+
+
+class LayerResult:
+    """Device outputs of one rtkv_compress_layer call; ``stats()`` is the single host sync."""
+
+    def __init__(self, bufs: LayerBuffers, B: int):
+        self.bufs = bufs
+        self.B = B
+        self._stats: Optional[LayerStats] = None
+
+    def stats(self) -> LayerStats:
+        if self._stats is None:
+            raw = self.bufs.stats.cpu().numpy().tobytes()  # D2H copy on the current stream + sync
+            self._stats = decode_stats(raw, self.B)
+        return self._stats
+
+    def kv(self):
+        """Dequantized (K', V') as contiguous [B, S'_max, F] views (reference return value)."""
+        st = self.stats()
+        n = self.B * st.max_kept * self.bufs.F
+        shape = (self.B, st.max_kept, self.bufs.F)
+        return self.bufs.k_out[:n].view(shape), self.bufs.v_out[:n].view(shape)
+
+
+def compress_layer(K, V, W, params: L.LayerParams, bufs: LayerBuffers, workspace: Workspace,
+                   layout: str = "bsf", stream: Optional[int] = None) -> LayerResult:
+    """Enqueue aggregation → scores/labels/selection → quantize+pack+compact for one layer."""
+    L.require_device(K, V, W)
+    kd = kv_desc(K, V, layout)
+    wd = attn_desc(W)
+    if wd.B != kd.B or wd.S != kd.S:
+        raise ValueError(f"attention weights {tuple(W.shape)} do not match key states {tuple(K.shape)}")
+    ws = workspace.get(kd.B, kd.S)
+    out = bufs.out_struct()
+    st = L.stream_ptr(K.device) if stream is None else stream
+    rc = L.lib().rtkv_compress_layer(ctypes.byref(kd), ctypes.byref(wd), ctypes.byref(params), ctypes.byref(out),
+                                     ws.data_ptr(), ws.numel(), st)
+    L.check(rc, "rtkv_compress_layer")
+    return LayerResult(bufs, kd.B)

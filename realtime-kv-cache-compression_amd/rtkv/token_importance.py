@@ -1,0 +1,163 @@
+"""Prompt-guided token importance on the GPU.
+
+Mirrors src/compression/token_importance.py of the reference: same classes, method names, argument
+meaning and return dtypes/shapes; every computation runs in librtkv (HIP, gfx950):
+
+    compute_attention_aggregation   token_importance.py:21-47   → rtkv_attention_aggregation
+    normalize_attention_scores      token_importance.py:49-85   → rtkv_minmax_normalize
+    compute_position_bias           token_importance.py:87-110  → rtkv_position_bias
+    compute_context_relevance       token_importance.py:112-132 (a constant fill)
+    compute_importance_scores       token_importance.py:134-176 → aggregation + rtkv_importance_scores
+    LayerWiseImportanceTracker      token_importance.py:178-214
+"""
+from __future__ import annotations
+
+import ctypes
+
+import torch
+
+from . import _lib as L
+from .engine import Workspace, attn_desc, params_from_config
+
+_WORKSPACES = {}
+
+
+def _workspace(device) -> Workspace:
+    key = torch.device(device)
+    if key not in _WORKSPACES:
+        _WORKSPACES[key] = Workspace(key)
+    return _WORKSPACES[key]
+
+
+def _prompt_view(attention_weights: torch.Tensor, prompt_indices: torch.Tensor):
+    """(W, P) such that columns [0, P) of W are W[..., prompt_indices].  The production prompt set
+    is arange(P) (unified_compressor.py:55-56): W is used as is.  Any other index set is gathered
+    on the device first."""
+    P = int(prompt_indices.numel())
+    if P == 0:
+        raise ValueError("prompt_indices must not be empty")
+    idx = prompt_indices.to(attention_weights.device)
+    if attention_weights.shape[-1] >= P and bool(torch.equal(idx, torch.arange(P, device=idx.device,
+                                                                                 dtype=idx.dtype))):
+        W = attention_weights if attention_weights.stride(-1) == 1 else attention_weights.contiguous()
+        return W, P
+    return attention_weights.index_select(-1, idx.long()).contiguous(), P
+
+
+class PromptGuidedImportanceScorer:
+    """s_i = α·Â_P,i·w_l + β·b_pos(i) + γ·r(i)  (token_importance.py:7-19)."""
+
+    def __init__(self, config):
+        self.config = config
+        self.alpha = config.alpha
+        self.beta = config.beta
+        self.gamma = config.gamma
+        self.layer_weights = config.layer_weights
+
+    def compute_attention_aggregation(self, attention_weights: torch.Tensor, prompt_indices: torch.Tensor,
+                                      layer_idx: int) -> torch.Tensor:
+        """[B,H,S,S|P] → [B,S] in the dtype of the attention weights."""
+        L.require_device(attention_weights)
+        W, P = _prompt_view(attention_weights, prompt_indices)
+        B, _, S, _ = W.shape
+        A = torch.empty(B, S, dtype=torch.float32, device=W.device)
+        d = attn_desc(W)
+        L.check(L.lib().rtkv_attention_aggregation(ctypes.byref(d), P, A.data_ptr(), None, 0,
+                                                   L.stream_ptr(W.device)), "rtkv_attention_aggregation")
+        return A.to(W.dtype)
+
+    def normalize_attention_scores(self, attention_scores: torch.Tensor, layer_idx: int) -> torch.Tensor:
+        """Per-row min-max to [0, 1]; rows with max - min ≤ 1e-8 become 0."""
+        L.require_device(attention_scores)
+        x = attention_scores.contiguous()
+        S = x.shape[-1]
+        B = x.numel() // S if S else 0
+        out = torch.empty_like(x)
+        if x.numel():
+            L.check(L.lib().rtkv_minmax_normalize(x.data_ptr(), L.dtype_code(x), B, S, out.data_ptr(),
+                                                  L.stream_ptr(x.device)), "rtkv_minmax_normalize")
+        return out
+
+    def compute_position_bias(self, seq_len: int, device: torch.device) -> torch.Tensor:
+        """b_pos(i) = log(i+1) / log(S) in fp32, zeros when S ≤ 1."""
+        pos = torch.empty(seq_len, dtype=torch.float32, device=device)
+        if seq_len:
+            L.require_device(pos)
+            L.check(L.lib().rtkv_position_bias(seq_len, pos.data_ptr(), L.stream_ptr(pos.device)),
+                    "rtkv_position_bias")
+        return pos
+
+    def compute_context_relevance(self, seq_len: int, prompt_len: int, device: torch.device) -> torch.Tensor:
+        """r(i) = min(1, N_p / N) for every token."""
+        return torch.full((seq_len,), min(1.0, prompt_len / seq_len), device=device)
+
+    def compute_importance_scores(self, attention_weights: torch.Tensor, prompt_indices: torch.Tensor,
+                                  layer_idx: int) -> torch.Tensor:
+        """[B,H,S,S|P] → fp32 [B,S] importance scores."""
+        L.require_device(attention_weights)
+        W, P = _prompt_view(attention_weights, prompt_indices)
+        B, _, S, _ = W.shape
+        dev = W.device
+        A = torch.empty(B, S, dtype=torch.float32, device=dev)
+        scores = torch.empty(B, S, dtype=torch.float32, device=dev)
+        d = attn_desc(W)
+        st = L.stream_ptr(dev)
+        L.check(L.lib().rtkv_attention_aggregation(ctypes.byref(d), P, A.data_ptr(), None, 0, st),
+                "rtkv_attention_aggregation")
+        p = params_from_config(self.config, layer_idx, P, 1.0, 0)
+        ws = _workspace(dev).get(B, S)
+        L.check(L.lib().rtkv_importance_scores(A.data_ptr(), d.dtype, B, S, ctypes.byref(p), scores.data_ptr(),
+                                               ws.data_ptr(), ws.numel(), st), "rtkv_importance_scores")
+        return scores
+
+
+class _HostScoreDict(dict):
+    """layer_idx → scores.  The reference stores ``scores.detach().cpu()`` (token_importance.py:198);
+    here the device tensor is kept and copied to the host on first access, so the hot path does not
+    synchronise for a copy nobody may read."""
+
+    def __getitem__(self, key):
+        v = dict.__getitem__(self, key)
+        if v.device.type != "cpu":
+            v = v.detach().cpu()
+            dict.__setitem__(self, key, v)
+        return v
+
+    def get(self, key, default=None):
+        return self[key] if key in self else default
+
+    def values(self):
+        return [self[k] for k in self.keys()]
+
+    def items(self):
+        return [(k, self[k]) for k in self.keys()]
+
+
+class LayerWiseImportanceTracker:
+    """Importance scores of every layer of the current sequence (token_importance.py:178-214)."""
+
+    def __init__(self, config):
+        self.config = config
+        self.scorer = PromptGuidedImportanceScorer(config)
+        self.layer_scores = _HostScoreDict()
+
+    def update_scores(self, layer_idx: int, attention_weights: torch.Tensor,
+                      prompt_indices: torch.Tensor) -> torch.Tensor:
+        scores = self.scorer.compute_importance_scores(attention_weights, prompt_indices, layer_idx)
+        self.record(layer_idx, scores)
+        return scores
+
+    def record(self, layer_idx: int, scores: torch.Tensor):
+        if not isinstance(self.layer_scores, _HostScoreDict):  # reset_compression_state assigns {}
+            self.layer_scores = _HostScoreDict(self.layer_scores)
+        self.layer_scores[layer_idx] = scores.detach().clone()
+
+    def get_cumulative_scores(self, layer_idx: int):
+        """Mean of the stored scores of layers 0..layer_idx (host tensors, as in the reference)."""
+        if not self.layer_scores:
+            return None
+        total = torch.zeros_like(self.layer_scores[0])
+        for l in range(min(layer_idx + 1, len(self.layer_scores))):
+            if l in self.layer_scores:
+                total += self.layer_scores[l]
+        return total / (layer_idx + 1)

@@ -1,0 +1,206 @@
+"""RealTimePrefillCompressor — the drop-in compressor object for the reference's modified LLaMA.
+
+Mirrors src/compression/unified_compressor.py.  ``model.set_compressor(RealTimePrefillCompressor(cfg))``
+(modified_llama.py:264-268) routes every prefill layer's call (modified_llama.py:113-117) to
+``compress_layer_kv_cache``, which runs the whole layer as three HIP kernels (aggregation, fused
+scores/classes/selection, quantize+pack+compact) with one host synchronisation for the output shape.
+"""
+from __future__ import annotations
+
+import os
+import time
+from typing import Dict, List, Optional, Tuple
+
+import torch
+
+from . import _lib as L
+from .dynamic_quantization import F16_OVERFLOW_MSG, DynamicPrecisionQuantizer
+from .engine import LayerBuffers, Workspace, compress_layer, params_from_config, prompt_length
+from .selective_propagation import SelectiveTokenPropagator
+from .token_importance import LayerWiseImportanceTracker
+
+
+class RealTimePrefillCompressor:
+    """Prompt-guided importance → dynamic precision → selective propagation, per layer."""
+
+    def __init__(self, config, model_config=None, emit_packed: bool = True):
+        self.config = config
+        self.model_config = model_config
+        self.importance_tracker = LayerWiseImportanceTracker(config)
+        self.quantizer = DynamicPrecisionQuantizer(config)
+        self.propagator = SelectiveTokenPropagator(config)
+        self.compression_stats = {}
+        self.layer_states = {}
+        # extension: keep the bit-packed codes of every layer (compression_layers.CompressedKVCache)
+        self.emit_packed = emit_packed
+        self._workspaces: Dict[torch.device, Workspace] = {}
+
+    # ------------------------------------------------------------------ reference API
+    def identify_prompt_tokens(self, input_ids: torch.Tensor, special_tokens: Optional[List[int]] = None):
+        """First max(1, min(S//5, 128)) positions (unified_compressor.py:35-58)."""
+        return torch.arange(prompt_length(input_ids.shape[1]), device=input_ids.device)
+
+    def _bits(self):
+        c = self.config
+        return (int(c.low_precision_bits), int(c.medium_precision_bits), int(c.high_precision_bits))
+
+    def compress_layer_kv_cache(self, key_states: torch.Tensor, value_states: torch.Tensor,
+                                attention_weights: torch.Tensor, input_ids: torch.Tensor,
+                                layer_idx: int) -> Tuple[torch.Tensor, torch.Tensor, Dict]:
+        """K, V [B,S,F] + attention [B,H,S,S] (or its [B,H,S,P] prompt columns) → (K', V', info).
+
+        K', V' are the dequantized kept rows in ascending token order, zero-padded across the batch,
+        in the input dtype — bit-identical to the reference."""
+        start_time = time.time()
+        L.require_device(key_states, value_states, attention_weights)
+        K = key_states if key_states.stride(-1) == 1 else key_states.contiguous()
+        V = value_states if value_states.stride() == K.stride() else value_states.contiguous()
+        if V.stride() != K.stride():
+            K, V = K.contiguous(), V.contiguous()
+        W = attention_weights if attention_weights.stride(-1) == 1 else attention_weights.contiguous()
+        B, S, F = K.shape
+        P = prompt_length(S)
+        ratio = self.propagator.get_layer_propagation_ratio(layer_idx)
+        bits = self._bits()
+        emit_packed = self.emit_packed and all(L.lib().rtkv_field_width(L.dtype_code(K), b) > 0 for b in bits)
+        if K.dtype == torch.float16 and any((1 << b) - 1 > 65504 for b in bits):
+            emit_packed = False
+        flags = L.EMIT_DEQUANT | (L.EMIT_PACKED if emit_packed else 0)
+        params = params_from_config(self.config, layer_idx, P, ratio, flags)
+        bufs = LayerBuffers(B, S, F, K.dtype, K.device, bits, emit_dequant=True, emit_packed=emit_packed)
+        ws = self._workspaces.setdefault(K.device, Workspace(K.device))
+        res = compress_layer(K, V, W, params, bufs, ws)
+        st = res.stats()  # the one host sync of the layer
+        if st.error_flags & L.FLAG_F16_QMAX_OVERFLOW:
+            raise RuntimeError(F16_OVERFLOW_MSG)
+        selected_keys, selected_values = res.kv()
+        Sp = st.max_kept
+        scores = bufs.scores
+        self.importance_tracker.record(layer_idx, scores)
+
+        # statistics (unified_compressor.py:143-167)
+        n = B * S
+        original_memory = K.numel() + V.numel()
+        compressed_memory = selected_keys.numel() + selected_values.numel()
+        compression_ratio = compressed_memory / original_memory if original_memory > 0 else 0
+        high = sum(r["class_count"][2] for r in st.batch)
+        medium = sum(r["class_count"][1] for r in st.batch)
+        low = n - high - medium
+        precision_stats = {"high_count": high, "medium_count": medium, "low_count": low,
+                           "high_ratio": high / n, "medium_ratio": medium / n, "low_ratio": low / n}
+        quant_info = {"scales": {}, "zero_points": {}, "bit_assignments": bufs.labels.long().cpu().numpy()}
+        selection_stats = self.propagator._selection_info(scores, st, ratio, S)
+        propagation_info = {"layer_idx": layer_idx, "propagation_ratio": ratio, "original_length": S,
+                            "max_selected_length": Sp, "selection_mask": bufs.mask.bool(),
+                            "selection_stats": selection_stats}
+        std = (st.score_m2 / (n - 1)) ** 0.5 if n > 1 else float("nan")
+        processing_time = time.time() - start_time
+        compression_info = {
+            "layer_idx": layer_idx,
+            "processing_time": processing_time,
+            "original_shape": key_states.shape,
+            "compressed_shape": selected_keys.shape,
+            "compression_ratio": compression_ratio,
+            "memory_savings": 1.0 - compression_ratio,
+            "importance_stats": {"mean_score": st.score_sum / n, "std_score": std,
+                                 "min_score": st.score_min, "max_score": st.score_max},
+            "precision_stats": precision_stats,
+            "quantization_info": quant_info,
+            "propagation_info": propagation_info,
+        }
+        if emit_packed:
+            compression_info["packed"] = {
+                "codes_k": bufs.packed_k[: st.total_packed_bytes],
+                "codes_v": bufs.packed_v[: st.total_packed_bytes],
+                "row_offset": bufs.row_offset[:, :Sp],
+                "scale_zp": bufs.scale_zp[:, :Sp],
+                "kept_index": bufs.kept_index[:, :Sp],
+                "labels": bufs.labels,
+                "rows": [r["kept"] for r in st.batch],
+                "bits": bits,
+                "dtype": K.dtype,
+                "feature_dim": F,
+            }
+        self.layer_states[layer_idx] = compression_info
+        return selected_keys, selected_values, compression_info
+
+    def get_overall_compression_stats(self) -> Dict:
+        """Aggregate of every processed layer (unified_compressor.py:174-230)."""
+        if not self.layer_states:
+            return {}
+        states = list(self.layer_states.values())
+        total_layers = len(states)
+        total_time = sum(s["processing_time"] for s in states)
+        avg_compression = sum(s["compression_ratio"] for s in states) / total_layers
+        avg_memory_savings = sum(s["memory_savings"] for s in states) / total_layers
+        total_high = sum(s["precision_stats"]["high_count"] for s in states)
+        total_medium = sum(s["precision_stats"]["medium_count"] for s in states)
+        total_low = sum(s["precision_stats"]["low_count"] for s in states)
+        total_tokens = total_high + total_medium + total_low
+        cumulative_compression = 1.0
+        ordered = sorted(states, key=lambda s: s["layer_idx"])
+        if ordered and "original_shape" in ordered[0]:
+            initial = ordered[0]["original_shape"][1]
+            if initial > 0:
+                cumulative_compression = ordered[-1]["compressed_shape"][1] / initial
+        return {
+            "total_layers_processed": total_layers,
+            "total_processing_time": total_time,
+            "avg_processing_time_per_layer": total_time / total_layers,
+            "avg_compression_ratio": avg_compression,
+            "avg_memory_savings": avg_memory_savings,
+            "cumulative_compression": cumulative_compression,
+            "overall_memory_savings": 1.0 - cumulative_compression,
+            "precision_distribution": {
+                "high_ratio": total_high / total_tokens if total_tokens > 0 else 0,
+                "medium_ratio": total_medium / total_tokens if total_tokens > 0 else 0,
+                "low_ratio": total_low / total_tokens if total_tokens > 0 else 0,
+            },
+        }
+
+    def reset_compression_state(self):
+        self.layer_states = {}
+        self.importance_tracker.layer_scores = {}
+
+    def estimate_memory_usage(self) -> Dict[str, float]:
+        try:
+            import psutil
+            mi = psutil.Process(os.getpid()).memory_info()
+            rss, vms = mi.rss, mi.vms
+        except ImportError:  # psutil is optional here
+            rss = vms = 0
+        cuda = torch.cuda.is_available()
+        return {
+            "rss_mb": rss / (1024 * 1024),
+            "vms_mb": vms / (1024 * 1024),
+            "gpu_memory_mb": torch.cuda.memory_allocated() / (1024 * 1024) if cuda else 0,
+            "gpu_memory_cached_mb": torch.cuda.memory_reserved() / (1024 * 1024) if cuda else 0,
+        }
+
+
+# The north_star names the orchestrator "UnifiedCompressor"; the reference class is
+# RealTimePrefillCompressor.  Both names refer to the same object.
+UnifiedCompressor = RealTimePrefillCompressor
+
+
+class CompressionHook:
+    """The reference's forward-hook placeholder (unified_compressor.py:250-286): registers hooks that
+    only log; kept for API completeness."""
+
+    def __init__(self, compressor: RealTimePrefillCompressor):
+        self.compressor = compressor
+        self.hooks = []
+
+    def register_hooks(self, model):
+        for layer_idx, layer in enumerate(model.model.layers):
+            self.hooks.append(layer.register_forward_hook(
+                lambda module, inp, out, l=layer_idx: self._compression_hook(module, inp, out, l)))
+
+    def _compression_hook(self, module, input, output, layer_idx):
+        print(f"Processing layer {layer_idx} with compression")
+        return output
+
+    def remove_hooks(self):
+        for h in self.hooks:
+            h.remove()
+        self.hooks = []

@@ -1,0 +1,26 @@
+#!/usr/bin/env bash
+# GPU session script: every GPU step has its own time limit; stop at the first crash-like exit.
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")}"
+export TMPDIR=/tmp
+mkdir -p gpurun_out
+step() {  # step NAME SECONDS CMD...
+  local name=$1 secs=$2; shift 2
+  echo "== $name ($(date +%T))"
+  timeout -k 10 "$secs" "$@" > "gpurun_out/$name.log" 2>&1
+  local rc=$?
+  echo "   rc=$rc"; tail -n 5 "gpurun_out/$name.log"
+  if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "stopping after $name (rc=$rc)"; exit $rc; fi
+  return 0
+}
+for s in ${STEPS:-smoke pytest bench}; do
+  case $s in
+    smoke)  step smoke 300 python -c "import __graft_entry__ as g; g.build(); g.smoke()" ;;
+    pytest) step pytest_gpu 1200 python -m pytest tests -m gpu -q -x -p no:cacheprovider ;;
+    pytestall) step pytest_gpu 1200 python -m pytest tests -m gpu -q -p no:cacheprovider ;;
+    bench)  step bench 600 python bench.py ${BENCH_ARGS:-} ;;
+    prof)   step rocprof 900 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python3 bench.py --steps 5 --warmup 1 --cpu-baseline-layers 0 ;;
+    pmc)    step pmc 900 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmc -o fetch -- python3 bench.py --steps 2 --warmup 1 --cpu-baseline-layers 0 ;;
+    pmcw)   step pmcw 900 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmcw -o write -- python3 bench.py --steps 2 --warmup 1 --cpu-baseline-layers 0 ;;
+  esac
+done

@@ -2,8 +2,8 @@
 
 Used by the golden generator (tests/golden/gen_golden.py, which feeds the same arrays to the
 reference) and by the tests / bench (which feed them to the HIP path and the oracle).  Only integer
-arithmetic and correctly-rounded IEEE operations (+, *, /, cumsum in a fixed order) are used, so the
-arrays are identical on every x86-64 host regardless of SIMD width.
+arithmetic and correctly-rounded fp32 IEEE operations (+, *, /, a sequential cumsum) are used, so
+the arrays are identical on every x86-64 host regardless of SIMD width.
 
 Shapes follow SURVEY.md §8(d): K, V ~ approx. N(0,1); W prompt slice [B,H,S,P] = a peaked,
 row-normalised positive distribution scaled by a per-row U(0,1) mass and causal inside the prompt.
@@ -29,17 +29,28 @@ def splitmix64(seed: int, n: int, stream: int = 0) -> np.ndarray:
 
 
 def uniform(seed: int, shape, stream: int = 0) -> np.ndarray:
-    """U[0,1) with 24-bit resolution, as float64 (exactly representable in float32)."""
+    """U[0,1) with 24-bit resolution as float32 (exact)."""
     n = int(np.prod(shape))
-    u = (splitmix64(seed, n, stream) >> np.uint64(40)).astype(np.float64) * (2.0 ** -24)
+    u = (splitmix64(seed, n, stream) >> np.uint64(40)).astype(np.float32) * np.float32(2.0 ** -24)
     return u.reshape(shape)
 
 
 def normal(seed: int, shape, stream: int = 0) -> np.ndarray:
-    """Irwin-Hall(4) approximation of N(0,1) (exact float64 arithmetic)."""
+    """Irwin-Hall(4) approximation of N(0,1) from the four 16-bit fields of one draw (float32;
+    the sum is exact, the final scale is one correctly rounded multiply)."""
     n = int(np.prod(shape))
-    u = uniform(seed, (4, n), stream)
-    return (((u[0] + u[1]) + (u[2] + u[3])) - 2.0).reshape(shape) * 1.7320508075688772
+    x = splitmix64(seed, n, stream)
+    m = np.uint64(0xFFFF)
+    acc = (x & m).astype(np.float32)
+    acc += ((x >> np.uint64(16)) & m).astype(np.float32)
+    t = ((x >> np.uint64(32)) & m).astype(np.float32)
+    t += (x >> np.uint64(48)).astype(np.float32)
+    del x
+    acc += t
+    acc *= np.float32(2.0 ** -16)
+    acc -= np.float32(2.0)
+    acc *= np.float32(1.7320508075688772)
+    return acc.reshape(shape)
 
 
 # ----------------------------------------------------------------------------- dtype casting
@@ -58,9 +69,9 @@ def bf16_bits_to_f32(b: np.ndarray) -> np.ndarray:
 DTYPES = {"float32": 0, "float16": 1, "bfloat16": 2}
 
 
-def cast(x64: np.ndarray, dtype: str) -> np.ndarray:
-    """float64 → dtype storage: float32 array, or uint16 bit patterns for half types."""
-    x32 = np.asarray(x64, np.float64).astype(np.float32)
+def cast(x: np.ndarray, dtype: str) -> np.ndarray:
+    """float32/float64 → dtype storage: float32 array, or uint16 bit patterns for half types."""
+    x32 = np.asarray(x).astype(np.float32, copy=False)
     if dtype == "float32":
         return x32
     if dtype == "float16":
@@ -87,14 +98,16 @@ def kv(seed: int, B: int, S: int, F: int, dtype: str, layout: str = "bsf"):
 
 
 def attention_slice(seed: int, B: int, H: int, S: int, P: int, dtype: str, causal: bool = True):
-    """W prompt slice [B,H,S,P] (float64 before cast): u^4 row-normalised (cumsum order) × U(0,1)."""
+    """W prompt slice [B,H,S,P]: u^4 row-normalised (sequential fp32 cumsum) × U(0,1) row mass."""
     u = uniform(seed, (B, H, S, P), 3)
-    raw = (u * u) * (u * u) + 1e-6
+    raw = u * u
+    raw *= raw
+    raw += np.float32(1e-6)
     if causal:
         i = np.arange(S)[:, None]
         p = np.arange(P)[None, :]
-        raw = np.where(p <= i, raw, 0.0)
-    rs = np.cumsum(raw, axis=-1)[..., -1:]
+        raw = np.where(p <= i, raw, np.float32(0.0))
+    rs = np.cumsum(raw, axis=-1, dtype=np.float32)[..., -1:]
     m = uniform(seed, (B, H, S, 1), 4)
     W = (raw / rs) * m
     return cast(W, dtype)
@@ -103,11 +116,11 @@ def attention_slice(seed: int, B: int, H: int, S: int, P: int, dtype: str, causa
 def attention_full(seed: int, B: int, H: int, S: int, dtype: str):
     """Full [B,H,S,S] non-causal row-stochastic W (small shapes only, reference test style)."""
     u = uniform(seed, (B, H, S, S), 5)
-    raw = (u * u) + 1e-3
-    rs = np.cumsum(raw, axis=-1)[..., -1:]
+    raw = u * u + np.float32(1e-3)
+    rs = np.cumsum(raw, axis=-1, dtype=np.float32)[..., -1:]
     return cast(raw / rs, dtype)
 
 
 def scores_like(seed: int, B: int, S: int) -> np.ndarray:
     """float32 importance-like scores in [0, 1] with realistic tie structure."""
-    return uniform(seed, (B, S), 6).astype(np.float32)
+    return uniform(seed, (B, S), 6)

@@ -1,0 +1,358 @@
+"""GPU parity: the HIP path (librtkv.so through the rtkv mirror classes / C ABI) against the golden
+fixtures generated from the reference and against the oracle.  Bit-exact for scores, classes,
+selection masks, dequantized K'/V' and packed codes; see tests/golden/gen_golden.py for how the
+fixtures were produced.  Run with `pytest -m gpu`."""
+import numpy as np
+import pytest
+import torch
+
+import rtkv_oracle as orc
+import synth
+from conftest import assert_matches, load_case, load_manifest
+
+pytestmark = pytest.mark.gpu
+
+CASES = load_manifest()["cases"]
+TD = {"float32": torch.float32, "float16": torch.float16, "bfloat16": torch.bfloat16}
+
+
+def by_kind(kind):
+    return [c for c in CASES if c["kind"] == kind]
+
+
+@pytest.fixture(scope="module", autouse=True)
+def gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no ROCm device")
+    import rtkv
+    rtkv.build()
+    return torch.device("cuda:0")
+
+
+def dev(stored: np.ndarray, dtype: str) -> torch.Tensor:
+    """storage array (float32 or uint16 bits) → device tensor of `dtype`."""
+    if dtype == "float32":
+        return torch.from_numpy(np.ascontiguousarray(stored, np.float32)).cuda()
+    t = torch.from_numpy(np.ascontiguousarray(stored, np.uint16).view(np.int16)).cuda()
+    return t.view(TD[dtype])
+
+
+def host(t: torch.Tensor) -> np.ndarray:
+    """device tensor → storage array (float32, or uint16 bits for half types)."""
+    t = t.detach().contiguous().cpu()
+    if t.dtype == torch.float32:
+        return t.numpy()
+    return t.view(torch.int16).numpy().view(np.uint16)
+
+
+def config(params: dict, L: int, bits=(2, 4, 8)):
+    import rtkv
+    kw = dict(params)
+    kw.update(low_precision_bits=bits[0], medium_precision_bits=bits[1], high_precision_bits=bits[2],
+              num_hidden_layers=L)
+    if L == 1:
+        kw["layer_weights"] = [1.0]
+    return rtkv.CompressionConfig(**kw)
+
+
+COVERAGE = dict(alpha=0.8, beta=0.1, gamma=0.1, theta_h=0.4, theta_m=0.25)
+
+
+# ----------------------------------------------------------------------------- stages
+@pytest.mark.parametrize("case", by_kind("position_bias"), ids=lambda c: c["name"])
+def test_position_bias(case):
+    import rtkv
+    sc = rtkv.PromptGuidedImportanceScorer(config(COVERAGE, 4))
+    pos = sc.compute_position_bias(case["spec"]["S"], torch.device("cuda"))
+    assert_matches(case, "pos", host(pos), load_case(case))
+
+
+def test_position_bias_exhaustive_up_to_2_20():
+    """Device logf path == torch CPU log for every integer 1..2^20 (incl. the Sleef exceptions)."""
+    import rtkv
+    S = 1 << 20
+    sc = rtkv.PromptGuidedImportanceScorer(config(COVERAGE, 4))
+    pos = host(sc.compute_position_bias(S, torch.device("cuda")))
+    assert np.array_equal(pos, orc.position_bias(S))
+
+
+@pytest.mark.parametrize("case", by_kind("aggregation"), ids=lambda c: c["name"])
+def test_aggregation_scores(case):
+    import rtkv
+    s = case["spec"]
+    arrays = load_case(case)
+    W = (synth.attention_full(s["seed"], s["B"], s["H"], s["S"], s["dtype"]) if s["full"]
+         else synth.attention_slice(s["seed"], s["B"], s["H"], s["S"], s["P"], s["dtype"]))
+    Wd = dev(W, s["dtype"])
+    sc = rtkv.PromptGuidedImportanceScorer(config(COVERAGE, s["L"]))
+    idx = torch.arange(s["P"], device="cuda")
+    A = sc.compute_attention_aggregation(Wd, idx, 0)
+    assert A.dtype == TD[s["dtype"]]
+    assert_matches(case, "A", host(A.float()), arrays)
+    assert_matches(case, "N", host(sc.normalize_attention_scores(A, 0).float()), arrays)
+    for layer in s["layers"]:
+        out = sc.compute_importance_scores(Wd, idx, layer)
+        assert out.dtype == torch.float32
+        assert_matches(case, f"scores_l{layer}", host(out), arrays)
+
+
+@pytest.mark.parametrize("case", by_kind("normalize"), ids=lambda c: c["name"])
+def test_normalize_edges(case):
+    import rtkv
+    arrays = load_case(case)
+    dt = case["spec"]["dtype"]
+    sc = rtkv.PromptGuidedImportanceScorer(config(COVERAGE, 4))
+    N = sc.normalize_attention_scores(dev(arrays["A"], dt), 0)
+    assert_matches(case, "N", host(N.float()), arrays)
+
+
+def quant_inputs(s):
+    K, V = synth.kv(s["seed"], s["B"], s["S"], s["F"], s["dtype"])
+    Kf = synth.to_f32(K, s["dtype"])
+    b, i = s["const_row"]
+    Kf[b, i, :] = Kf[b, i, 0]
+    return synth.cast(Kf.astype(np.float64), s["dtype"]), V
+
+
+@pytest.mark.parametrize("case", by_kind("quant"), ids=lambda c: c["name"])
+def test_mixed_precision_quant(case):
+    import rtkv
+    s = case["spec"]
+    arrays = load_case(case)
+    K, V = quant_inputs(s)
+    q = rtkv.DynamicPrecisionQuantizer(config(dict(COVERAGE, theta_h=s["theta"][0], theta_m=s["theta"][1]), 4,
+                                              s["bits"]))
+    scores = torch.from_numpy(synth.scores_like(s["seed"], s["B"], s["S"])).cuda()
+    labels, stats = q.assign_precision_levels(scores)
+    assert labels.dtype == torch.int64
+    assert_matches(case, "labels", labels.cpu().numpy().astype(np.uint8), arrays)
+    assert [stats["low_count"], stats["medium_count"], stats["high_count"]] == \
+        [case["scalars"]["low"], case["scalars"]["medium"], case["scalars"]["high"]]
+    kq, vq, info = q.apply_mixed_precision_quantization(dev(K, s["dtype"]), dev(V, s["dtype"]), labels)
+    assert "bit_assignments" in info
+    assert_matches(case, "k_q", host(kq), arrays)
+    assert_matches(case, "v_q", host(vq), arrays)
+
+
+def test_f16_16bit_raises_like_the_reference():
+    import rtkv
+    case = by_kind("quant_error")[0]
+    s = case["spec"]
+    K, V = synth.kv(s["seed"], s["B"], s["S"], s["F"], "float16")
+    q = rtkv.DynamicPrecisionQuantizer(config(COVERAGE, 4, s["bits"]))
+    labels = torch.tensor(s["labels"], device="cuda")
+    with pytest.raises(RuntimeError, match="c10::Half without overflow"):
+        q.apply_mixed_precision_quantization(dev(K, "float16"), dev(V, "float16"), labels)
+
+
+def test_tensor_quant_helpers_match_oracle():
+    import rtkv
+    q = rtkv.DynamicPrecisionQuantizer(config(COVERAGE, 4))
+    for dt in ["float32", "float16", "bfloat16"]:
+        x = synth.cast(synth.normal(42, (3, 50)), dt)
+        for bits in (2, 4, 8):
+            sc, zp = q.get_quantization_params(dev(x, dt), bits)
+            osc, ozp = orc.quant_params(x, synth.DTYPES[dt], bits)
+            assert float(sc) == osc and float(zp) == ozp
+            out = q.quantize_tensor(dev(x, dt), bits, sc, zp)
+            _, ref = orc.fake_quant(x, synth.DTYPES[dt], bits, osc, ozp)
+            assert np.array_equal(host(out), ref)
+
+
+def test_adaptive_quantization_matches_per_class_oracle():
+    import rtkv
+    for dt in ["float32", "bfloat16"]:
+        x = synth.cast(synth.normal(7, (2, 20, 32)), dt)
+        labels = (synth.uniform(8, (2, 20)) * 3).astype(np.int64)
+        aq = rtkv.AdaptiveQuantization(32)
+        out = host(aq(dev(x, dt), torch.from_numpy(labels).cuda()))
+        xf = synth.to_f32(x, dt)
+        for level, bits in enumerate([2, 4, 8]):
+            rows = labels.reshape(-1) == level
+            if not rows.any():
+                continue
+            sub = synth.cast(xf.reshape(-1, 32)[rows].astype(np.float64), dt)
+            sc, zp = orc.quant_params(sub, synth.DTYPES[dt], bits)
+            _, ref = orc.fake_quant(sub, synth.DTYPES[dt], bits, sc, zp)
+            assert np.array_equal(out.reshape(-1, 32)[rows], ref)
+
+
+@pytest.mark.parametrize("case", by_kind("select"), ids=lambda c: c["name"])
+def test_selection(case):
+    import rtkv
+    s = case["spec"]
+    arrays = load_case(case)
+    cfg = config(dict(COVERAGE, theta_h=s["theta"][0], theta_m=s["theta"][1]), s["L"], s["bits"])
+    scores_np = synth.scores_like(s["seed"], s["B"], s["S"])
+    scores = torch.from_numpy(scores_np).cuda()
+    labels = torch.from_numpy(arrays["labels"].astype(np.int64)).cuda()
+    prop = rtkv.SelectiveTokenPropagator(cfg)
+    if s.get("fallback"):
+        cfg.early_layer_ratio = cfg.middle_layer_ratio = cfg.later_layer_ratio = s["ratio"]
+        prop = rtkv.SelectiveTokenPropagator(cfg)
+        K, V = synth.kv(s["seed"], s["B"], s["S"], 16, "float32")
+        ks, vs, ss, ls, info = prop.apply_token_selection(dev(K, "float32"), dev(V, "float32"), scores, labels, 0)
+        mask = info["selection_mask"].cpu().numpy().astype(np.uint8)
+        assert info["max_selected_length"] == case["scalars"]["max_selected"]
+        if not s["tie_ambiguous"]:
+            assert_matches(case, "mask", mask, arrays)
+            assert_matches(case, "k_sel", host(ks), arrays)
+        return
+    mask, info = prop.select_tokens_with_budget(scores, labels, s["ratio"], s["layer"])
+    mask = mask.cpu().numpy().astype(np.uint8)
+    omask, kept, _, _ = orc.select(scores_np, arrays["labels"], s["bits"], s["ratio"])
+    assert np.array_equal(mask, omask)  # stable tie order, always
+    if not s["tie_ambiguous"]:
+        assert_matches(case, "mask", mask, arrays)
+        assert info["selected_counts"] == case["scalars"]["selected_counts"]
+
+
+# ----------------------------------------------------------------------------- full layer
+def layer_inputs(s):
+    F = s["Hkv"] * s["D"]
+    K, V = synth.kv(s["seed"], s["B"], s["S"], F, s["dtype"])
+    W = synth.attention_slice(s["seed"], s["B"], s["H"], s["S"], s["P"], s["dtype"])
+    return K, V, W
+
+
+def layer_config(s):
+    cfg = config(s["params"], s["L"], s["bits"])
+    if s["no_selection"]:
+        cfg.early_layer_ratio = cfg.middle_layer_ratio = cfg.later_layer_ratio = 1.0
+    return cfg
+
+
+@pytest.mark.parametrize("case", by_kind("layer"), ids=lambda c: c["name"])
+def test_compress_layer_kv_cache(case):
+    import rtkv
+    s = case["spec"]
+    arrays = load_case(case)
+    K, V, W = layer_inputs(s)
+    comp = rtkv.RealTimePrefillCompressor(layer_config(s))
+    Kd, Vd, Wd = dev(K, s["dtype"]), dev(V, s["dtype"]), dev(W, s["dtype"])
+    ids = torch.zeros(s["B"], s["S"], dtype=torch.long, device="cuda")
+    if s["no_selection"]:
+        scores = comp.importance_tracker.update_scores(s["layer"], Wd, comp.identify_prompt_tokens(ids))
+        labels, _ = comp.quantizer.assign_precision_levels(scores)
+        k2, v2, _ = comp.quantizer.apply_mixed_precision_quantization(Kd, Vd, labels)
+        assert_matches(case, "scores", host(scores), arrays)
+        assert_matches(case, "k_out", host(k2), arrays)
+        assert_matches(case, "v_out", host(v2), arrays)
+        return
+    k2, v2, info = comp.compress_layer_kv_cache(Kd, Vd, Wd, ids, s["layer"])
+    assert_matches(case, "scores", comp.importance_tracker.layer_scores[s["layer"]].numpy(), arrays)
+    assert_matches(case, "labels", info["quantization_info"]["bit_assignments"].astype(np.uint8), arrays)
+    mask = info["propagation_info"]["selection_mask"].cpu().numpy().astype(np.uint8)
+    if s["tie_ambiguous"]:
+        pytest.skip("reference selection depends on its unstable argsort tie order")
+    assert_matches(case, "mask", mask, arrays)
+    assert k2.shape[1] == case["scalars"]["max_selected"]
+    assert_matches(case, "k_out", host(k2), arrays)
+    assert_matches(case, "v_out", host(v2), arrays)
+    ps = info["precision_stats"]
+    assert [ps["high_count"], ps["medium_count"], ps["low_count"]] == \
+        [case["scalars"]["high"], case["scalars"]["medium"], case["scalars"]["low"]]
+    assert info["compression_ratio"] == case["scalars"]["compression_ratio"]
+    ist = info["importance_stats"]
+    for k in ("mean_score", "std_score", "min_score", "max_score"):
+        assert abs(ist[k] - case["scalars"][k]) <= 1e-5 * max(1.0, abs(case["scalars"][k])), k
+    # packed codes: decode → identical to the dequantized output, and identical bytes to the oracle
+    if "packed" in info:
+        pk = info["packed"]
+        dk, dv = rtkv.unpack_layer(pk)
+        assert torch.equal(dk.view(torch.int16 if dk.element_size() == 2 else torch.int32),
+                           k2.view(torch.int16 if k2.element_size() == 2 else torch.int32))
+        assert torch.equal(dv.view(torch.int16 if dv.element_size() == 2 else torch.int32),
+                           v2.view(torch.int16 if v2.element_size() == 2 else torch.int32))
+        if s["S"] * s["Hkv"] * s["D"] <= (1 << 22):
+            dt = synth.DTYPES[s["dtype"]]
+            pr = s["params"]
+            o = orc.compress_layer(K, V, dt, W, dt, s["P"], pr["alpha"], pr["beta"], pr["gamma"], s["layer_weight"],
+                                   pr["theta_h"], pr["theta_m"], s["bits"], s["ratio"])
+            assert np.array_equal(pk["codes_k"].cpu().numpy(), o["packed_k"])
+            assert np.array_equal(pk["codes_v"].cpu().numpy(), o["packed_v"])
+            assert np.array_equal(pk["scale_zp"].cpu().numpy(), o["scale_zp"])
+            assert np.array_equal(pk["row_offset"].cpu().numpy(), o["row_offset"])
+
+
+def test_native_bhsd_layout_matches_bsf():
+    """[B,H,S,D] input (no transpose copy) gives the same outputs as the [B,S,H*D] API layout."""
+    import rtkv
+    from rtkv import _lib as L
+    B, H, S, D = 2, 4, 300, 64
+    cfg = config(COVERAGE, 4)
+    K, V = synth.kv(11, B, S, H * D, "float16")
+    W = synth.attention_slice(11, B, 8, S, rtkv.prompt_length(S), "float16")
+    Kd, Vd, Wd = dev(K, "float16"), dev(V, "float16"), dev(W, "float16")
+    Kh = Kd.view(B, S, H, D).transpose(1, 2).contiguous()
+    Vh = Vd.view(B, S, H, D).transpose(1, 2).contiguous()
+    bits = (2, 4, 8)
+    P = rtkv.prompt_length(S)
+    outs = []
+    for layout, (k, v) in (("bsf", (Kd, Vd)), ("bhsd", (Kh, Vh))):
+        p = rtkv.params_from_config(cfg, 1, P, 0.6, L.EMIT_DEQUANT | L.EMIT_PACKED)
+        bufs = rtkv.LayerBuffers(B, S, H * D, torch.float16, "cuda", bits)
+        res = rtkv.compress_layer(k, v, Wd, p, bufs, rtkv.Workspace("cuda"), layout=layout)
+        kk, vv = res.kv()
+        outs.append((kk.clone(), vv.clone(), bufs.packed_k[: res.stats().total_packed_bytes].clone()))
+    assert torch.equal(outs[0][0].view(torch.int16), outs[1][0].view(torch.int16))
+    assert torch.equal(outs[0][1].view(torch.int16), outs[1][1].view(torch.int16))
+    assert torch.equal(outs[0][2], outs[1][2])
+
+
+# ----------------------------------------------------------------------------- full-size properties
+@pytest.mark.parametrize("S,dtype,ratio", [(16384, "float16", 0.6), (65536, "float16", 0.4),
+                                           (32768, "bfloat16", 0.8)])
+def test_full_size_properties(S, dtype, ratio):
+    """BASELINE sizes: closed-form greedy counts, ascending order, budget, pack→unpack == dequant,
+    and sampled rows re-quantized by the oracle."""
+    import rtkv
+    from rtkv import _lib as L
+    H, D = 32, 128
+    F = H * D
+    cfg = config(COVERAGE, 32)
+    P = rtkv.prompt_length(S)
+    K, V = synth.kv(5000 + S, 1, S, F, dtype)
+    W = synth.attention_slice(5000 + S, 1, H, S, P, dtype)
+    Kd, Vd, Wd = dev(K, dtype), dev(V, dtype), dev(W, dtype)
+    del W
+    p = rtkv.params_from_config(cfg, 3, P, ratio, L.EMIT_DEQUANT | L.EMIT_PACKED)
+    bufs = rtkv.LayerBuffers(1, S, F, TD[dtype], "cuda", (2, 4, 8))
+    res = rtkv.compress_layer(Kd, Vd, Wd, p, bufs, rtkv.Workspace("cuda"))
+    st = res.stats()
+    k2, v2 = res.kv()
+    row = st.batch[0]
+    n = row["class_count"]
+    # closed form of the greedy (selective_propagation.py:119-131)
+    U = int(np.floor(8.0 * (S * ratio)))
+    used, want = 0, [0, 0, 0]
+    for g, b in ((2, 8), (1, 4), (0, 2)):
+        want[g] = min(n[g], (U - used) // b)
+        used += want[g] * b
+    assert row["kept_class"] == want and row["kept"] == sum(want) == st.max_kept
+    assert row["cost_units"] == used <= U
+    kept = bufs.kept_index[0, : row["kept"]].cpu().numpy()
+    assert np.all(np.diff(kept) > 0)
+    scores = bufs.scores[0].cpu().numpy()
+    labels = bufs.labels[0].cpu().numpy()
+    # every kept token of class g scores >= every dropped token of class g
+    mask = np.zeros(S, bool)
+    mask[kept] = True
+    for g in range(3):
+        ks, ds = scores[mask & (labels == g)], scores[~mask & (labels == g)]
+        if ks.size and ds.size:
+            assert ks.min() >= ds.max()
+    dk, dv = rtkv.unpack_layer(dict(codes_k=bufs.packed_k, codes_v=bufs.packed_v, row_offset=bufs.row_offset[:, :st.max_kept],
+                                    scale_zp=bufs.scale_zp[:, :st.max_kept], kept_index=bufs.kept_index[:, :st.max_kept],
+                                    labels=bufs.labels, rows=[row["kept"]], bits=(2, 4, 8), dtype=TD[dtype],
+                                    feature_dim=F))
+    assert torch.equal(dk.view(torch.int16), k2.view(torch.int16))
+    assert torch.equal(dv.view(torch.int16), v2.view(torch.int16))
+    rng = np.random.default_rng(0)
+    k2h = host(k2)[0]
+    for r in rng.choice(row["kept"], size=16, replace=False):
+        i = kept[r]
+        bits = (2, 4, 8)[labels[i]]
+        sc, zp = orc.quant_params(K[0, i], synth.DTYPES[dtype], bits)
+        _, ref = orc.fake_quant(K[0, i], synth.DTYPES[dtype], bits, sc, zp)
+        assert np.array_equal(k2h[r], ref)
