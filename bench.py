@@ -110,6 +110,7 @@ class Job:
             else:
                 kd, wd = rtkv.engine.kv_desc(K, V), rtkv.engine.attn_desc(W)
                 out = self.bufs[l].out_struct()
+                out.o_stride_h = kd.D
                 ev = (ctypes.c_void_p * 4)(*[e.cuda_event for e in events[l]])
                 L.check(L.lib().rtkv_compress_layer_events(ctypes.byref(kd), ctypes.byref(wd),
                                                            ctypes.byref(self.params[l]), ctypes.byref(out),

@@ -13,6 +13,8 @@
 // such loads).  Row min/max → wave shuffle reduction; the per-element ops are fp32 ops rounded to
 // the dtype after each op (bit-identical to PyTorch CPU).  8 codes of w bits pack into exactly w
 // bytes, so each lane writes its chunk's codes with one store at byte offset c*w.
+#include <type_traits>
+
 #include "common.h"
 
 namespace rtkv {
@@ -80,7 +82,7 @@ __device__ __forceinline__ void store_bytes(uint8_t* dst, int nbytes, uint64_t p
     for (int k = 0; k < nbytes; ++k) {
       const uint64_t word = k < 8 ? p0 : (k < 16 ? p1 : p2);
       dst[k] = (uint8_t)(word >> ((k & 7) * 8));
-    }
+    }  // (scalar tail path: non-multiple-of-8 rows and unusual widths only)
   }
 }
 
@@ -106,7 +108,7 @@ template <int DT> __device__ __forceinline__ RowParams row_params(float mn, floa
 template <int DT> __device__ __forceinline__ float quant_code(float x, const RowParams& rp) {
   // dynamic_quantization.py:120-121
   const float t = Dt<DT>::rnd(Dt<DT>::rnd(x / rp.scale) + rp.zp);
-  float q = Dt<DT>::rnd(__builtin_rintf(t));
+  float q = __builtin_rintf(t);  // rint of a dtype value is a dtype value: no rounding needed
   q = q < 0.f ? 0.f : q;
   q = q > rp.qmaxT ? rp.qmaxT : q;
   return q;
@@ -116,146 +118,249 @@ template <int DT> __device__ __forceinline__ float dequant(float q, const RowPar
 }
 
 // ------------------------------------------------------------------------------------ K4
-template <int DT, int NCH, bool VEC>
-__global__ __launch_bounds__(256) void quant_rows_kernel(QuantArgs a) {
+// Pack 8 codes of W bits (compile-time W in {2,4,8,16}) and store them at dst (W bytes).
+template <int W> __device__ __forceinline__ void pack_store(uint8_t* dst, const uint32_t (&q)[8], bool aligned) {
+  if constexpr (W == 2) {
+    uint32_t v = 0;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v |= q[e] << (2 * e);
+    if (aligned) *reinterpret_cast<uint16_t*>(dst) = (uint16_t)v;
+    else { dst[0] = (uint8_t)v; dst[1] = (uint8_t)(v >> 8); }
+  } else if constexpr (W == 4) {
+    uint32_t v = 0;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v |= q[e] << (4 * e);
+    if (aligned) *reinterpret_cast<uint32_t*>(dst) = v;
+    else {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) dst[k] = (uint8_t)(v >> (8 * k));
+    }
+  } else if constexpr (W == 8) {
+    const uint32_t lo = q[0] | (q[1] << 8) | (q[2] << 16) | (q[3] << 24);
+    const uint32_t hi = q[4] | (q[5] << 8) | (q[6] << 16) | (q[7] << 24);
+    if (aligned) *reinterpret_cast<uint2*>(dst) = make_uint2(lo, hi);
+    else {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) dst[k] = (uint8_t)((k < 4 ? lo : hi) >> (8 * (k & 3)));
+    }
+  } else {  // W == 16
+    const uint4 v = make_uint4(q[0] | (q[1] << 16), q[2] | (q[3] << 16), q[4] | (q[5] << 16), q[6] | (q[7] << 16));
+    if (aligned) *reinterpret_cast<uint4*>(dst) = v;
+    else {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const uint32_t wv = k == 0 ? v.x : (k == 1 ? v.y : (k == 2 ? v.z : v.w));
+#pragma unroll
+        for (int j = 0; j < 4; ++j) dst[4 * k + j] = (uint8_t)(wv >> (8 * j));
+      }
+    }
+  }
+}
+
+// Row geometry shared by every task of a launch: element f of a row lives at (f / D) * stride_h + f % D.
+// CONTIG (stride_h == D on input and output) makes that plain f.  FULL: the row is exactly NCH*64
+// chunks of 8 (F a multiple of 512), so no lane is idle and packed rows stay 16-byte aligned.
+template <int DT, int NCH, bool CONTIG, bool FULL>
+__global__ __launch_bounds__(256, 2) void quant_rows_kernel(QuantArgs a) {
+  using S_ = typename Dt<DT>::S;
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int nw = gridDim.x * (blockDim.x >> 6);
+  const int B = (int)a.kv.B;
+  const int S = (int)a.kv.S;
+  const int F = (int)(a.kv.H * a.kv.D);
+  const int nch = FULL ? NCH * 64 : (F + 7) >> 3;
+  const int cap = (int)a.out.row_capacity;
+  int R = a.kept_index ? (int)a.stats->max_kept : S;  // rows per batch row
+  if (R > cap) R = cap;
+  const int tasks = 2 * B * R;
+  const rtkv_batch_stats* bst = a.stats ? reinterpret_cast<const rtkv_batch_stats*>(a.stats + 1) : nullptr;
+  const bool emit_deq = a.out.k_out_dev != nullptr;
+  const bool emit_pk = a.out.packed_k_dev != nullptr;
+  const int64_t osb = a.out.o_stride_b >= 0 ? a.out.o_stride_b : (int64_t)R * a.out.o_stride_s;
+  // per-lane in-row offsets of each chunk (task independent)
+  int in_off[NCH], out_off[NCH];
+#pragma unroll
+  for (int k = 0; k < NCH; ++k) {
+    const int f = (k * 64 + lane) * 8;
+    if constexpr (CONTIG) {
+      in_off[k] = f;
+      out_off[k] = f;
+    } else {
+      const int D = (int)a.kv.D;
+      const int h = f / D, d = f - h * D;
+      in_off[k] = (int)(h * a.kv.stride_h) + d;
+      out_off[k] = (int)(h * a.out.o_stride_h) + d;
+    }
+  }
+  auto valid = [&](int k) { return FULL || (k * 64 + lane) < nch; };
+  for (int t = blockIdx.x * (blockDim.x >> 6) + wave; t < tasks; t += nw) {
+    const int which = t & 1;
+    const int rr = t >> 1;
+    const int b = rr / R, r = rr - b * R;
+    const int kept_b = a.kept_index ? (int)bst[b].kept : S;
+    int i = (r < kept_b) ? (a.kept_index ? a.kept_index[(int64_t)b * cap + r] : r) : 0;
+    int lab = (r < kept_b) ? (int)a.labels[(int64_t)b * S + i] : 0;
+    i = __builtin_amdgcn_readfirstlane(i);
+    lab = __builtin_amdgcn_readfirstlane(lab);
+    S_* orow = emit_deq ? static_cast<S_*>(which ? a.out.v_out_dev : a.out.k_out_dev) + b * osb +
+                              (int64_t)r * a.out.o_stride_s
+                        : nullptr;
+    const int64_t sz_idx = ((int64_t)b * cap + r) * 4 + which * 2;
+    if (r >= kept_b || lab > 2) {  // zero padding row (selective_propagation.py:214-222)
+      if (emit_deq) {
+        const Chunk<DT> z = f32_to_chunk<DT>({0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f});
+#pragma unroll
+        for (int k = 0; k < NCH; ++k)
+          if (valid(k)) *reinterpret_cast<Chunk<DT>*>(orow + out_off[k]) = z;
+      }
+      if (a.out.scale_zp_dev && lane < 2) a.out.scale_zp_dev[sz_idx + lane] = 0.f;
+      continue;
+    }
+    const int bits = a.bits[lab];
+    const int w = field_width(DT, bits);
+    const S_* src = static_cast<const S_*>(which ? a.kv.v_dev : a.kv.k_dev) + b * a.kv.stride_b +
+                    (int64_t)i * a.kv.stride_s;
+    // ---- load the whole row once (all chunks in flight), min/max
+    Chunk<DT> raw[NCH];
+#pragma unroll
+    for (int k = 0; k < NCH; ++k)
+      if (valid(k)) raw[k] = *reinterpret_cast<const Chunk<DT>*>(src + in_off[k]);
+    float mn = INFINITY, mx = -INFINITY;
+#pragma unroll
+    for (int k = 0; k < NCH; ++k) {
+      if (valid(k)) {
+        float x[8];
+        chunk_to_f32<DT>(raw[k], x);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) { mn = fminf(mn, x[e]); mx = fmaxf(mx, x[e]); }
+      }
+    }
+    mn = wave_min(mn);
+    mx = wave_max(mx);
+    const RowParams rp = row_params<DT>(mn, mx, bits);
+    if (a.out.scale_zp_dev && lane < 2) a.out.scale_zp_dev[sz_idx + lane] = lane == 0 ? rp.scale : rp.zp;
+    uint8_t* pk = emit_pk ? (which ? a.out.packed_v_dev : a.out.packed_k_dev) + a.out.row_offset_dev[(int64_t)b * cap + r]
+                          : nullptr;
+    // ---- quantize, pack, dequantize, store (one chunk at a time)
+    auto process = [&](auto wtag) {
+      constexpr int W = decltype(wtag)::value;
+      const bool aligned = FULL || (((uintptr_t)pk & 15) == 0 && (nch * W) % 16 == 0);
+#pragma unroll
+      for (int k = 0; k < NCH; ++k) {
+        const int c = k * 64 + lane;
+        __builtin_amdgcn_sched_barrier(0);  // keep one chunk's temporaries live at a time
+        if (!valid(k)) continue;
+        float x[8];
+        chunk_to_f32<DT>(raw[k], x);
+        float d[8];
+        uint32_t qi[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const float q = quant_code<DT>(x[e], rp);
+          d[e] = dequant<DT>(q, rp);
+          qi[e] = (uint32_t)q;
+        }
+        if (emit_pk) pack_store<W>(pk + c * W, qi, aligned);
+        if (emit_deq) *reinterpret_cast<Chunk<DT>*>(orow + out_off[k]) = f32_to_chunk<DT>(d);
+      }
+    };
+    switch (w) {
+      case 2: process(std::integral_constant<int, 2>{}); break;
+      case 4: process(std::integral_constant<int, 4>{}); break;
+      case 8: process(std::integral_constant<int, 8>{}); break;
+      default: process(std::integral_constant<int, 16>{}); break;  // launcher guarantees w in {2,4,8,16}
+    }
+  }
+}
+
+// Generic path: any D, any alignment, any F (scalar element access, partial last chunk).
+template <int DT>
+__global__ __launch_bounds__(256) void quant_rows_generic_kernel(QuantArgs a) {
   using S_ = typename Dt<DT>::S;
   const int lane = threadIdx.x & 63;
   const int64_t gw = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
   const int64_t nw = (int64_t)gridDim.x * (blockDim.x >> 6);
-  const int64_t B = a.kv.B, S = a.kv.S, H = a.kv.H, D = a.kv.D, F = H * D;
+  const int64_t B = a.kv.B, S = a.kv.S, D = a.kv.D, F = a.kv.H * a.kv.D;
   const int64_t nch = (F + 7) >> 3;
   const int64_t cap = a.out.row_capacity;
-  int64_t R = a.kept_index ? a.stats->max_kept : S;  // rows per batch row
+  int64_t R = a.kept_index ? a.stats->max_kept : S;
   if (R > cap) R = cap;
-  const int64_t tasks = 2 * B * R;
   const rtkv_batch_stats* bst = a.stats ? reinterpret_cast<const rtkv_batch_stats*>(a.stats + 1) : nullptr;
   const bool emit_deq = a.out.k_out_dev != nullptr;
   const bool emit_pk = a.out.packed_k_dev != nullptr;
-  for (int64_t t = gw; t < tasks; t += nw) {
+  const int64_t osb = a.out.o_stride_b >= 0 ? a.out.o_stride_b : R * a.out.o_stride_s;
+  for (int64_t t = gw; t < 2 * B * R; t += nw) {
     const int which = (int)(t & 1);
-    const int64_t rr = t >> 1;
-    const int64_t b = rr / R, r = rr - b * R;
+    const int64_t rr = t >> 1, b = rr / R, r = rr - b * R;
     const int64_t kept_b = a.kept_index ? bst[b].kept : S;
-    S_* out = static_cast<S_*>(which ? a.out.v_out_dev : a.out.k_out_dev);
-    const int64_t osb = a.out.o_stride_b >= 0 ? a.out.o_stride_b : R * a.out.o_stride_s;
-    S_* orow = emit_deq ? out + b * osb + r * a.out.o_stride_s : nullptr;
     const int64_t i = (r < kept_b) ? (a.kept_index ? a.kept_index[b * cap + r] : r) : 0;
     const int lab = (r < kept_b) ? a.labels[b * S + i] : 0;
-    if (r >= kept_b || lab > 2) {  // zero padding row (selective_propagation.py:214-222)
-      if (emit_deq) {
-#pragma unroll
-        for (int k = 0; k < NCH; ++k) {
-          const int64_t c = (int64_t)k * 64 + lane;
-          if (c >= nch) break;
-          for (int e = 0; e < 8; ++e) {
-            const int64_t f = c * 8 + e;
-            if (f < F) orow[(f / D) * a.out.o_stride_h + (f % D)] = Dt<DT>::store(0.f);
-          }
-        }
-      }
+    S_* orow = emit_deq ? static_cast<S_*>(which ? a.out.v_out_dev : a.out.k_out_dev) + b * osb + r * a.out.o_stride_s
+                        : nullptr;
+    auto oaddr = [&](int64_t f) { return (f / D) * a.out.o_stride_h + (f % D); };
+    if (r >= kept_b || lab > 2) {
+      if (emit_deq)
+        for (int64_t f = lane; f < F; f += 64) orow[oaddr(f)] = Dt<DT>::store(0.f);
       if (a.out.scale_zp_dev && lane < 2) a.out.scale_zp_dev[(b * cap + r) * 4 + which * 2 + lane] = 0.f;
       continue;
     }
     const int bits = a.bits[lab];
     const int w = field_width(DT, bits);
     const S_* src = static_cast<const S_*>(which ? a.kv.v_dev : a.kv.k_dev) + b * a.kv.stride_b + i * a.kv.stride_s;
-
-    // ---- load the row (one HBM read)
-    float x[NCH][8];
+    auto load = [&](int64_t f) { return Dt<DT>::load(src[(f / D) * a.kv.stride_h + (f % D)]); };
     float mn = INFINITY, mx = -INFINITY;
-    if constexpr (VEC) {
-      Chunk<DT> raw[NCH];
-#pragma unroll
-      for (int k = 0; k < NCH; ++k) {
-        const int64_t c = (int64_t)k * 64 + lane;
-        if (c < nch) {
-          const int64_t f = c * 8;
-          raw[k] = *reinterpret_cast<const Chunk<DT>*>(src + (f / D) * a.kv.stride_h + (f % D));
-        }
-      }
-#pragma unroll
-      for (int k = 0; k < NCH; ++k) {
-        const int64_t c = (int64_t)k * 64 + lane;
-        if (c < nch) {
-          chunk_to_f32<DT>(raw[k], x[k]);
-#pragma unroll
-          for (int e = 0; e < 8; ++e) { mn = fminf(mn, x[k][e]); mx = fmaxf(mx, x[k][e]); }
-        }
-      }
-    } else {
-#pragma unroll
-      for (int k = 0; k < NCH; ++k) {
-        const int64_t c = (int64_t)k * 64 + lane;
-#pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          const int64_t f = c * 8 + e;
-          if (c < nch && f < F) {
-            x[k][e] = Dt<DT>::load(src[(f / D) * a.kv.stride_h + (f % D)]);
-            mn = fminf(mn, x[k][e]);
-            mx = fmaxf(mx, x[k][e]);
-          } else {
-            x[k][e] = 0.f;
-          }
-        }
-      }
-    }
+    for (int64_t f = lane; f < F; f += 64) { const float v = load(f); mn = fminf(mn, v); mx = fmaxf(mx, v); }
     mn = wave_min(mn);
     mx = wave_max(mx);
     const RowParams rp = row_params<DT>(mn, mx, bits);
     if (a.out.scale_zp_dev && lane < 2)
       a.out.scale_zp_dev[(b * cap + r) * 4 + which * 2 + lane] = lane == 0 ? rp.scale : rp.zp;
-    uint8_t* pk = nullptr;
-    if (emit_pk) {
-      pk = (which ? a.out.packed_v_dev : a.out.packed_k_dev) + a.out.row_offset_dev[b * cap + r];
-    }
-    // ---- quantize, pack, dequantize, store
-#pragma unroll
-    for (int k = 0; k < NCH; ++k) {
-      const int64_t c = (int64_t)k * 64 + lane;
-      if (c >= nch) break;
-      float q[8], d[8];
-      uint32_t qi[8];
-#pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        q[e] = quant_code<DT>(x[k][e], rp);
-        d[e] = dequant<DT>(q[e], rp);
-        qi[e] = (uint32_t)q[e];
-      }
+    uint8_t* pk = emit_pk ? (which ? a.out.packed_v_dev : a.out.packed_k_dev) + a.out.row_offset_dev[b * cap + r] : nullptr;
+    for (int64_t c = lane; c < nch; c += 64) {
       const int64_t f0 = c * 8;
       const int nvalid = (F - f0) < 8 ? (int)(F - f0) : 8;
+      uint32_t qi[8];
+      for (int e = 0; e < 8; ++e) {
+        if (e < nvalid) {
+          const float q = quant_code<DT>(load(f0 + e), rp);
+          qi[e] = (uint32_t)q;
+          if (emit_deq) orow[oaddr(f0 + e)] = Dt<DT>::store(dequant<DT>(q, rp));
+        } else {
+          qi[e] = 0u;
+        }
+      }
       if (emit_pk) {
-        if (nvalid < 8)
-          for (int e = nvalid; e < 8; ++e) qi[e] = 0u;
         uint64_t p0, p1, p2;
         pack8(qi, w, p0, p1, p2);
         store_bytes(pk + c * w, (nvalid * w + 7) >> 3, p0, p1, p2);
-      }
-      if (emit_deq) {
-        if constexpr (VEC) {
-          *reinterpret_cast<Chunk<DT>*>(orow + (f0 / D) * a.out.o_stride_h + (f0 % D)) = f32_to_chunk<DT>(d);
-        } else {
-          for (int e = 0; e < nvalid; ++e) {
-            const int64_t f = f0 + e;
-            orow[(f / D) * a.out.o_stride_h + (f % D)] = Dt<DT>::store(d[e]);
-          }
-        }
       }
     }
   }
 }
 
-template <int DT, bool VEC>
-static int launch_quant_vec(const QuantArgs& a, int nch_per_lane, dim3 grid, hipStream_t st) {
-#define RTKV_Q(N)                                                                            \
-  if (nch_per_lane <= N) {                                                                   \
-    hipLaunchKernelGGL((quant_rows_kernel<DT, N, VEC>), grid, dim3(256), 0, st, a);          \
-    RTKV_HIP_CHECK(hipGetLastError());                                                       \
-    return RTKV_OK;                                                                          \
+template <int DT, bool CONTIG>
+static int launch_quant_vec(const QuantArgs& a, int64_t nch, dim3 grid, hipStream_t st) {
+  const int per_lane = (int)((nch + 63) / 64);
+#define RTKV_Q(N)                                                                              \
+  if (nch == (int64_t)N * 64) {                                                                \
+    hipLaunchKernelGGL((quant_rows_kernel<DT, N, CONTIG, true>), grid, dim3(256), 0, st, a);   \
+    RTKV_HIP_CHECK(hipGetLastError());                                                         \
+    return RTKV_OK;                                                                            \
   }
-  RTKV_Q(1) RTKV_Q(2) RTKV_Q(4) RTKV_Q(8) RTKV_Q(10) RTKV_Q(16) RTKV_Q(32)
+  RTKV_Q(8) RTKV_Q(10) RTKV_Q(16) RTKV_Q(4) RTKV_Q(2) RTKV_Q(1)
 #undef RTKV_Q
-  set_error("rtkv: row of more than 16384 elements unsupported");
-  return RTKV_ERR_UNSUPPORTED;
+#define RTKV_Q(N)                                                                              \
+  if (per_lane <= N) {                                                                         \
+    hipLaunchKernelGGL((quant_rows_kernel<DT, N, CONTIG, false>), grid, dim3(256), 0, st, a);  \
+    RTKV_HIP_CHECK(hipGetLastError());                                                         \
+    return RTKV_OK;                                                                            \
+  }
+  RTKV_Q(1) RTKV_Q(2) RTKV_Q(4) RTKV_Q(8) RTKV_Q(16)
+#undef RTKV_Q
+  hipLaunchKernelGGL((quant_rows_generic_kernel<DT>), grid, dim3(256), 0, st, a);
+  RTKV_HIP_CHECK(hipGetLastError());
+  return RTKV_OK;
 }
 
 template <int DT>
@@ -267,7 +372,7 @@ static int launch_quant_dt(const QuantArgs& a, hipStream_t st) {
   const int64_t R = a.kept_index ? (a.out.row_capacity < kv.S ? a.out.row_capacity : kv.S) : kv.S;
   const int64_t tasks = 2 * kv.B * R;
   int64_t blocks = (tasks + 3) / 4;
-  if (blocks > 2048) blocks = 2048;
+  if (blocks > 4096) blocks = 4096;
   if (blocks < 1) blocks = 1;
   const int esz = Dt<DT>::kBytes;
   auto al16 = [](const void* p) { return p == nullptr || ((uintptr_t)p % 16) == 0; };
@@ -276,8 +381,23 @@ static int launch_quant_dt(const QuantArgs& a, hipStream_t st) {
   if (a.out.k_out_dev)
     vec = vec && al16(a.out.k_out_dev) && al16(a.out.v_out_dev) && (a.out.o_stride_s * esz) % 16 == 0 &&
           (a.out.o_stride_h * esz) % 16 == 0 && (a.out.o_stride_b * esz) % 16 == 0;
-  if (vec) return launch_quant_vec<DT, true>(a, per_lane, dim3((unsigned)blocks), st);
-  return launch_quant_vec<DT, false>(a, per_lane, dim3((unsigned)blocks), st);
+  // every in-row offset (and 2·B·R tasks) must fit in 32 bits for the vector kernel
+  const int64_t in_span = (kv.H - 1) * kv.stride_h + kv.D;
+  const int64_t out_span = (kv.H - 1) * a.out.o_stride_h + kv.D;
+  vec = vec && in_span < ((int64_t)1 << 31) && out_span < ((int64_t)1 << 31) && tasks < ((int64_t)1 << 31) &&
+        kv.S < ((int64_t)1 << 31) && a.out.row_capacity < ((int64_t)1 << 31);
+  const bool contig = (kv.H == 1 || kv.stride_h == kv.D) && (!a.out.k_out_dev || kv.H == 1 || a.out.o_stride_h == kv.D);
+  for (int g = 0; g < 3; ++g) {  // the vector kernel packs widths 2/4/8/16 only
+    const int w = field_width(DT, a.bits[g]);
+    vec = vec && (w == 2 || w == 4 || w == 8 || w == 16 || !a.out.packed_k_dev);
+  }
+  if (!vec) {
+    hipLaunchKernelGGL((quant_rows_generic_kernel<DT>), dim3((unsigned)blocks), dim3(256), 0, st, a);
+    RTKV_HIP_CHECK(hipGetLastError());
+    return RTKV_OK;
+  }
+  if (contig) return launch_quant_vec<DT, true>(a, nch, dim3((unsigned)blocks), st);
+  return launch_quant_vec<DT, false>(a, nch, dim3((unsigned)blocks), st);
 }
 
 int launch_quant(const QuantArgs& a, hipStream_t st) {
@@ -288,6 +408,7 @@ int launch_quant(const QuantArgs& a, hipStream_t st) {
   RTKV_REQUIRE(!a.out.packed_k_dev == !a.out.packed_v_dev, "quantize_rows: packed_k and packed_v must match");
   RTKV_REQUIRE(!a.out.packed_k_dev || a.out.row_offset_dev, "quantize_rows: packed output needs row offsets");
   RTKV_REQUIRE(a.out.row_capacity >= 1, "quantize_rows: row_capacity must be >= 1");
+  RTKV_REQUIRE(a.kept_index || a.out.row_capacity >= a.kv.S, "quantize_rows: row_capacity < S without kept_index");
   for (int g = 0; g < 3; ++g) {
     RTKV_REQUIRE(a.bits[g] >= 1 && a.bits[g] <= 16, "quantize_rows: bits must be in [1, 16]");
     if (a.out.packed_k_dev)

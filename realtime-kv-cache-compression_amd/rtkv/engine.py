@@ -193,6 +193,7 @@ def compress_layer(K, V, W, params: L.LayerParams, bufs: LayerBuffers, workspace
         raise ValueError(f"attention weights {tuple(W.shape)} do not match key states {tuple(K.shape)}")
     ws = workspace.get(kd.B, kd.S)
     out = bufs.out_struct()
+    out.o_stride_h = kd.D  # output rows are [H, D] row-major whatever the input layout
     st = L.stream_ptr(K.device) if stream is None else stream
     rc = L.lib().rtkv_compress_layer(ctypes.byref(kd), ctypes.byref(wd), ctypes.byref(params), ctypes.byref(out),
                                      ws.data_ptr(), ws.numel(), st)
