@@ -13,16 +13,17 @@ void set_error(const std::string& msg) { g_last_error = msg; }
 
 static inline size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 
-// Workspace layout: [A: B*S fp32][labels scratch: B*S u8][stats scratch][tensor partials: 8 KiB]
+// Workspace layout: [A: B*S fp32][T2: S fp32][labels scratch: B*S u8][stats scratch][partials: 8 KiB]
 struct Workspace {
   float* A;
+  float* T2;
   uint8_t* labels;
   rtkv_layer_stats* stats;
   float* partial;
 };
 static size_t ws_bytes(int64_t B, int64_t S) {
-  return align_up((size_t)(B * S) * 4, 256) + align_up((size_t)(B * S), 256) + align_up(rtkv_stats_bytes(B), 256) +
-         8192;
+  return align_up((size_t)(B * S) * 4, 256) + align_up((size_t)S * 4, 256) + align_up((size_t)(B * S), 256) +
+         align_up(rtkv_stats_bytes(B), 256) + 8192;
 }
 static int carve(void* ws, size_t bytes, int64_t B, int64_t S, Workspace& w) {
   if (!ws || bytes < ws_bytes(B, S)) {
@@ -32,6 +33,8 @@ static int carve(void* ws, size_t bytes, int64_t B, int64_t S, Workspace& w) {
   char* p = static_cast<char*>(ws);
   w.A = reinterpret_cast<float*>(p);
   p += align_up((size_t)(B * S) * 4, 256);
+  w.T2 = reinterpret_cast<float*>(p);
+  p += align_up((size_t)S * 4, 256);
   w.labels = reinterpret_cast<uint8_t*>(p);
   p += align_up((size_t)(B * S), 256);
   w.stats = reinterpret_cast<rtkv_layer_stats*>(p);
@@ -208,11 +211,12 @@ int rtkv_compress_layer_events(const rtkv_kv_desc* kv, const rtkv_attn_desc* w, 
     return RTKV_OK;
   };
   if ((rc = mark(0))) return rc;
-  rc = launch_aggregation(*w, p->prompt_len, ws.A, st);
+  FinalizeArgs a = finalize_args(p, kv->B, kv->S);
+  rc = launch_aggregation(*w, p->prompt_len, ws.A, st, ws.T2, p->beta, a.logS);
   if (rc) return rc;
   if ((rc = mark(1))) return rc;
-  FinalizeArgs a = finalize_args(p, kv->B, kv->S);
   a.A = ws.A;
+  a.T2 = ws.T2;
   a.a_dtype = w->dtype;
   a.scores = out->scores_dev;
   a.labels = out->labels_dev;

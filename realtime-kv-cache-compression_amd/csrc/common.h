@@ -143,12 +143,16 @@ void set_error(const std::string& msg);
 
 // ------------------------------------------------------------------------------------ launchers
 // (implemented in the .hip translation units; all return rtkv_status)
-int launch_aggregation(const rtkv_attn_desc& w, int P, float* A, hipStream_t st);
+// K1.  Optional t2 output: t2[i] = β·log(i+1)/log(S) (fp32, the position term of the score) written
+// by the batch-row-0 blocks, so K2 needs no transcendental per token.
+int launch_aggregation(const rtkv_attn_desc& w, int P, float* A, hipStream_t st, float* t2 = nullptr,
+                       float beta = 0.f, float logS = 1.f);
 int launch_position_bias(int64_t S, float* pos, hipStream_t st);
 int launch_minmax_normalize(const void* x, int dt, int64_t B, int64_t S, void* out, hipStream_t st);
 
 struct FinalizeArgs {
   const float* A;          // aggregation (mode_scores = 1)
+  const float* T2;         // β·pos per token from K1 (nullable: computed in place)
   int a_dtype;
   float* scores;           // written when mode_scores = 1, read otherwise
   uint8_t* labels;         // written when mode_labels = 1, read otherwise

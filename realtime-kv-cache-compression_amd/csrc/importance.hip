@@ -76,7 +76,8 @@ template <int DT, int VEC>
 __global__ __launch_bounds__(256) void aggregation_vec_kernel(const typename Dt<DT>::S* __restrict__ W,
                                                               int H, int64_t S, int P, int64_t sb,
                                                               int64_t sh, int64_t ss, int TT, int64_t lim,
-                                                              float* __restrict__ A) {
+                                                              float* __restrict__ A, float* __restrict__ t2,
+                                                              float beta, float logS) {
   using S_ = typename Dt<DT>::S;
   using V = typename VecT<DT, VEC>::T;
   extern __shared__ __attribute__((aligned(16))) float smem[];
@@ -169,6 +170,7 @@ __global__ __launch_bounds__(256) void aggregation_vec_kernel(const typename Dt<
       fin = row_sum_ilp4([&](int k) { return x[k]; }, P);
     }
     A[(int64_t)b * S + i] = Dt<DT>::rnd(fin);
+    if (t2 && b == 0) t2[i] = beta * ((S > 1) ? torch_logf((uint32_t)(i + 1)) / logS : 0.f);
   }
 }
 
@@ -177,7 +179,8 @@ template <int DT>
 __global__ __launch_bounds__(256) void aggregation_scalar_kernel(const typename Dt<DT>::S* __restrict__ W,
                                                                  int H, int64_t S, int P, int64_t sb,
                                                                  int64_t sh, int64_t ss, int TT, int64_t lim,
-                                                                 float* __restrict__ A) {
+                                                                 float* __restrict__ A, float* __restrict__ t2,
+                                                                 float beta, float logS) {
   using S_ = typename Dt<DT>::S;
   extern __shared__ __attribute__((aligned(16))) float smem[];
   float* means = smem;
@@ -222,6 +225,7 @@ __global__ __launch_bounds__(256) void aggregation_scalar_kernel(const typename 
       fin = row_sum_ilp4([&](int k) { return x[k]; }, P);
     }
     A[(int64_t)b * S + i] = Dt<DT>::rnd(fin);
+    if (t2 && b == 0) t2[i] = beta * ((S > 1) ? torch_logf((uint32_t)(i + 1)) / logS : 0.f);
   }
 }
 
@@ -234,7 +238,8 @@ static int64_t cascade_limit(int dt, int64_t M) {
 }
 
 template <int DT>
-static int launch_agg_dt(const rtkv_attn_desc& w, int P, float* A, hipStream_t st) {
+static int launch_agg_dt(const rtkv_attn_desc& w, int P, float* A, hipStream_t st, float* t2, float beta,
+                         float logS) {
   using S_ = typename Dt<DT>::S;
   constexpr int VEC = 16 / Dt<DT>::kBytes;
   const S_* W = static_cast<const S_*>(w.w_dev);
@@ -250,20 +255,21 @@ static int launch_agg_dt(const rtkv_attn_desc& w, int P, float* A, hipStream_t s
     const size_t lds = sizeof(float) * (size_t)TT * (P + 8);
     dim3 grid((unsigned)((w.S + TT - 1) / TT), (unsigned)w.B);
     hipLaunchKernelGGL((aggregation_vec_kernel<DT, VEC>), grid, dim3(256), lds, st, W, H, w.S, P,
-                       w.stride_b, w.stride_h, w.stride_s, TT, lim, A);
+                       w.stride_b, w.stride_h, w.stride_s, TT, lim, A, t2, beta, logS);
   } else {
     int TT = 256 / P;
     if (TT < 1) TT = 1;
     const size_t lds = sizeof(float) * (size_t)TT * (P + 8);
     dim3 grid((unsigned)((w.S + TT - 1) / TT), (unsigned)w.B);
     hipLaunchKernelGGL((aggregation_scalar_kernel<DT>), grid, dim3(256), lds, st, W, H, w.S, P,
-                       w.stride_b, w.stride_h, w.stride_s, TT, lim, A);
+                       w.stride_b, w.stride_h, w.stride_s, TT, lim, A, t2, beta, logS);
   }
   RTKV_HIP_CHECK(hipGetLastError());
   return RTKV_OK;
 }
 
-int launch_aggregation(const rtkv_attn_desc& w, int P, float* A, hipStream_t st) {
+int launch_aggregation(const rtkv_attn_desc& w, int P, float* A, hipStream_t st, float* t2, float beta,
+                       float logS) {
   RTKV_REQUIRE(w.w_dev && A, "aggregation: null pointer");
   RTKV_REQUIRE(w.B >= 1 && w.H >= 1 && w.S >= 1, "aggregation: empty shape");
   RTKV_REQUIRE(w.H < (1 << 20), "aggregation: H must be < 2^20");
@@ -271,9 +277,9 @@ int launch_aggregation(const rtkv_attn_desc& w, int P, float* A, hipStream_t st)
   RTKV_REQUIRE(P <= 8192, "aggregation: prompt_len > 8192 unsupported");
   RTKV_REQUIRE(w.B <= 65535, "aggregation: B > 65535 unsupported");
   switch (w.dtype) {
-    case RTKV_F32: return launch_agg_dt<RTKV_F32>(w, P, A, st);
-    case RTKV_F16: return launch_agg_dt<RTKV_F16>(w, P, A, st);
-    case RTKV_BF16: return launch_agg_dt<RTKV_BF16>(w, P, A, st);
+    case RTKV_F32: return launch_agg_dt<RTKV_F32>(w, P, A, st, t2, beta, logS);
+    case RTKV_F16: return launch_agg_dt<RTKV_F16>(w, P, A, st, t2, beta, logS);
+    case RTKV_BF16: return launch_agg_dt<RTKV_BF16>(w, P, A, st, t2, beta, logS);
   }
   RTKV_REQUIRE(false, "aggregation: bad dtype");
 }

@@ -368,7 +368,6 @@ static int launch_quant_dt(const QuantArgs& a, hipStream_t st) {
   const rtkv_kv_desc& kv = a.kv;
   const int64_t F = kv.H * kv.D;
   const int64_t nch = (F + 7) / 8;
-  const int per_lane = (int)((nch + 63) / 64);
   const int64_t R = a.kept_index ? (a.out.row_capacity < kv.S ? a.out.row_capacity : kv.S) : kv.S;
   const int64_t tasks = 2 * kv.B * R;
   int64_t blocks = (tasks + 3) / 4;
@@ -380,7 +379,7 @@ static int launch_quant_dt(const QuantArgs& a, hipStream_t st) {
              (kv.stride_h * esz) % 16 == 0 && (kv.stride_b * esz) % 16 == 0;
   if (a.out.k_out_dev)
     vec = vec && al16(a.out.k_out_dev) && al16(a.out.v_out_dev) && (a.out.o_stride_s * esz) % 16 == 0 &&
-          (a.out.o_stride_h * esz) % 16 == 0 && (a.out.o_stride_b * esz) % 16 == 0;
+          (a.out.o_stride_h * esz) % 16 == 0 && (a.out.o_stride_b < 0 || (a.out.o_stride_b * esz) % 16 == 0);
   // every in-row offset (and 2·B·R tasks) must fit in 32 bits for the vector kernel
   const int64_t in_span = (kv.H - 1) * kv.stride_h + kv.D;
   const int64_t out_span = (kv.H - 1) * a.out.o_stride_h + kv.D;
