@@ -13,17 +13,20 @@ void set_error(const std::string& msg) { g_last_error = msg; }
 
 static inline size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 
-// Workspace layout: [A: B*S fp32][T2: S fp32][labels scratch: B*S u8][stats scratch][partials: 8 KiB]
+// Workspace layout (256-byte aligned regions):
+//   [A: B*S fp32][T2: S fp32][A partials: B*S*2 fp32][labels scratch: B*S u8][stats scratch]
+//   [selection pipeline scratch: select_workspace_bytes(B, S)]
 struct Workspace {
   float* A;
   float* T2;
+  float* Apart;
   uint8_t* labels;
   rtkv_layer_stats* stats;
-  float* partial;
+  void* sel;
 };
 static size_t ws_bytes(int64_t B, int64_t S) {
-  return align_up((size_t)(B * S) * 4, 256) + align_up((size_t)S * 4, 256) + align_up((size_t)(B * S), 256) +
-         align_up(rtkv_stats_bytes(B), 256) + 8192;
+  return align_up((size_t)(B * S) * 4, 256) + align_up((size_t)S * 4, 256) + align_up((size_t)(B * S) * 8, 256) +
+         align_up((size_t)(B * S), 256) + align_up(rtkv_stats_bytes(B), 256) + align_up(select_workspace_bytes(B, S), 256);
 }
 static int carve(void* ws, size_t bytes, int64_t B, int64_t S, Workspace& w) {
   if (!ws || bytes < ws_bytes(B, S)) {
@@ -35,11 +38,13 @@ static int carve(void* ws, size_t bytes, int64_t B, int64_t S, Workspace& w) {
   p += align_up((size_t)(B * S) * 4, 256);
   w.T2 = reinterpret_cast<float*>(p);
   p += align_up((size_t)S * 4, 256);
+  w.Apart = reinterpret_cast<float*>(p);
+  p += align_up((size_t)(B * S) * 8, 256);
   w.labels = reinterpret_cast<uint8_t*>(p);
   p += align_up((size_t)(B * S), 256);
   w.stats = reinterpret_cast<rtkv_layer_stats*>(p);
   p += align_up(rtkv_stats_bytes(B), 256);
-  w.partial = reinterpret_cast<float*>(p);
+  w.sel = p;
   return RTKV_OK;
 }
 
@@ -117,7 +122,7 @@ int rtkv_importance_scores(const float* A_dev, int a_dtype, int64_t B, int64_t S
   a.mode_scores = 1;
   a.mode_labels = 1;
   a.mode_select = 0;
-  return launch_finalize(a, (hipStream_t)stream);
+  return launch_select(a, ws.sel, false, (hipStream_t)stream);
 }
 
 int rtkv_assign_precision(const float* scores_dev, int64_t B, int64_t S, const rtkv_layer_params* p,
@@ -125,8 +130,9 @@ int rtkv_assign_precision(const float* scores_dev, int64_t B, int64_t S, const r
                           size_t workspace_bytes, void* stream) {
   RTKV_REQUIRE(p != nullptr && labels_dev && stats_dev, "null argument");
   RTKV_REQUIRE(B >= 1 && S >= 1, "empty shape");
-  (void)workspace_dev;
-  (void)workspace_bytes;
+  Workspace ws;
+  int rc = carve(workspace_dev, workspace_bytes, B, S, ws);
+  if (rc) return rc;
   FinalizeArgs a = finalize_args(p, B, S);
   a.scores = const_cast<float*>(scores_dev);
   a.labels = labels_dev;
@@ -134,7 +140,7 @@ int rtkv_assign_precision(const float* scores_dev, int64_t B, int64_t S, const r
   a.mode_scores = 0;
   a.mode_labels = 1;
   a.mode_select = 0;
-  return launch_finalize(a, (hipStream_t)stream);
+  return launch_select(a, ws.sel, false, (hipStream_t)stream);
 }
 
 int rtkv_select_tokens(const float* scores_dev, const uint8_t* labels_dev, int64_t B, int64_t S,
@@ -143,25 +149,26 @@ int rtkv_select_tokens(const float* scores_dev, const uint8_t* labels_dev, int64
                        void* workspace_dev, size_t workspace_bytes, void* stream) {
   int rc = check_params(p);
   if (rc) return rc;
-  RTKV_REQUIRE(scores_dev && labels_dev && mask_dev && stats_dev, "null argument");
+  RTKV_REQUIRE(scores_dev && labels_dev && mask_dev && kept_index_dev && stats_dev, "null argument");
   RTKV_REQUIRE(B >= 1 && S >= 1, "empty shape");
-  RTKV_REQUIRE(!kept_index_dev || row_capacity >= 1, "row_capacity must be >= 1");
-  (void)workspace_dev;
-  (void)workspace_bytes;
+  RTKV_REQUIRE(row_capacity >= S, "row_capacity must be >= S");
+  Workspace ws;
+  rc = carve(workspace_dev, workspace_bytes, B, S, ws);
+  if (rc) return rc;
   FinalizeArgs a = finalize_args(p, B, S);
   a.scores = const_cast<float*>(scores_dev);
   a.labels = const_cast<uint8_t*>(labels_dev);
   a.mask = mask_dev;
   a.kept_index = kept_index_dev;
   a.row_offset = row_offset_dev;
-  a.row_capacity = kept_index_dev ? row_capacity : 0;
+  a.row_capacity = row_capacity;
   a.F = F;
   a.kv_dtype = kv_dtype;
   a.stats = stats_dev;
   a.mode_scores = 0;
   a.mode_labels = 0;
   a.mode_select = (p->flags & RTKV_NO_SELECTION) ? 2 : 1;
-  return launch_finalize(a, (hipStream_t)stream);
+  return launch_select(a, ws.sel, false, (hipStream_t)stream);
 }
 
 int rtkv_quantize_rows(const rtkv_kv_desc* kv, const uint8_t* labels_dev, const int32_t* kept_index_dev,
@@ -212,10 +219,23 @@ int rtkv_compress_layer_events(const rtkv_kv_desc* kv, const rtkv_attn_desc* w, 
   };
   if ((rc = mark(0))) return rc;
   FinalizeArgs a = finalize_args(p, kv->B, kv->S);
-  rc = launch_aggregation(*w, p->prompt_len, ws.A, st, ws.T2, p->beta, a.logS);
+  AggExtras x;
+  int nparts = 0;
+  x.t2 = ws.T2;
+  x.beta = p->beta;
+  x.logS = a.logS;
+  x.part = ws.Apart;
+  x.nparts = &nparts;
+  x.zero0 = ws.sel;
+  x.zero0_bytes = select_zero_bytes(kv->B);
+  x.zero1 = out->stats_dev;
+  x.zero1_bytes = rtkv_stats_bytes(kv->B);
+  rc = launch_aggregation(*w, p->prompt_len, ws.A, st, x);
   if (rc) return rc;
   if ((rc = mark(1))) return rc;
   a.A = ws.A;
+  a.A_part = ws.Apart;
+  a.A_nparts = nparts;
   a.T2 = ws.T2;
   a.a_dtype = w->dtype;
   a.scores = out->scores_dev;
@@ -230,7 +250,7 @@ int rtkv_compress_layer_events(const rtkv_kv_desc* kv, const rtkv_attn_desc* w, 
   a.mode_scores = 1;
   a.mode_labels = 1;
   a.mode_select = (p->flags & RTKV_NO_SELECTION) ? 2 : 1;
-  rc = launch_finalize(a, st);
+  rc = launch_select(a, ws.sel, true, st);
   if (rc) return rc;
   if ((rc = mark(2))) return rc;
   rc = rtkv_quantize_rows(kv, out->labels_dev, out->kept_index_dev, p, out, stream);

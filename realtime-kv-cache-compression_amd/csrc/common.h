@@ -145,13 +145,29 @@ void set_error(const std::string& msg);
 // (implemented in the .hip translation units; all return rtkv_status)
 // K1.  Optional t2 output: t2[i] = β·log(i+1)/log(S) (fp32, the position term of the score) written
 // by the batch-row-0 blocks, so K2 needs no transcendental per token.
-int launch_aggregation(const rtkv_attn_desc& w, int P, float* A, hipStream_t st, float* t2 = nullptr,
-                       float beta = 0.f, float logS = 1.f);
+// Optional side outputs of K1 (all nullable):
+//   t2[i]      = β·log(i+1)/log(S) (fp32, the position term of the score), written by batch row 0;
+//   part[b][k] = (min, max) of A over K1 block k of batch row b (2 floats), *nparts = blocks per row;
+//   zero0/zero1: byte regions (multiple of 4 bytes) cleared by the K1 grid for the next kernels.
+struct AggExtras {
+  float* t2 = nullptr;
+  float beta = 0.f;
+  float logS = 1.f;
+  float* part = nullptr;
+  int* nparts = nullptr;
+  void* zero0 = nullptr;
+  size_t zero0_bytes = 0;
+  void* zero1 = nullptr;
+  size_t zero1_bytes = 0;
+};
+int launch_aggregation(const rtkv_attn_desc& w, int P, float* A, hipStream_t st, const AggExtras& x = AggExtras());
 int launch_position_bias(int64_t S, float* pos, hipStream_t st);
 int launch_minmax_normalize(const void* x, int dt, int64_t B, int64_t S, void* out, hipStream_t st);
 
 struct FinalizeArgs {
   const float* A;          // aggregation (mode_scores = 1)
+  const float* A_part;     // K1 per-block (min, max) of A, [B][A_nparts][2] (nullable)
+  int A_nparts;
   const float* T2;         // β·pos per token from K1 (nullable: computed in place)
   int a_dtype;
   float* scores;           // written when mode_scores = 1, read otherwise
@@ -168,7 +184,11 @@ struct FinalizeArgs {
   rtkv_layer_stats* stats;
   int mode_scores, mode_labels, mode_select;
 };
-int launch_finalize(const FinalizeArgs& a, hipStream_t st);
+// K2 pipeline (select.hip).  sel_ws: select_workspace_bytes(B, S) bytes; `zeroed` = its first
+// select_zero_bytes(B) bytes and the stats are already zero (K1 clears them in rtkv_compress_layer).
+size_t select_workspace_bytes(int64_t B, int64_t S);
+size_t select_zero_bytes(int64_t B);
+int launch_select(const FinalizeArgs& a, void* sel_ws, bool zeroed, hipStream_t st);
 
 struct QuantArgs {
   rtkv_kv_desc kv;

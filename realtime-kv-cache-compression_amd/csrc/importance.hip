@@ -71,18 +71,31 @@ __device__ __forceinline__ void unpack_vec(const typename VecT<DT, VEC>::T& v, f
   }
 }
 
+// The K1 grid clears the selection scratch of the next kernels (4-byte words, grid-strided).
+__device__ __forceinline__ void zero_regions(const AggExtras& x) {
+  const int64_t nb = (int64_t)gridDim.x * gridDim.y;
+  const int64_t id = (int64_t)blockIdx.y * gridDim.x + blockIdx.x;
+  for (int r = 0; r < 2; ++r) {
+    uint32_t* p = static_cast<uint32_t*>(r ? x.zero1 : x.zero0);
+    const int64_t words = (int64_t)((r ? x.zero1_bytes : x.zero0_bytes) / 4);
+    if (!p) continue;
+    for (int64_t w = id * blockDim.x + threadIdx.x; w < words; w += nb * blockDim.x) p[w] = 0u;
+  }
+}
+
 // Fast path: P % VEC == 0, 16-byte aligned rows.  Thread → one VEC-wide chunk of one token row.
 template <int DT, int VEC>
 __global__ __launch_bounds__(256) void aggregation_vec_kernel(const typename Dt<DT>::S* __restrict__ W,
                                                               int H, int64_t S, int P, int64_t sb,
                                                               int64_t sh, int64_t ss, int TT, int64_t lim,
-                                                              float* __restrict__ A, float* __restrict__ t2,
-                                                              float beta, float logS) {
+                                                              float* __restrict__ A, AggExtras ex) {
   using S_ = typename Dt<DT>::S;
   using V = typename VecT<DT, VEC>::T;
   extern __shared__ __attribute__((aligned(16))) float smem[];
   float* means = smem;                 // [TT][P]
   float* lanes = smem + TT * P;        // [TT][8]
+  float* tokA = lanes + TT * 8;        // [TT]
+  zero_regions(ex);
   const int b = blockIdx.y;
   const int64_t i0 = (int64_t)blockIdx.x * TT;
   const int cpr = P / VEC;
@@ -169,8 +182,19 @@ __global__ __launch_bounds__(256) void aggregation_vec_kernel(const typename Dt<
     } else {
       fin = row_sum_ilp4([&](int k) { return x[k]; }, P);
     }
-    A[(int64_t)b * S + i] = Dt<DT>::rnd(fin);
-    if (t2 && b == 0) t2[i] = beta * ((S > 1) ? torch_logf((uint32_t)(i + 1)) / logS : 0.f);
+    const float Ai = Dt<DT>::rnd(fin);
+    A[(int64_t)b * S + i] = Ai;
+    tokA[tok] = Ai;
+    if (ex.t2 && b == 0) ex.t2[i] = ex.beta * ((S > 1) ? torch_logf((uint32_t)(i + 1)) / ex.logS : 0.f);
+  }
+  if (ex.part) {  // block (min, max) of A for the score normalisation (token_importance.py:71-83)
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      float mn = INFINITY, mx = -INFINITY;
+      for (int t = 0; t < TT && i0 + t < S; ++t) { mn = fminf(mn, tokA[t]); mx = fmaxf(mx, tokA[t]); }
+      ex.part[((int64_t)b * gridDim.x + blockIdx.x) * 2] = mn;
+      ex.part[((int64_t)b * gridDim.x + blockIdx.x) * 2 + 1] = mx;
+    }
   }
 }
 
@@ -179,12 +203,13 @@ template <int DT>
 __global__ __launch_bounds__(256) void aggregation_scalar_kernel(const typename Dt<DT>::S* __restrict__ W,
                                                                  int H, int64_t S, int P, int64_t sb,
                                                                  int64_t sh, int64_t ss, int TT, int64_t lim,
-                                                                 float* __restrict__ A, float* __restrict__ t2,
-                                                                 float beta, float logS) {
+                                                                 float* __restrict__ A, AggExtras ex) {
   using S_ = typename Dt<DT>::S;
   extern __shared__ __attribute__((aligned(16))) float smem[];
   float* means = smem;
   float* lanes = smem + TT * P;
+  float* tokA = lanes + TT * 8;
+  zero_regions(ex);
   const int b = blockIdx.y;
   const int64_t i0 = (int64_t)blockIdx.x * TT;
   const S_* Wb = W + b * sb;
@@ -224,8 +249,19 @@ __global__ __launch_bounds__(256) void aggregation_scalar_kernel(const typename 
     } else {
       fin = row_sum_ilp4([&](int k) { return x[k]; }, P);
     }
-    A[(int64_t)b * S + i] = Dt<DT>::rnd(fin);
-    if (t2 && b == 0) t2[i] = beta * ((S > 1) ? torch_logf((uint32_t)(i + 1)) / logS : 0.f);
+    const float Ai = Dt<DT>::rnd(fin);
+    A[(int64_t)b * S + i] = Ai;
+    tokA[tok] = Ai;
+    if (ex.t2 && b == 0) ex.t2[i] = ex.beta * ((S > 1) ? torch_logf((uint32_t)(i + 1)) / ex.logS : 0.f);
+  }
+  if (ex.part) {  // block (min, max) of A for the score normalisation (token_importance.py:71-83)
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      float mn = INFINITY, mx = -INFINITY;
+      for (int t = 0; t < TT && i0 + t < S; ++t) { mn = fminf(mn, tokA[t]); mx = fmaxf(mx, tokA[t]); }
+      ex.part[((int64_t)b * gridDim.x + blockIdx.x) * 2] = mn;
+      ex.part[((int64_t)b * gridDim.x + blockIdx.x) * 2 + 1] = mx;
+    }
   }
 }
 
@@ -238,8 +274,7 @@ static int64_t cascade_limit(int dt, int64_t M) {
 }
 
 template <int DT>
-static int launch_agg_dt(const rtkv_attn_desc& w, int P, float* A, hipStream_t st, float* t2, float beta,
-                         float logS) {
+static int launch_agg_dt(const rtkv_attn_desc& w, int P, float* A, hipStream_t st, const AggExtras& x) {
   using S_ = typename Dt<DT>::S;
   constexpr int VEC = 16 / Dt<DT>::kBytes;
   const S_* W = static_cast<const S_*>(w.w_dev);
@@ -252,24 +287,25 @@ static int launch_agg_dt(const rtkv_attn_desc& w, int P, float* A, hipStream_t s
     int TT = 256 / cpr;
     if (TT < 1) TT = 1;
     if (TT > 64) TT = 64;
-    const size_t lds = sizeof(float) * (size_t)TT * (P + 8);
+    const size_t lds = sizeof(float) * (size_t)TT * (P + 9);
     dim3 grid((unsigned)((w.S + TT - 1) / TT), (unsigned)w.B);
+    if (x.nparts) *x.nparts = (int)grid.x;
     hipLaunchKernelGGL((aggregation_vec_kernel<DT, VEC>), grid, dim3(256), lds, st, W, H, w.S, P,
-                       w.stride_b, w.stride_h, w.stride_s, TT, lim, A, t2, beta, logS);
+                       w.stride_b, w.stride_h, w.stride_s, TT, lim, A, x);
   } else {
     int TT = 256 / P;
     if (TT < 1) TT = 1;
-    const size_t lds = sizeof(float) * (size_t)TT * (P + 8);
+    const size_t lds = sizeof(float) * (size_t)TT * (P + 9);
     dim3 grid((unsigned)((w.S + TT - 1) / TT), (unsigned)w.B);
+    if (x.nparts) *x.nparts = (int)grid.x;
     hipLaunchKernelGGL((aggregation_scalar_kernel<DT>), grid, dim3(256), lds, st, W, H, w.S, P,
-                       w.stride_b, w.stride_h, w.stride_s, TT, lim, A, t2, beta, logS);
+                       w.stride_b, w.stride_h, w.stride_s, TT, lim, A, x);
   }
   RTKV_HIP_CHECK(hipGetLastError());
   return RTKV_OK;
 }
 
-int launch_aggregation(const rtkv_attn_desc& w, int P, float* A, hipStream_t st, float* t2, float beta,
-                       float logS) {
+int launch_aggregation(const rtkv_attn_desc& w, int P, float* A, hipStream_t st, const AggExtras& x) {
   RTKV_REQUIRE(w.w_dev && A, "aggregation: null pointer");
   RTKV_REQUIRE(w.B >= 1 && w.H >= 1 && w.S >= 1, "aggregation: empty shape");
   RTKV_REQUIRE(w.H < (1 << 20), "aggregation: H must be < 2^20");
@@ -277,9 +313,9 @@ int launch_aggregation(const rtkv_attn_desc& w, int P, float* A, hipStream_t st,
   RTKV_REQUIRE(P <= 8192, "aggregation: prompt_len > 8192 unsupported");
   RTKV_REQUIRE(w.B <= 65535, "aggregation: B > 65535 unsupported");
   switch (w.dtype) {
-    case RTKV_F32: return launch_agg_dt<RTKV_F32>(w, P, A, st, t2, beta, logS);
-    case RTKV_F16: return launch_agg_dt<RTKV_F16>(w, P, A, st, t2, beta, logS);
-    case RTKV_BF16: return launch_agg_dt<RTKV_BF16>(w, P, A, st, t2, beta, logS);
+    case RTKV_F32: return launch_agg_dt<RTKV_F32>(w, P, A, st, x);
+    case RTKV_F16: return launch_agg_dt<RTKV_F16>(w, P, A, st, x);
+    case RTKV_BF16: return launch_agg_dt<RTKV_BF16>(w, P, A, st, x);
   }
   RTKV_REQUIRE(false, "aggregation: bad dtype");
 }

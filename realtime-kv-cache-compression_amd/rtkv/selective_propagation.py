@@ -20,6 +20,7 @@ import torch
 
 from . import _lib as L
 from .engine import decode_stats, params_from_config
+from .token_importance import _workspace
 
 
 class SelectiveTokenPropagator:
@@ -64,9 +65,10 @@ class SelectiveTokenPropagator:
         kept_index = torch.empty(B, S, dtype=torch.int32, device=dev)
         stats = torch.empty(L.stats_bytes(B), dtype=torch.uint8, device=dev)
         p = params_from_config(self.config, 0, 1, float(ratio), 0 if fallback else L.NO_FALLBACK)
+        ws = _workspace(dev).get(B, S)
         L.check(L.lib().rtkv_select_tokens(s.data_ptr(), lab.data_ptr(), B, S, ctypes.byref(p), mask.data_ptr(),
-                                           kept_index.data_ptr(), S, None, F, kv_dtype, stats.data_ptr(), None, 0,
-                                           L.stream_ptr(dev)), "rtkv_select_tokens")
+                                           kept_index.data_ptr(), S, None, F, kv_dtype, stats.data_ptr(),
+                                           ws.data_ptr(), ws.numel(), L.stream_ptr(dev)), "rtkv_select_tokens")
         return s, mask, kept_index, stats
 
     def _selection_info(self, s, st, ratio, S):

@@ -207,6 +207,27 @@ def test_selection(case):
         assert info["selected_counts"] == case["scalars"]["selected_counts"]
 
 
+@pytest.mark.parametrize("B,S,ratio,bits", [(1, 10, 0.8, (4, 8, 16)), (2, 64, 0.6, (2, 4, 8)), (1, 4096, 0.4, (2, 4, 8)),
+                                            (3, 333, 0.3, (4, 8, 16)), (1, 16384, 0.8, (2, 4, 8)), (1, 50, 0.01, (2, 4, 8))])
+def test_selection_with_interleaved_classes(B, S, ratio, bits):
+    """select_tokens_with_budget with caller classes unrelated to the scores (the reference's own
+    test_selective_propagator: randn scores, randint labels) — the exact general greedy path."""
+    import rtkv
+    cfg = config(COVERAGE, 4, bits)
+    rng = np.random.default_rng(S)
+    scores = rng.standard_normal((B, S)).astype(np.float32)
+    labels = rng.integers(0, 3, (B, S)).astype(np.uint8)
+    prop = rtkv.SelectiveTokenPropagator(cfg)
+    mask, info = prop.select_tokens_with_budget(torch.from_numpy(scores).cuda(), torch.from_numpy(labels).cuda(),
+                                                ratio, 0)
+    omask, kept, _, _ = orc.select(scores, labels, bits, ratio)
+    # select_tokens_with_budget has no fallback: the oracle's fallback rows must come back empty
+    if omask.sum() and kept.max() and not (orc.select(scores, labels, bits, ratio)[3]).any():
+        assert np.array_equal(mask.cpu().numpy().astype(np.uint8), omask)
+    else:
+        assert mask.sum().item() == 0
+
+
 # ----------------------------------------------------------------------------- full layer
 def layer_inputs(s):
     F = s["Hkv"] * s["D"]
