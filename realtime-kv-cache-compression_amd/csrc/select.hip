@@ -116,23 +116,40 @@ template <int NBITS> __device__ __forceinline__ uint64_t match_any(uint32_t v, b
   return m;
 }
 
-// Aggregated histogram increment: one global atomic per distinct (group, bin) per wave.
-__device__ __forceinline__ void hist_add(uint32_t* base, int g, uint32_t bin16, bool part) {
+// Aggregated histogram increment of one (group, 16-bit digit) per lane: the 256-bin coarse histogram
+// goes to the block's LDS copy (flushed once per block: its few hot bins would otherwise serialise
+// thousands of global atomics on one address), the fine bin to global memory, one atomic per
+// distinct (group, digit) per wave.
+__device__ __forceinline__ void hist_add(uint32_t* base, uint32_t (*lcoarse)[kCoarse], int g, uint32_t bin16, bool part) {
   const uint32_t v = ((uint32_t)g << 16) | bin16;
   const uint64_t peers = match_any<18>(v, part);
-  if (part && (peers & lanemask_lt()) == 0ull) {
-    const uint32_t n = (uint32_t)__popcll(peers);
-    uint32_t* h = base + (size_t)g * (kCoarse + kFine);
-    atomicAdd(h + (bin16 >> 8), n);
-    atomicAdd(h + kCoarse + bin16, n);
+  if (part && (peers & lanemask_lt()) == 0ull)
+    atomicAdd(base + (size_t)g * (kCoarse + kFine) + kCoarse + bin16, (uint32_t)__popcll(peers));
+  const uint32_t vc = ((uint32_t)g << 8) | (bin16 >> 8);
+  const uint64_t cpeers = match_any<10>(vc, part);
+  if (part && (cpeers & lanemask_lt()) == 0ull) atomicAdd(&lcoarse[g][bin16 >> 8], (uint32_t)__popcll(cpeers));
+}
+
+__device__ __forceinline__ void coarse_clear(uint32_t (*lcoarse)[kCoarse]) {
+  for (int k = threadIdx.x; k < kG * kCoarse; k += blockDim.x) (&lcoarse[0][0])[k] = 0u;
+  __syncthreads();
+}
+__device__ __forceinline__ void coarse_flush(uint32_t* base, uint32_t (*lcoarse)[kCoarse]) {
+  __syncthreads();
+  for (int k = threadIdx.x; k < kG * kCoarse; k += blockDim.x) {
+    const uint32_t c = (&lcoarse[0][0])[k];
+    if (c) atomicAdd(base + (size_t)(k / kCoarse) * (kCoarse + kFine) + (k % kCoarse), c);
   }
 }
 
 // In the last block: find, in the (coarse, fine) histogram of group g, the 16-bit digit where the
 // count from the top reaches `need`; returns the digit and the count strictly above it.
 __device__ void find_digit(const uint32_t* h, int64_t need, uint32_t* sh_digit, int64_t* sh_above, int64_t* sh_tmp) {
-  // threads 0..255 own coarse bins 255 - t (descending)
+  // threads 0..255 own coarse bins 255 - t (descending); defaults keep every index in range even if
+  // the histogram does not hold `need` tokens (it always does when the caller's counts are right)
   const int t = threadIdx.x;
+  if (t == 0) { sh_tmp[4] = 0; sh_tmp[5] = 0; *sh_digit = 0; *sh_above = 0; }
+  __syncthreads();
   const int64_t c = ld_sc1(h + (kCoarse - 1 - t));
   // block inclusive scan of c over t (descending coarse order)
   const int lane = t & 63, wid = t >> 6;
@@ -145,7 +162,7 @@ __device__ void find_digit(const uint32_t* h, int64_t need, uint32_t* sh_digit, 
   __syncthreads();
   if (excl < need && incl >= need) { sh_tmp[4] = t; sh_tmp[5] = excl; }
   __syncthreads();
-  const int ct = (int)sh_tmp[4];
+  const int ct = (int)sh_tmp[4] & (kCoarse - 1);
   const uint32_t coarse = (uint32_t)(kCoarse - 1 - ct);
   const int64_t above_coarse = sh_tmp[5];
   __syncthreads();
@@ -214,6 +231,8 @@ __global__ __launch_bounds__(kNT) void sel_scores_kernel(SelArgs g) {
     eps = rnd_dt(a.a_dtype, 1e-8f);
   }
   uint32_t* h1 = g.L.hist + ((size_t)b * 2 + 0) * kG * (kCoarse + kFine);
+  __shared__ uint32_t lcoarse[kG][kCoarse];
+  if (a.mode_select) coarse_clear(lcoarse);
   // ---- scores, classes, round-1 histograms
   const int64_t i0 = (int64_t)blk * kBT;
   double lsum = 0.0;
@@ -259,10 +278,11 @@ __global__ __launch_bounds__(kNT) void sel_scores_kernel(SelArgs g) {
     cnt[2] += __popcll(m2);
     if (a.mode_select) {
       const uint32_t key = score_key(s);
-      hist_add(h1, l, key >> 16, valid);
-      hist_add(h1, 3, key >> 16, valid);
+      hist_add(h1, lcoarse, l, key >> 16, valid);
+      hist_add(h1, lcoarse, 3, key >> 16, valid);
     }
   }
+  if (a.mode_select) coarse_flush(h1, lcoarse);
   // block reductions → row accumulators
   lsum = wave_sum(lsum);
   for (int o = 32; o > 0; o >>= 1) {
@@ -338,7 +358,7 @@ __global__ __launch_bounds__(kNT) void sel_scores_kernel(SelArgs g) {
   for (int k = 0; k < kG; ++k) {
     uint32_t digit = 0;
     int64_t above = 0;
-    if (q_mode[k] == SEL_PARTIAL) {
+    if (a.mode_select && q_mode[k] == SEL_PARTIAL) {
       find_digit(h1 + (size_t)k * (kCoarse + kFine), q_need[k], &s_digit, &s_above, s_tmp);
       digit = s_digit;
       above = s_above;
@@ -364,6 +384,8 @@ __global__ __launch_bounds__(kNT) void sel_refine_kernel(SelArgs g) {
   const float* sc = a.scores + (int64_t)b * S;
   const uint8_t* lb = a.labels + (int64_t)b * S;
   uint32_t* h2 = g.L.hist + ((size_t)b * 2 + 1) * kG * (kCoarse + kFine);
+  __shared__ uint32_t lcoarse[kG][kCoarse];
+  coarse_clear(lcoarse);
   const int mode_l = st->sel_mode[0] | (st->sel_mode[1] << 2) | (st->sel_mode[2] << 4) | (st->sel_mode[3] << 6);
   uint32_t pre[kG];
   for (int k = 0; k < kG; ++k) pre[k] = st->prefix[k] >> 16;
@@ -380,9 +402,10 @@ __global__ __launch_bounds__(kNT) void sel_refine_kernel(SelArgs g) {
     }
     const bool pc = valid && ((mode_l >> (2 * l)) & 3) == SEL_PARTIAL && (key >> 16) == pre[l];
     const bool pa = valid && ((mode_l >> 6) & 3) == SEL_PARTIAL && (key >> 16) == pre[3];
-    hist_add(h2, l, key & 0xffffu, pc);
-    hist_add(h2, 3, key & 0xffffu, pa);
+    hist_add(h2, lcoarse, l, key & 0xffffu, pc);
+    hist_add(h2, lcoarse, 3, key & 0xffffu, pa);
   }
+  coarse_flush(h2, lcoarse);
   if (!arrive_last(&st->done_b, gridDim.x, &s_flag)) return;
   for (int k = 0; k < kG; ++k) {
     const int md = (mode_l >> (2 * k)) & 3;
