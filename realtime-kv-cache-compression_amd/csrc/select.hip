@@ -142,41 +142,53 @@ __device__ __forceinline__ void coarse_flush(uint32_t* base, uint32_t (*lcoarse)
   }
 }
 
-// In the last block: find, in the (coarse, fine) histogram of group g, the 16-bit digit where the
-// count from the top reaches `need`; returns the digit and the count strictly above it.
-__device__ void find_digit(const uint32_t* h, int64_t need, uint32_t* sh_digit, int64_t* sh_above, int64_t* sh_tmp) {
-  // threads 0..255 own coarse bins 255 - t (descending); defaults keep every index in range even if
-  // the histogram does not hold `need` tokens (it always does when the caller's counts are right)
-  const int t = threadIdx.x;
-  if (t == 0) { sh_tmp[4] = 0; sh_tmp[5] = 0; *sh_digit = 0; *sh_above = 0; }
+// In the last block: for every group g with want[g] (one wave per group, all four concurrently),
+// find in its (coarse, fine) histogram the 16-bit digit where the count from the top reaches
+// need[g]; digit[g] / above[g] = that digit and the count strictly above it.  Two dependent L2
+// reads per group.  Defaults keep every index in range even if a histogram holds fewer tokens.
+__device__ void find_digits(const uint32_t* h_rows, const bool want[kG], const int64_t need[kG], uint32_t digit[kG],
+                            int64_t above[kG]) {
+  const int lane = threadIdx.x & 63, g = threadIdx.x >> 6;  // kNT = 256: wave g ↔ group g
+  if (lane == 0) { digit[g] = 0; above[g] = 0; }
   __syncthreads();
-  const int64_t c = ld_sc1(h + (kCoarse - 1 - t));
-  // block inclusive scan of c over t (descending coarse order)
-  const int lane = t & 63, wid = t >> 6;
-  const int64_t inc = wave_inclusive_scan(c);
-  if (lane == 63) sh_tmp[wid] = inc;
-  __syncthreads();
-  int64_t base = 0;
-  for (int w = 0; w < wid; ++w) base += sh_tmp[w];
-  const int64_t incl = base + inc, excl = incl - c;
-  __syncthreads();
-  if (excl < need && incl >= need) { sh_tmp[4] = t; sh_tmp[5] = excl; }
-  __syncthreads();
-  const int ct = (int)sh_tmp[4] & (kCoarse - 1);
-  const uint32_t coarse = (uint32_t)(kCoarse - 1 - ct);
-  const int64_t above_coarse = sh_tmp[5];
-  __syncthreads();
-  // fine bins of that coarse bin: thread t owns fine digit (coarse << 8) | (255 - t)
-  const uint32_t fd = (coarse << 8) | (uint32_t)(255 - t);
-  const int64_t f = ld_sc1(h + kCoarse + fd);
-  const int64_t finc = wave_inclusive_scan(f);
-  if (lane == 63) sh_tmp[wid] = finc;
-  __syncthreads();
-  int64_t fbase = above_coarse;
-  for (int w = 0; w < wid; ++w) fbase += sh_tmp[w];
-  const int64_t fincl = fbase + finc, fexcl = fincl - f;
-  __syncthreads();
-  if (fexcl < need && fincl >= need) { *sh_digit = fd; *sh_above = fexcl; }
+  if (want[g]) {
+    const uint32_t* h = h_rows + (size_t)g * (kCoarse + kFine);
+    const int64_t nd = need[g];
+    // coarse: lane l owns descending bins 4l..4l+3 (bin index 255 - j)
+    uint32_t c[4];
+    int64_t lsum = 0;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) { c[q] = ld_sc1(h + (kCoarse - 1 - (4 * lane + q))); lsum += c[q]; }
+    int64_t incl = wave_inclusive_scan(lsum), excl = incl - lsum;
+    const bool hit = excl < nd && incl >= nd;  // exactly one lane when the histogram holds nd tokens
+    uint32_t my_coarse = 0;
+    int64_t my_ac = 0;
+    if (hit) {
+      int64_t run = excl;
+      for (int q = 0; q < 4; ++q) {
+        if (run + (int64_t)c[q] >= nd) { my_coarse = (uint32_t)(kCoarse - 1 - (4 * lane + q)); my_ac = run; break; }
+        run += c[q];
+      }
+    }
+    const uint64_t hm = __ballot(hit);
+    const int src = hm ? (__ffsll((unsigned long long)hm) - 1) : 0;  // wave-uniform
+    const uint32_t coarse = (uint32_t)__shfl((int)my_coarse, src, 64) & (kCoarse - 1);
+    const int64_t ac = __shfl(my_ac, src, 64);
+    // fine bins of that coarse bin: lane l owns digits (coarse << 8) | (255 - 4l - q)
+    uint32_t f[4];
+    lsum = 0;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) { f[q] = ld_sc1(h + kCoarse + ((coarse << 8) | (uint32_t)(255 - (4 * lane + q)))); lsum += f[q]; }
+    incl = ac + wave_inclusive_scan(lsum);
+    excl = incl - lsum;
+    if (excl < nd && incl >= nd) {
+      int64_t run = excl;
+      for (int q = 0; q < 4; ++q) {
+        if (run + (int64_t)f[q] >= nd) { digit[g] = (coarse << 8) | (uint32_t)(255 - (4 * lane + q)); above[g] = run; break; }
+        run += f[q];
+      }
+    }
+  }
   __syncthreads();
 }
 
@@ -198,8 +210,6 @@ __global__ __launch_bounds__(kNT) void sel_scores_kernel(SelArgs g) {
   __shared__ uint32_t s_key[2];
   __shared__ uint32_t s_ckey[3][2];
   __shared__ int s_flag;
-  __shared__ uint32_t s_digit;
-  __shared__ int64_t s_above, s_tmp[8];
   const int b = blockIdx.y, blk = blockIdx.x;
   const int64_t S = a.S;
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
@@ -355,20 +365,17 @@ __global__ __launch_bounds__(kNT) void sel_scores_kernel(SelArgs g) {
     st->quota[3] = kf;
   }
   __syncthreads();
-  for (int k = 0; k < kG; ++k) {
-    uint32_t digit = 0;
-    int64_t above = 0;
-    if (a.mode_select && q_mode[k] == SEL_PARTIAL) {
-      find_digit(h1 + (size_t)k * (kCoarse + kFine), q_need[k], &s_digit, &s_above, s_tmp);
-      digit = s_digit;
-      above = s_above;
-    }
-    if (threadIdx.x == 0) {
-      st->sel_mode[k] = q_mode[k];
-      st->prefix[k] = digit << 16;
-      st->need[k] = q_need[k] - above;
-    }
-    __syncthreads();
+  __shared__ uint32_t q_digit[kG];
+  __shared__ int64_t q_above[kG];
+  __shared__ bool q_want[kG];
+  if (threadIdx.x < kG) q_want[threadIdx.x] = a.mode_select && q_mode[threadIdx.x] == SEL_PARTIAL;
+  __syncthreads();
+  find_digits(h1, q_want, q_need, q_digit, q_above);
+  if (threadIdx.x < kG) {
+    const int k = threadIdx.x;
+    st->sel_mode[k] = q_mode[k];
+    st->prefix[k] = q_digit[k] << 16;
+    st->need[k] = q_need[k] - q_above[k];
   }
 }
 
@@ -376,8 +383,6 @@ __global__ __launch_bounds__(kNT) void sel_scores_kernel(SelArgs g) {
 __global__ __launch_bounds__(kNT) void sel_refine_kernel(SelArgs g) {
   const FinalizeArgs& a = g.f;
   __shared__ int s_flag;
-  __shared__ uint32_t s_digit;
-  __shared__ int64_t s_above, s_tmp[8];
   const int b = blockIdx.y, blk = blockIdx.x;
   const int64_t S = a.S;
   SelState* st = g.L.state + b;
@@ -407,16 +412,19 @@ __global__ __launch_bounds__(kNT) void sel_refine_kernel(SelArgs g) {
   }
   coarse_flush(h2, lcoarse);
   if (!arrive_last(&st->done_b, gridDim.x, &s_flag)) return;
-  for (int k = 0; k < kG; ++k) {
-    const int md = (mode_l >> (2 * k)) & 3;
-    if (md != SEL_PARTIAL) continue;  // uniform
-    const int64_t need = st->need[k];
-    find_digit(h2 + (size_t)k * (kCoarse + kFine), need, &s_digit, &s_above, s_tmp);
-    if (threadIdx.x == 0) {
-      st->prefix[k] = (st->prefix[k] & 0xffff0000u) | s_digit;
-      st->need[k] = need - s_above;  // ties at the threshold key to take, in index order
-    }
-    __syncthreads();
+  __shared__ uint32_t q_digit[kG];
+  __shared__ int64_t q_above[kG], q_need[kG];
+  __shared__ bool q_want[kG];
+  if (threadIdx.x < kG) {
+    q_want[threadIdx.x] = ((mode_l >> (2 * threadIdx.x)) & 3) == SEL_PARTIAL;
+    q_need[threadIdx.x] = st->need[threadIdx.x];
+  }
+  __syncthreads();
+  find_digits(h2, q_want, q_need, q_digit, q_above);
+  if (threadIdx.x < kG && q_want[threadIdx.x]) {
+    const int k = threadIdx.x;
+    st->prefix[k] = (st->prefix[k] & 0xffff0000u) | q_digit[k];
+    st->need[k] = q_need[k] - q_above[k];  // ties at the threshold key to take, in index order
   }
 }
 
@@ -671,19 +679,36 @@ __global__ __launch_bounds__(kNT) void sel_compact_kernel(SelArgs g) {
   int64_t need[3];
   for (int k = 0; k < 3; ++k) { mode[k] = st->sel_mode[k]; thr[k] = st->prefix[k]; need[k] = st->need[k]; }
   const SelPartial* pp = g.L.part + (size_t)b * g.L.nb;
-  int64_t row = 0, bytes = 0, tb[3] = {0, 0, 0};
-  for (int q = 0; q < blk; ++q) {  // every thread walks the (few) earlier partials
-    row += pp[q].gt_rows[0];
-    bytes += pp[q].gt_bytes[0];
-    for (int k = 0; k < 3; ++k) {
-      const int64_t t = pp[q].ties[k];
-      int64_t take = need[k] - tb[k];
-      take = take < 0 ? 0 : (take > t ? t : take);
-      row += take;
-      bytes += take * rb[k];
-      tb[k] += t;
+  // bases = sums over the earlier blocks' C1 partials: wave 0 loads 64 partials per step (lane q
+  // ↔ block q), scans ties per group to know how many each earlier block takes, reduces rows/bytes
+  __shared__ int64_t s_base[5];
+  if (wid == 0) {
+    int64_t row_acc = 0, byte_acc = 0, tie_acc[3] = {0, 0, 0};
+    for (int q0 = 0; q0 < blk; q0 += 64) {
+      const int q = q0 + lane;
+      const bool in = q < blk;
+      const int64_t gr = in ? pp[q].gt_rows[0] : 0, gb = in ? pp[q].gt_bytes[0] : 0;
+      int64_t r_here = gr, b_here = gb;
+      for (int k = 0; k < 3; ++k) {
+        const int64_t t = in ? pp[q].ties[k] : 0;
+        const int64_t before = tie_acc[k] + wave_inclusive_scan(t) - t;  // ties of blocks before q
+        int64_t take = need[k] - before;
+        take = take < 0 ? 0 : (take > t ? t : take);
+        r_here += take;
+        b_here += take * rb[k];
+        tie_acc[k] += wave_sum(t);
+      }
+      row_acc += wave_sum(r_here);
+      byte_acc += wave_sum(b_here);
+    }
+    if (lane == 0) {
+      s_base[0] = row_acc;
+      s_base[1] = byte_acc;
+      for (int k = 0; k < 3; ++k) s_base[2 + k] = tie_acc[k];
     }
   }
+  __syncthreads();
+  int64_t row = s_base[0], bytes = s_base[1], tb[3] = {s_base[2], s_base[3], s_base[4]};
   double ksum = 0.0;
   const int64_t i0 = (int64_t)blk * kBT;
   for (int j0 = 0; j0 < kBT; j0 += kNT) {
