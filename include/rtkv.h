@@ -285,6 +285,14 @@ int rtkv_tensor_fake_quant(const void* x_dev, int dtype, int64_t n_rows, int64_t
                            const uint8_t* row_labels_dev, int32_t label_value, int bits,
                            const float* scale_zp_dev, void* out_dev, void* stream);
 
+/* Numerics self-check (no reference counterpart; replaces nothing).  The quantizer divides by the
+ * row scale with a reciprocal + one FMA correction instead of the IEEE division for 16-bit rows;
+ * this enumerates every (dividend, positive divisor) pair of the 16-bit dtype that the fast path
+ * admits and counts bitwise differences from the IEEE fp32 quotient.  counts_dev[0] = pairs
+ * checked, counts_dev[1] = mismatches (must be 0).  RTKV_ERR_UNSUPPORTED for RTKV_F32 (fp32 rows
+ * always use the IEEE division). */
+int rtkv_selfcheck_division(int32_t dtype, unsigned long long* counts_dev, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -293,4 +293,8 @@ int rtkv_tensor_fake_quant(const void* x_dev, int dtype, int64_t n_rows, int64_t
                                   out_dev, (hipStream_t)stream);
 }
 
+int rtkv_selfcheck_division(int32_t dtype, unsigned long long* counts_dev, void* stream) {
+  return launch_selfcheck_division(dtype, counts_dev, (hipStream_t)stream);
+}
+
 }  // extern "C"

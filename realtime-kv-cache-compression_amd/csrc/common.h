@@ -211,5 +211,6 @@ int launch_tensor_params(const void* x, int dt, int64_t n_rows, int64_t row_len,
                          int label_value, int bits, float* scale_zp, void* ws, size_t ws_bytes, hipStream_t st);
 int launch_tensor_fake_quant(const void* x, int dt, int64_t n_rows, int64_t row_len, const uint8_t* row_labels,
                              int label_value, int bits, const float* scale_zp, void* out, hipStream_t st);
+int launch_selfcheck_division(int dt, unsigned long long* counts, hipStream_t st);
 
 }  // namespace rtkv

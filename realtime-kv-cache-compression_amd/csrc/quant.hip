@@ -1,403 +1,13 @@
-// quant.hip — K4: per-token asymmetric min-max quantization + bit-pack + ordered compaction, plus
-// the unpack (consumer) kernel and the whole-tensor quantization helpers.
-//
-// Reference: DynamicPrecisionQuantizer.get_quantization_params / quantize_tensor /
-// apply_mixed_precision_quantization (dynamic_quantization.py:62-196) followed by the gather of
-// SelectiveTokenPropagator.apply_token_selection (selective_propagation.py:214-232).  The reference
-// fake-quantizes EVERY token with ~12 tiny torch ops and then gathers the kept rows; here each kept
-// row is read from HBM once, quantized in registers and written once (dequantized row in the output
-// position + packed codes), and dropped rows are never read.
-//
-// Work decomposition: one wave64 per (kept row, tensor).  Lane l owns 8-element chunks
-// c = k*64 + l (k < NCH), so every wave-instruction moves 64 × 16 B = 1 KiB of one row (fp32: two
-// such loads).  Row min/max → wave shuffle reduction; the per-element ops are fp32 ops rounded to
-// the dtype after each op (bit-identical to PyTorch CPU).  8 codes of w bits pack into exactly w
-// bytes, so each lane writes its chunk's codes with one store at byte offset c*w.
-#include <type_traits>
-
-#include "common.h"
+// quant.hip — the K4 dispatcher (per-dtype instantiations live in quant_f16/bf16/f32.hip so they
+// compile in parallel), the gather, unpack (consumer), whole-tensor and self-check kernels.
+// Device helpers and the K4 kernel: quant_impl.h.
+#include "quant_impl.h"
 
 namespace rtkv {
 
-template <int DT> struct Chunk;  // 8 elements of storage
-template <> struct Chunk<RTKV_F32> { float4 a, b; };
-template <> struct Chunk<RTKV_F16> { uint4 a; };
-template <> struct Chunk<RTKV_BF16> { uint4 a; };
-
-template <int DT> __device__ __forceinline__ void chunk_to_f32(const Chunk<DT>& c, float (&x)[8]) {
-  if constexpr (DT == RTKV_F32) {
-    x[0] = c.a.x; x[1] = c.a.y; x[2] = c.a.z; x[3] = c.a.w;
-    x[4] = c.b.x; x[5] = c.b.y; x[6] = c.b.z; x[7] = c.b.w;
-  } else {
-    const uint32_t w[4] = {c.a.x, c.a.y, c.a.z, c.a.w};
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      x[2 * k] = Dt<DT>::load((uint16_t)(w[k] & 0xffffu));
-      x[2 * k + 1] = Dt<DT>::load((uint16_t)(w[k] >> 16));
-    }
-  }
-}
-template <int DT> __device__ __forceinline__ Chunk<DT> f32_to_chunk(const float (&x)[8]) {
-  Chunk<DT> c;
-  if constexpr (DT == RTKV_F32) {
-    c.a = make_float4(x[0], x[1], x[2], x[3]);
-    c.b = make_float4(x[4], x[5], x[6], x[7]);
-  } else {
-    uint32_t w[4];
-#pragma unroll
-    for (int k = 0; k < 4; ++k)
-      w[k] = (uint32_t)Dt<DT>::store(x[2 * k]) | ((uint32_t)Dt<DT>::store(x[2 * k + 1]) << 16);
-    c.a = make_uint4(w[0], w[1], w[2], w[3]);
-  }
-  return c;
-}
-
-// Little-endian accumulation of 8 codes of w bits (w <= 17) into 3 × 64-bit words.
-__device__ __forceinline__ void pack8(const uint32_t (&q)[8], int w, uint64_t& p0, uint64_t& p1, uint64_t& p2) {
-  p0 = p1 = p2 = 0;
-#pragma unroll
-  for (int e = 0; e < 8; ++e) {
-    const int bit = e * w;
-    const uint64_t v = q[e];
-    const int word = bit >> 6, sh = bit & 63;
-    const uint64_t lo = v << sh;
-    const uint64_t hi = sh ? (v >> (64 - sh)) : 0ull;
-    if (word == 0) { p0 |= lo; p1 |= hi; }
-    else if (word == 1) { p1 |= lo; p2 |= hi; }
-    else { p2 |= lo; }
-  }
-}
-
-__device__ __forceinline__ void store_bytes(uint8_t* dst, int nbytes, uint64_t p0, uint64_t p1, uint64_t p2) {
-  const uintptr_t addr = (uintptr_t)dst;
-  if (nbytes == 16 && (addr & 15) == 0) {
-    *reinterpret_cast<uint4*>(dst) = make_uint4((uint32_t)p0, (uint32_t)(p0 >> 32), (uint32_t)p1, (uint32_t)(p1 >> 32));
-  } else if (nbytes == 8 && (addr & 7) == 0) {
-    *reinterpret_cast<uint2*>(dst) = make_uint2((uint32_t)p0, (uint32_t)(p0 >> 32));
-  } else if (nbytes == 4 && (addr & 3) == 0) {
-    *reinterpret_cast<uint32_t*>(dst) = (uint32_t)p0;
-  } else if (nbytes == 2 && (addr & 1) == 0) {
-    *reinterpret_cast<uint16_t*>(dst) = (uint16_t)p0;
-  } else {
-    for (int k = 0; k < nbytes; ++k) {
-      const uint64_t word = k < 8 ? p0 : (k < 16 ? p1 : p2);
-      dst[k] = (uint8_t)(word >> ((k & 7) * 8));
-    }  // (scalar tail path: non-multiple-of-8 rows and unusual widths only)
-  }
-}
-
-struct RowParams {
-  float scale, zp, qmaxT;
-};
-
-template <int DT> __device__ __forceinline__ RowParams row_params(float mn, float mx, int bits) {
-  // dynamic_quantization.py:79-93 (each op rounded to the dtype)
-  RowParams r;
-  const float qmax = (float)((1u << bits) - 1u);
-  r.qmaxT = Dt<DT>::rnd(qmax);  // clamp bound as converted by torch.clamp (:121)
-  if (mx == mn) {
-    r.scale = 1.f;
-    r.zp = 0.f;
-  } else {
-    r.scale = Dt<DT>::rnd(Dt<DT>::rnd(mx - mn) / qmax);
-    r.zp = Dt<DT>::rnd(0.f - Dt<DT>::rnd(mn / r.scale));
-  }
-  return r;
-}
-
-template <int DT> __device__ __forceinline__ float quant_code(float x, const RowParams& rp) {
-  // dynamic_quantization.py:120-121
-  const float t = Dt<DT>::rnd(Dt<DT>::rnd(x / rp.scale) + rp.zp);
-  float q = __builtin_rintf(t);  // rint of a dtype value is a dtype value: no rounding needed
-  q = q < 0.f ? 0.f : q;
-  q = q > rp.qmaxT ? rp.qmaxT : q;
-  return q;
-}
-template <int DT> __device__ __forceinline__ float dequant(float q, const RowParams& rp) {
-  return Dt<DT>::rnd(Dt<DT>::rnd(q - rp.zp) * rp.scale);  // :124
-}
-
-// ------------------------------------------------------------------------------------ K4
-// Pack 8 codes of W bits (compile-time W in {2,4,8,16}) and store them at dst (W bytes).
-template <int W> __device__ __forceinline__ void pack_store(uint8_t* dst, const uint32_t (&q)[8], bool aligned) {
-  if constexpr (W == 2) {
-    uint32_t v = 0;
-#pragma unroll
-    for (int e = 0; e < 8; ++e) v |= q[e] << (2 * e);
-    if (aligned) *reinterpret_cast<uint16_t*>(dst) = (uint16_t)v;
-    else { dst[0] = (uint8_t)v; dst[1] = (uint8_t)(v >> 8); }
-  } else if constexpr (W == 4) {
-    uint32_t v = 0;
-#pragma unroll
-    for (int e = 0; e < 8; ++e) v |= q[e] << (4 * e);
-    if (aligned) *reinterpret_cast<uint32_t*>(dst) = v;
-    else {
-#pragma unroll
-      for (int k = 0; k < 4; ++k) dst[k] = (uint8_t)(v >> (8 * k));
-    }
-  } else if constexpr (W == 8) {
-    const uint32_t lo = q[0] | (q[1] << 8) | (q[2] << 16) | (q[3] << 24);
-    const uint32_t hi = q[4] | (q[5] << 8) | (q[6] << 16) | (q[7] << 24);
-    if (aligned) *reinterpret_cast<uint2*>(dst) = make_uint2(lo, hi);
-    else {
-#pragma unroll
-      for (int k = 0; k < 8; ++k) dst[k] = (uint8_t)((k < 4 ? lo : hi) >> (8 * (k & 3)));
-    }
-  } else {  // W == 16
-    const uint4 v = make_uint4(q[0] | (q[1] << 16), q[2] | (q[3] << 16), q[4] | (q[5] << 16), q[6] | (q[7] << 16));
-    if (aligned) *reinterpret_cast<uint4*>(dst) = v;
-    else {
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const uint32_t wv = k == 0 ? v.x : (k == 1 ? v.y : (k == 2 ? v.z : v.w));
-#pragma unroll
-        for (int j = 0; j < 4; ++j) dst[4 * k + j] = (uint8_t)(wv >> (8 * j));
-      }
-    }
-  }
-}
-
-// Row geometry shared by every task of a launch: element f of a row lives at (f / D) * stride_h + f % D.
-// CONTIG (stride_h == D on input and output) makes that plain f.  FULL: the row is exactly NCH*64
-// chunks of 8 (F a multiple of 512), so no lane is idle and packed rows stay 16-byte aligned.
-template <int DT, int NCH, bool CONTIG, bool FULL>
-__global__ __launch_bounds__(256, 2) void quant_rows_kernel(QuantArgs a) {
-  using S_ = typename Dt<DT>::S;
-  const int lane = threadIdx.x & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int nw = gridDim.x * (blockDim.x >> 6);
-  const int B = (int)a.kv.B;
-  const int S = (int)a.kv.S;
-  const int F = (int)(a.kv.H * a.kv.D);
-  const int nch = FULL ? NCH * 64 : (F + 7) >> 3;
-  const int cap = (int)a.out.row_capacity;
-  int R = a.kept_index ? (int)a.stats->max_kept : S;  // rows per batch row
-  if (R > cap) R = cap;
-  const int tasks = 2 * B * R;
-  const rtkv_batch_stats* bst = a.stats ? reinterpret_cast<const rtkv_batch_stats*>(a.stats + 1) : nullptr;
-  const bool emit_deq = a.out.k_out_dev != nullptr;
-  const bool emit_pk = a.out.packed_k_dev != nullptr;
-  const int64_t osb = a.out.o_stride_b >= 0 ? a.out.o_stride_b : (int64_t)R * a.out.o_stride_s;
-  // per-lane in-row offsets of each chunk (task independent)
-  int in_off[NCH], out_off[NCH];
-#pragma unroll
-  for (int k = 0; k < NCH; ++k) {
-    const int f = (k * 64 + lane) * 8;
-    if constexpr (CONTIG) {
-      in_off[k] = f;
-      out_off[k] = f;
-    } else {
-      const int D = (int)a.kv.D;
-      const int h = f / D, d = f - h * D;
-      in_off[k] = (int)(h * a.kv.stride_h) + d;
-      out_off[k] = (int)(h * a.out.o_stride_h) + d;
-    }
-  }
-  auto valid = [&](int k) { return FULL || (k * 64 + lane) < nch; };
-  for (int t = blockIdx.x * (blockDim.x >> 6) + wave; t < tasks; t += nw) {
-    const int which = t & 1;
-    const int rr = t >> 1;
-    const int b = rr / R, r = rr - b * R;
-    const int kept_b = a.kept_index ? (int)bst[b].kept : S;
-    int i = (r < kept_b) ? (a.kept_index ? a.kept_index[(int64_t)b * cap + r] : r) : 0;
-    int lab = (r < kept_b) ? (int)a.labels[(int64_t)b * S + i] : 0;
-    i = __builtin_amdgcn_readfirstlane(i);
-    lab = __builtin_amdgcn_readfirstlane(lab);
-    S_* orow = emit_deq ? static_cast<S_*>(which ? a.out.v_out_dev : a.out.k_out_dev) + b * osb +
-                              (int64_t)r * a.out.o_stride_s
-                        : nullptr;
-    const int64_t sz_idx = ((int64_t)b * cap + r) * 4 + which * 2;
-    if (r >= kept_b || lab > 2) {  // zero padding row (selective_propagation.py:214-222)
-      if (emit_deq) {
-        const Chunk<DT> z = f32_to_chunk<DT>({0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f});
-#pragma unroll
-        for (int k = 0; k < NCH; ++k)
-          if (valid(k)) *reinterpret_cast<Chunk<DT>*>(orow + out_off[k]) = z;
-      }
-      if (a.out.scale_zp_dev && lane < 2) a.out.scale_zp_dev[sz_idx + lane] = 0.f;
-      continue;
-    }
-    const int bits = a.bits[lab];
-    const int w = field_width(DT, bits);
-    const S_* src = static_cast<const S_*>(which ? a.kv.v_dev : a.kv.k_dev) + b * a.kv.stride_b +
-                    (int64_t)i * a.kv.stride_s;
-    // ---- load the whole row once (all chunks in flight), min/max
-    Chunk<DT> raw[NCH];
-#pragma unroll
-    for (int k = 0; k < NCH; ++k)
-      if (valid(k)) raw[k] = *reinterpret_cast<const Chunk<DT>*>(src + in_off[k]);
-    float mn = INFINITY, mx = -INFINITY;
-#pragma unroll
-    for (int k = 0; k < NCH; ++k) {
-      if (valid(k)) {
-        float x[8];
-        chunk_to_f32<DT>(raw[k], x);
-#pragma unroll
-        for (int e = 0; e < 8; ++e) { mn = fminf(mn, x[e]); mx = fmaxf(mx, x[e]); }
-      }
-    }
-    mn = wave_min(mn);
-    mx = wave_max(mx);
-    const RowParams rp = row_params<DT>(mn, mx, bits);
-    if (a.out.scale_zp_dev && lane < 2) a.out.scale_zp_dev[sz_idx + lane] = lane == 0 ? rp.scale : rp.zp;
-    uint8_t* pk = emit_pk ? (which ? a.out.packed_v_dev : a.out.packed_k_dev) + a.out.row_offset_dev[(int64_t)b * cap + r]
-                          : nullptr;
-    // ---- quantize, pack, dequantize, store (one chunk at a time)
-    auto process = [&](auto wtag) {
-      constexpr int W = decltype(wtag)::value;
-      const bool aligned = FULL || (((uintptr_t)pk & 15) == 0 && (nch * W) % 16 == 0);
-#pragma unroll
-      for (int k = 0; k < NCH; ++k) {
-        const int c = k * 64 + lane;
-        __builtin_amdgcn_sched_barrier(0);  // keep one chunk's temporaries live at a time
-        if (!valid(k)) continue;
-        float x[8];
-        chunk_to_f32<DT>(raw[k], x);
-        float d[8];
-        uint32_t qi[8];
-#pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          const float q = quant_code<DT>(x[e], rp);
-          d[e] = dequant<DT>(q, rp);
-          qi[e] = (uint32_t)q;
-        }
-        if (emit_pk) pack_store<W>(pk + c * W, qi, aligned);
-        if (emit_deq) *reinterpret_cast<Chunk<DT>*>(orow + out_off[k]) = f32_to_chunk<DT>(d);
-      }
-    };
-    switch (w) {
-      case 2: process(std::integral_constant<int, 2>{}); break;
-      case 4: process(std::integral_constant<int, 4>{}); break;
-      case 8: process(std::integral_constant<int, 8>{}); break;
-      default: process(std::integral_constant<int, 16>{}); break;  // launcher guarantees w in {2,4,8,16}
-    }
-  }
-}
-
-// Generic path: any D, any alignment, any F (scalar element access, partial last chunk).
-template <int DT>
-__global__ __launch_bounds__(256) void quant_rows_generic_kernel(QuantArgs a) {
-  using S_ = typename Dt<DT>::S;
-  const int lane = threadIdx.x & 63;
-  const int64_t gw = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
-  const int64_t nw = (int64_t)gridDim.x * (blockDim.x >> 6);
-  const int64_t B = a.kv.B, S = a.kv.S, D = a.kv.D, F = a.kv.H * a.kv.D;
-  const int64_t nch = (F + 7) >> 3;
-  const int64_t cap = a.out.row_capacity;
-  int64_t R = a.kept_index ? a.stats->max_kept : S;
-  if (R > cap) R = cap;
-  const rtkv_batch_stats* bst = a.stats ? reinterpret_cast<const rtkv_batch_stats*>(a.stats + 1) : nullptr;
-  const bool emit_deq = a.out.k_out_dev != nullptr;
-  const bool emit_pk = a.out.packed_k_dev != nullptr;
-  const int64_t osb = a.out.o_stride_b >= 0 ? a.out.o_stride_b : R * a.out.o_stride_s;
-  for (int64_t t = gw; t < 2 * B * R; t += nw) {
-    const int which = (int)(t & 1);
-    const int64_t rr = t >> 1, b = rr / R, r = rr - b * R;
-    const int64_t kept_b = a.kept_index ? bst[b].kept : S;
-    const int64_t i = (r < kept_b) ? (a.kept_index ? a.kept_index[b * cap + r] : r) : 0;
-    const int lab = (r < kept_b) ? a.labels[b * S + i] : 0;
-    S_* orow = emit_deq ? static_cast<S_*>(which ? a.out.v_out_dev : a.out.k_out_dev) + b * osb + r * a.out.o_stride_s
-                        : nullptr;
-    auto oaddr = [&](int64_t f) { return (f / D) * a.out.o_stride_h + (f % D); };
-    if (r >= kept_b || lab > 2) {
-      if (emit_deq)
-        for (int64_t f = lane; f < F; f += 64) orow[oaddr(f)] = Dt<DT>::store(0.f);
-      if (a.out.scale_zp_dev && lane < 2) a.out.scale_zp_dev[(b * cap + r) * 4 + which * 2 + lane] = 0.f;
-      continue;
-    }
-    const int bits = a.bits[lab];
-    const int w = field_width(DT, bits);
-    const S_* src = static_cast<const S_*>(which ? a.kv.v_dev : a.kv.k_dev) + b * a.kv.stride_b + i * a.kv.stride_s;
-    auto load = [&](int64_t f) { return Dt<DT>::load(src[(f / D) * a.kv.stride_h + (f % D)]); };
-    float mn = INFINITY, mx = -INFINITY;
-    for (int64_t f = lane; f < F; f += 64) { const float v = load(f); mn = fminf(mn, v); mx = fmaxf(mx, v); }
-    mn = wave_min(mn);
-    mx = wave_max(mx);
-    const RowParams rp = row_params<DT>(mn, mx, bits);
-    if (a.out.scale_zp_dev && lane < 2)
-      a.out.scale_zp_dev[(b * cap + r) * 4 + which * 2 + lane] = lane == 0 ? rp.scale : rp.zp;
-    uint8_t* pk = emit_pk ? (which ? a.out.packed_v_dev : a.out.packed_k_dev) + a.out.row_offset_dev[b * cap + r] : nullptr;
-    for (int64_t c = lane; c < nch; c += 64) {
-      const int64_t f0 = c * 8;
-      const int nvalid = (F - f0) < 8 ? (int)(F - f0) : 8;
-      uint32_t qi[8];
-      for (int e = 0; e < 8; ++e) {
-        if (e < nvalid) {
-          const float q = quant_code<DT>(load(f0 + e), rp);
-          qi[e] = (uint32_t)q;
-          if (emit_deq) orow[oaddr(f0 + e)] = Dt<DT>::store(dequant<DT>(q, rp));
-        } else {
-          qi[e] = 0u;
-        }
-      }
-      if (emit_pk) {
-        uint64_t p0, p1, p2;
-        pack8(qi, w, p0, p1, p2);
-        store_bytes(pk + c * w, (nvalid * w + 7) >> 3, p0, p1, p2);
-      }
-    }
-  }
-}
-
-template <int DT, bool CONTIG>
-static int launch_quant_vec(const QuantArgs& a, int64_t nch, dim3 grid, hipStream_t st) {
-  const int per_lane = (int)((nch + 63) / 64);
-#define RTKV_Q(N)                                                                              \
-  if (nch == (int64_t)N * 64) {                                                                \
-    hipLaunchKernelGGL((quant_rows_kernel<DT, N, CONTIG, true>), grid, dim3(256), 0, st, a);   \
-    RTKV_HIP_CHECK(hipGetLastError());                                                         \
-    return RTKV_OK;                                                                            \
-  }
-  RTKV_Q(8) RTKV_Q(10) RTKV_Q(16) RTKV_Q(4) RTKV_Q(2) RTKV_Q(1)
-#undef RTKV_Q
-#define RTKV_Q(N)                                                                              \
-  if (per_lane <= N) {                                                                         \
-    hipLaunchKernelGGL((quant_rows_kernel<DT, N, CONTIG, false>), grid, dim3(256), 0, st, a);  \
-    RTKV_HIP_CHECK(hipGetLastError());                                                         \
-    return RTKV_OK;                                                                            \
-  }
-  RTKV_Q(1) RTKV_Q(2) RTKV_Q(4) RTKV_Q(8) RTKV_Q(16)
-#undef RTKV_Q
-  hipLaunchKernelGGL((quant_rows_generic_kernel<DT>), grid, dim3(256), 0, st, a);
-  RTKV_HIP_CHECK(hipGetLastError());
-  return RTKV_OK;
-}
-
-template <int DT>
-static int launch_quant_dt(const QuantArgs& a, hipStream_t st) {
-  const rtkv_kv_desc& kv = a.kv;
-  const int64_t F = kv.H * kv.D;
-  const int64_t nch = (F + 7) / 8;
-  const int64_t R = a.kept_index ? (a.out.row_capacity < kv.S ? a.out.row_capacity : kv.S) : kv.S;
-  const int64_t tasks = 2 * kv.B * R;
-  int64_t blocks = (tasks + 3) / 4;
-  if (blocks > 4096) blocks = 4096;
-  if (blocks < 1) blocks = 1;
-  const int esz = Dt<DT>::kBytes;
-  auto al16 = [](const void* p) { return p == nullptr || ((uintptr_t)p % 16) == 0; };
-  bool vec = (kv.D % 8 == 0) && al16(kv.k_dev) && al16(kv.v_dev) && (kv.stride_s * esz) % 16 == 0 &&
-             (kv.stride_h * esz) % 16 == 0 && (kv.stride_b * esz) % 16 == 0;
-  if (a.out.k_out_dev)
-    vec = vec && al16(a.out.k_out_dev) && al16(a.out.v_out_dev) && (a.out.o_stride_s * esz) % 16 == 0 &&
-          (a.out.o_stride_h * esz) % 16 == 0 && (a.out.o_stride_b < 0 || (a.out.o_stride_b * esz) % 16 == 0);
-  // every in-row offset (and 2·B·R tasks) must fit in 32 bits for the vector kernel
-  const int64_t in_span = (kv.H - 1) * kv.stride_h + kv.D;
-  const int64_t out_span = (kv.H - 1) * a.out.o_stride_h + kv.D;
-  vec = vec && in_span < ((int64_t)1 << 31) && out_span < ((int64_t)1 << 31) && tasks < ((int64_t)1 << 31) &&
-        kv.S < ((int64_t)1 << 31) && a.out.row_capacity < ((int64_t)1 << 31);
-  const bool contig = (kv.H == 1 || kv.stride_h == kv.D) && (!a.out.k_out_dev || kv.H == 1 || a.out.o_stride_h == kv.D);
-  for (int g = 0; g < 3; ++g) {  // the vector kernel packs widths 2/4/8/16 only
-    const int w = field_width(DT, a.bits[g]);
-    vec = vec && (w == 2 || w == 4 || w == 8 || w == 16 || !a.out.packed_k_dev);
-  }
-  if (!vec) {
-    hipLaunchKernelGGL((quant_rows_generic_kernel<DT>), dim3((unsigned)blocks), dim3(256), 0, st, a);
-    RTKV_HIP_CHECK(hipGetLastError());
-    return RTKV_OK;
-  }
-  if (contig) return launch_quant_vec<DT, true>(a, nch, dim3((unsigned)blocks), st);
-  return launch_quant_vec<DT, false>(a, nch, dim3((unsigned)blocks), st);
-}
+extern template int launch_quant_dt<RTKV_F32>(const QuantArgs&, hipStream_t);
+extern template int launch_quant_dt<RTKV_F16>(const QuantArgs&, hipStream_t);
+extern template int launch_quant_dt<RTKV_BF16>(const QuantArgs&, hipStream_t);
 
 int launch_quant(const QuantArgs& a, hipStream_t st) {
   RTKV_REQUIRE(a.kv.k_dev && a.kv.v_dev && a.labels, "quantize_rows: null K/V/labels");
@@ -625,6 +235,50 @@ int launch_tensor_fake_quant(const void* x, int dt, int64_t n_rows, int64_t row_
 #undef RTKV_T
     default:
       RTKV_REQUIRE(false, "tensor_fake_quant: bad dtype");
+  }
+  RTKV_HIP_CHECK(hipGetLastError());
+  return RTKV_OK;
+}
+
+
+// ------------------------------------------------------------------------------------ self-check
+// Exhaustive proof obligation of fast_quotient: every (dividend, positive divisor) pair of the 16-bit
+// dtype admitted by fast_div_ok is compared bitwise with the IEEE division.  counts = {checked, bad}.
+template <int DT>
+__global__ __launch_bounds__(256) void selfcheck_division_kernel(unsigned long long* counts) {
+  const float s = Dt<DT>::load((uint16_t)(blockIdx.x + 1));  // 0x0001 .. 0x7fff: every positive pattern
+  const float r = 1.f / s;
+  unsigned long long checked = 0, bad = 0;
+  for (uint32_t xb = threadIdx.x; xb < 65536u; xb += blockDim.x) {
+    const float x = Dt<DT>::load((uint16_t)xb);
+    const float ax = __builtin_fabsf(x);
+    if (!(ax < INFINITY)) continue;  // finite dividends only (NaN fails the test)
+    // a row admits x iff fast_div_ok(s, amax, amin_nz) with amax >= |x| and, for x != 0, amin_nz <= |x|;
+    // the pair is therefore reachable iff fast_div_ok(s, |x|, x != 0 ? |x| : +inf)
+    if (!fast_div_ok<DT>(s, ax, x != 0.f ? ax : INFINITY)) continue;
+    const float q = fast_quotient(x, s, r);
+    const float ref = x / s;
+    ++checked;
+    bad += __builtin_bit_cast(uint32_t, q) != __builtin_bit_cast(uint32_t, ref);
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    checked += __shfl_xor(checked, o);
+    bad += __shfl_xor(bad, o);
+  }
+  if ((threadIdx.x & 63) == 0) {
+    atomicAdd(counts, checked);
+    atomicAdd(counts + 1, bad);
+  }
+}
+
+int launch_selfcheck_division(int dt, unsigned long long* counts, hipStream_t st) {
+  RTKV_REQUIRE(counts, "selfcheck_division: null counts");
+  RTKV_HIP_CHECK(hipMemsetAsync(counts, 0, 2 * sizeof(unsigned long long), st));
+  if (dt == RTKV_F16) hipLaunchKernelGGL((selfcheck_division_kernel<RTKV_F16>), dim3(0x7fff), dim3(256), 0, st, counts);
+  else if (dt == RTKV_BF16) hipLaunchKernelGGL((selfcheck_division_kernel<RTKV_BF16>), dim3(0x7fff), dim3(256), 0, st, counts);
+  else {
+    set_error("rtkv: selfcheck_division: fp32 rows always use the IEEE division");
+    return RTKV_ERR_UNSUPPORTED;
   }
   RTKV_HIP_CHECK(hipGetLastError());
   return RTKV_OK;

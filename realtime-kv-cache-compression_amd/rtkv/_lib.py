@@ -84,6 +84,7 @@ _SIGS = {
                              c_i64, c_i64, c_i64, c_p], c_i32),
     "rtkv_tensor_quant_params": ([c_p, c_i32, c_i64, c_i64, c_p, c_i32, c_i32, c_p, c_p, c_sz, c_p], c_i32),
     "rtkv_tensor_fake_quant": ([c_p, c_i32, c_i64, c_i64, c_p, c_i32, c_i32, c_p, c_p, c_p], c_i32),
+    "rtkv_selfcheck_division": ([c_i32, c_p, c_p], c_i32),
     "rtkv_gather_rows": ([c_p, c_i64, c_i64, c_i64, c_p, c_i64, c_i64, c_p, c_i64, c_i64, c_p, c_p], c_i32),
 }
 EXPORTS = tuple(_SIGS)

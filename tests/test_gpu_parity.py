@@ -145,6 +145,74 @@ def test_f16_16bit_raises_like_the_reference():
         q.apply_mixed_precision_quantization(dev(K, "float16"), dev(V, "float16"), labels)
 
 
+@pytest.mark.parametrize("dtype", ["float16", "bfloat16"])
+def test_fast_division_exhaustive(dtype):
+    """K4 divides by the row scale with reciprocal + FMA correction (quant_impl.h fast_quotient).
+    The device enumerates every (x, s) pair of the 16-bit dtype its row gate admits and compares
+    the quotient bitwise with the IEEE fp32 division."""
+    import rtkv
+    counts = torch.zeros(2, dtype=torch.int64, device="cuda")
+    rc = rtkv._lib.lib().rtkv_selfcheck_division(synth.DTYPES[dtype], counts.data_ptr(),
+                                                 rtkv._lib.stream_ptr(counts.device))
+    rtkv._lib.check(rc, "rtkv_selfcheck_division")
+    checked, bad = counts.cpu().tolist()
+    assert bad == 0
+    assert checked > (2_000_000_000 if dtype == "float16" else 700_000_000)
+
+
+def _division_edge_rows(dtype: str, F: int) -> np.ndarray:
+    """Rows that sit on either side of K4's fast-division row gate."""
+    rng = np.random.default_rng(5)
+    rows = [rng.standard_normal(F)]                                   # ordinary row (fast path)
+    z = rng.standard_normal(F)
+    z[::3] = 0.0
+    z[1::7] = -0.0
+    rows.append(z)                                                    # exact and negative zeros
+    rows.append(np.full(F, 0.75))                                     # constant row (scale 1)
+    if dtype == "float16":
+        t = np.zeros(F)
+        t[::5] = 2.0 ** -24
+        rows.append(t)                                                # scale underflows to 0: IEEE x/0
+        big = rng.choice([-60000.0, 60000.0, 1.0], F)
+        rows.append(big)                                              # range overflows: scale = inf
+        rows.append(rng.integers(-1023, 1024, F) * 2.0 ** -24)        # subnormal values
+    elif dtype == "bfloat16":
+        t = 1.0 + rng.standard_normal(F)
+        t[::11] = 1e-30
+        rows.append(t)                                                # tiny nonzero next to O(1) values
+        rows.append(rng.standard_normal(F) * 1e30)                    # |x| > 2^62
+        rows.append(rng.standard_normal(F) * 1e-25)                   # scale < 2^-62
+        rows.append(rng.standard_normal(F) * 2.0 ** -120)             # subnormal-adjacent
+    else:
+        rows.append(rng.standard_normal(F) * 1e-38)
+        rows.append(rng.standard_normal(F) * 1e37)
+    return synth.cast(np.stack(rows)[None], dtype)
+
+
+@pytest.mark.parametrize("dtype", ["float16", "bfloat16", "float32"])
+@pytest.mark.parametrize("F", [4096, 512])
+def test_quant_rows_on_both_sides_of_the_division_gate(dtype, F):
+    import rtkv
+    x = _division_edge_rows(dtype, F)
+    S = x.shape[1]
+    for bits in ((2, 4, 8), (4, 8, 16)):
+        if dtype == "float16" and bits[2] == 16:
+            continue
+        for shift in range(3):
+            lab = ((np.arange(S) + shift) % 3).astype(np.int64)[None]
+            q = rtkv.DynamicPrecisionQuantizer(config(COVERAGE, 4, bits))
+            kq, vq, _ = q.apply_mixed_precision_quantization(dev(x, dtype), dev(x[:, ::-1].copy(), dtype),
+                                                             torch.from_numpy(lab).cuda())
+            ref_k = orc.mixed_precision(x, synth.DTYPES[dtype], lab, bits)
+            ref_v = orc.mixed_precision(x[:, ::-1].copy(), synth.DTYPES[dtype], lab, bits)
+            for got, ref in ((host(kq), ref_k), (host(vq), ref_v)):
+                # NaN outputs (scale 0 / inf rows) are compared by position: the sign of a generated
+                # NaN is platform-defined (x86 default NaN is negative, gfx950's is positive)
+                nan_g, nan_r = np.isnan(synth.to_f32(got, dtype)), np.isnan(synth.to_f32(ref, dtype))
+                assert np.array_equal(nan_g, nan_r), (bits, shift)
+                assert np.array_equal(got[~nan_g], ref[~nan_r]), (bits, shift)
+
+
 def test_tensor_quant_helpers_match_oracle():
     import rtkv
     q = rtkv.DynamicPrecisionQuantizer(config(COVERAGE, 4))
