@@ -157,7 +157,26 @@ def test_fast_division_exhaustive(dtype):
     rtkv._lib.check(rc, "rtkv_selfcheck_division")
     checked, bad = counts.cpu().tolist()
     assert bad == 0
-    assert checked > (2_000_000_000 if dtype == "float16" else 700_000_000)
+    assert checked == _admitted_division_pairs(dtype)
+
+
+def _admitted_division_pairs(dtype: str) -> int:
+    """Host count of the (x, s) pairs quant_impl.h fast_div_ok admits: finite x, positive finite s;
+    bf16 additionally 2^-62 <= s <= 2^62, |x| <= 2^62 and (x == 0 or |x| >= 2^-48 * s)."""
+    bitsv = np.arange(65536, dtype=np.uint32)
+    with np.errstate(invalid="ignore"):
+        vals = synth.to_f32(bitsv.astype(np.uint16), dtype).astype(np.float64)
+    finite = np.isfinite(vals)
+    pos_s = vals[1:0x8000]
+    pos_s = pos_s[np.isfinite(pos_s)]
+    if dtype == "float16":
+        return int(pos_s.size) * int(finite.sum())
+    ax = np.abs(vals[finite])
+    zeros = int((ax == 0).sum())
+    nz = np.sort(ax[(ax != 0) & (ax <= 2.0 ** 62)])
+    s = pos_s[(pos_s >= 2.0 ** -62) & (pos_s <= 2.0 ** 62)]
+    lo = np.searchsorted(nz, s * 2.0 ** -48, side="left")
+    return int(s.size) * zeros + int((nz.size - lo).sum())
 
 
 def _division_edge_rows(dtype: str, F: int) -> np.ndarray:
