@@ -52,15 +52,15 @@ def parse():
     return ap.parse_args()
 
 
-def synth_layer(l: int, S: int, H: int, D: int, P: int, dtype, device, gen):
+def synth_layer(l: int, S: int, H: int, D: int, P: int, dtype, device, gen, row0: int = 0):
     """K, V [1,S,H*D] ~ N(0,1); W prompt slice [1,H,S,P] = u^4 row-normalised × U(0,1), causal in
-    the prompt."""
+    the prompt.  row0: global index of the first token (sequence shards)."""
     F = H * D
     K = torch.randn(1, S, F, generator=gen, device=device, dtype=torch.float32).to(dtype)
     V = torch.randn(1, S, F, generator=gen, device=device, dtype=torch.float32).to(dtype)
     u = torch.rand(1, H, S, P, generator=gen, device=device, dtype=torch.float32)
     raw = (u * u) ** 2 + 1e-6
-    causal = torch.arange(P, device=device)[None, :] <= torch.arange(S, device=device)[:, None]
+    causal = torch.arange(P, device=device)[None, :] <= row0 + torch.arange(S, device=device)[:, None]
     raw = raw * causal
     W = raw / raw.sum(-1, keepdim=True) * torch.rand(1, H, S, 1, generator=gen, device=device)
     return K, V, W.to(dtype)
@@ -135,6 +135,70 @@ class Job:
         return tot, k4
 
 
+class ShardedJob:
+    """Sequence-sharded prefill (weak scaling): this rank owns tokens [rank*S, (rank+1)*S) of an
+    N*S-token prefill.  One step = every layer's shard stages (K1 on own rows, RCCL all-gather of A,
+    global selection, K4 on own kept rows) + the end-of-prefill exchange of the packed KV."""
+
+    def __init__(self, args, device, rank, world):
+        import rtkv
+        from rtkv.sharded import ShardedPrefillCompressor
+        self.args, self.device, self.rank, self.world = args, device, rank, world
+        self.dtype = getattr(torch, args.dtype)
+        self.S, self.H, self.D = args.seq, args.heads, args.head_dim
+        self.F = self.H * self.D
+        self.S_total = self.S * world
+        self.P = rtkv.prompt_length(self.S_total)
+        self.cfg = rtkv.CompressionConfig(alpha=0.8, beta=0.1, gamma=0.1, theta_h=0.4, theta_m=0.25,
+                                          high_precision_bits=8, medium_precision_bits=4, low_precision_bits=2,
+                                          early_layer_ratio=0.8, middle_layer_ratio=0.6, later_layer_ratio=0.4,
+                                          num_hidden_layers=args.layers)
+        self.bits = (2, 4, 8)
+        self.comp = ShardedPrefillCompressor(self.cfg, emit_packed=not args.no_packed, emit_dequant=True,
+                                             device=device)
+        gen = torch.Generator(device=device)
+        gen.manual_seed(1234 + 7919 * rank)
+        self.inputs, self.params = [], []
+        for l in range(args.layers):
+            self.inputs.append(synth_layer(l, self.S, self.H, self.D, self.P, self.dtype, device, gen,
+                                           row0=rank * self.S))
+            self.params.append(self.comp.params(l, self.S_total))
+        self.last = None
+        torch.cuda.synchronize(device)
+
+    def step(self, events=None):
+        for l in range(self.args.layers):
+            K, V, W = self.inputs[l]
+            self.comp.enqueue_layer(K, V, W, l, params=self.params[l])
+        self.last = self.comp.exchange()
+
+    def layer_bytes(self):
+        """Algorithmic HBM bytes per layer of the whole N*S-token job (same formula as Job)."""
+        from rtkv.engine import decode_stats
+        e = torch.tensor([], dtype=self.dtype).element_size()
+        tot, k4 = [], []
+        for sl in self.last:
+            st = decode_stats(sl.bufs.g.stats.cpu().numpy().tobytes(), 1)
+            Sp, pk = st.max_kept, st.total_packed_bytes
+            w_read = self.H * self.S_total * self.P * e
+            kv_read = 2 * Sp * self.F * e
+            deq = 2 * Sp * self.F * e
+            packed = (2 * pk + Sp * 16) if not self.args.no_packed else 0
+            meta = self.S_total * (4 + 4 + 4 + 1 + 1) + Sp * (4 + 8 + 1)
+            k4.append(kv_read + deq + packed + Sp * (4 + 8 + 1))
+            tot.append(w_read + kv_read + deq + packed + meta)
+        return tot, k4
+
+    def exchanged_bytes(self):
+        """Bytes of packed KV (codes + scale/zero-point) this rank received in the exchange."""
+        n = 0
+        for sl in self.last:
+            r = sl.ranges[0]
+            mine = (int(r[self.rank + 1, 1] - r[self.rank, 1]) * 2 + int(r[self.rank + 1, 0] - r[self.rank, 0]) * 16)
+            n += (int(r[-1, 1] - r[0, 1]) * 2 + int(r[-1, 0] - r[0, 0]) * 16) - mine
+        return n
+
+
 def cpu_baseline(args, job):
     """The C oracle (single thread, a literal restatement of the reference) on a bounded sample:
     the first `cpu_baseline_layers` layers of the same workload, same inputs."""
@@ -176,8 +240,7 @@ def main():
     if world > 1:
         import torch.distributed as dist
         dist.init_process_group("nccl", device_id=device)
-        from rtkv.sharded import ShardedJob
-        job = ShardedJob(args, device, rank, world, Job)
+        job = ShardedJob(args, device, rank, world)
     else:
         dist = None
         job = Job(args, device, rank, world)
@@ -217,11 +280,7 @@ def main():
                 for k in range(3):
                     k_ms[k] += evs[k].elapsed_time(evs[k + 1])
     tot_bytes, k4_bytes = job.layer_bytes()
-    step_bytes = sum(tot_bytes)
-    if dist is not None:
-        b = torch.tensor([float(step_bytes)], device=device, dtype=torch.float64)
-        dist.all_reduce(b)
-        step_bytes = float(b.item())
+    step_bytes = sum(tot_bytes)  # whole-job algorithmic bytes (the sharded job counts all N*S tokens)
     value = step_bytes / (ms_per_step / 1e3) / 1e9
 
     if rank == 0:
@@ -245,6 +304,11 @@ def main():
                        "model": "Llama-2-7B (KV shapes only)", "global_batch": 1, "seq_len": job.S * world,
                        "parallelism": f"sequence-shard x{world}" if world > 1 else "single GPU"},
         }
+        if world > 1:
+            line["exchange"] = {"received_bytes_per_rank_per_step": job.exchanged_bytes(),
+                                "kind": "one grouped RCCL send/recv batch of packed K/V codes + scale/zp "
+                                        "(exact byte ranges, all peers at once)",
+                                "per_layer_collective": "RCCL all-gather of A (4 B/token)"}
         if world == 1:
             per_launch_ms = k_ms[2] / (reps * args.layers)
             achieved = sum(k4_bytes) / args.layers / (per_launch_ms / 1e3) / 1e9

@@ -248,6 +248,49 @@ int rtkv_compress_layer_events(const rtkv_kv_desc* kv, const rtkv_attn_desc* w,
                                void* workspace_dev, size_t workspace_bytes, void* stream,
                                void* const events[4]);
 
+/* ------------------------------------------------------------------------------------------------
+ * Sequence shards (multi-GPU prefill; no reference counterpart — the reference is single-device).
+ * Rank j of N owns tokens [row0, row0 + S_local) of an S_total-token prefill.  Per layer:
+ *   1. rtkv_attention_aggregation_shard on its W rows          → A_local [B, S_local]
+ *   2. all-gather A (4 B/token)                                 → A [B, S_total] on every rank
+ *   3. rtkv_finalize_select on A (replicated, deterministic)    → scores, labels, selection, offsets
+ *   4. rtkv_shard_ranges                                        → per-rank output row / byte bounds
+ *   5. rtkv_quantize_rows_shard on its K/V rows                 → its kept rows: packed codes at
+ *      their global byte offsets (the single-GPU layout), dequantized rows local
+ * and one exchange of every rank's row/byte ranges at the end: every rank then holds the
+ * single-GPU result byte for byte.
+ * ---------------------------------------------------------------------------------------------- */
+
+/* rtkv_attention_aggregation of W rows [row0, row0 + w->S) of an S_total-row attention matrix:
+ * bit-identical to rows [row0, row0 + S) of the unsharded aggregation. */
+int rtkv_attention_aggregation_shard(const rtkv_attn_desc* w, int32_t prompt_len, int64_t row0,
+                                     int64_t S_total, float* A_dev, void* stream);
+
+/* Scores → classes → budgeted selection → compaction map from a (gathered) aggregation A [B, S]
+ * (values rounded to a_dtype): the second kernel group of rtkv_compress_layer.  Writes out->scores,
+ * labels, mask, kept_index, row_offset (when RTKV_EMIT_PACKED) and stats. */
+int rtkv_finalize_select(const float* A_dev, int a_dtype, int64_t B, int64_t S, const rtkv_layer_params* p,
+                         const rtkv_layer_out* out, int64_t F, int kv_dtype, void* workspace_dev,
+                         size_t workspace_bytes, void* stream);
+
+/* rtkv_quantize_rows for the kept rows whose token lies in [row0, row0 + kv->S) (rank `rank` of
+ * `nranks`); kv describes the local K/V rows (token row0 + i at local row i).  Packed codes and
+ * scale/zero-point land at their global positions.  Dequantized rows: with ranges_dev (the
+ * rtkv_shard_ranges table of this layer) at LOCAL output row r - first_row(b, rank), batch stride
+ * out->o_stride_b (required >= 0); without it at the global output row, rank 0 writing the zero
+ * padding rows. */
+int rtkv_quantize_rows_shard(const rtkv_kv_desc* kv, int64_t row0, int64_t S_total, int32_t rank,
+                             int32_t nranks, const int64_t* ranges_dev, const uint8_t* labels_dev,
+                             const int32_t* kept_index_dev, const rtkv_layer_params* p,
+                             const rtkv_layer_out* out, void* stream);
+
+/* ranges_dev[(b*(nranks+1) + j)*2 + {0,1}] = {first output row, first packed byte} of rank j's tokens
+ * [j*S_local, (j+1)*S_local) in batch row b; j = nranks is the end of the row.  row_offset_dev may be
+ * NULL (bytes = 0). */
+int rtkv_shard_ranges(const int32_t* kept_index_dev, const int64_t* row_offset_dev,
+                      const rtkv_layer_stats* stats_dev, int64_t B, int64_t row_capacity, int64_t S_local,
+                      int32_t nranks, int64_t* ranges_dev, void* stream);
+
 /* Reconstruct dequantized rows from packed codes (+ scale/zp, labels of the kept rows); bit-identical
  * to the RTKV_EMIT_DEQUANT output.  rows_per_batch[b] rows of batch row b are decoded.
  * Consumer side of the packed format (compression_layers.py:7-45 CompressedKVCache). */

@@ -263,6 +263,90 @@ int rtkv_compress_layer(const rtkv_kv_desc* kv, const rtkv_attn_desc* w, const r
   return rtkv_compress_layer_events(kv, w, p, out, workspace_dev, workspace_bytes, stream, nullptr);
 }
 
+// ---------------------------------------------------------------------------------- sequence shards
+int rtkv_attention_aggregation_shard(const rtkv_attn_desc* w, int32_t prompt_len, int64_t row0, int64_t S_total,
+                                     float* A_dev, void* stream) {
+  RTKV_REQUIRE(w != nullptr, "null attention descriptor");
+  RTKV_REQUIRE(row0 >= 0 && S_total >= row0 + w->S, "shard rows [row0, row0 + S) must lie inside [0, S_total)");
+  AggExtras x;
+  x.row0 = row0;
+  x.S_total = S_total;
+  return launch_aggregation(*w, prompt_len, A_dev, (hipStream_t)stream, x);
+}
+
+int rtkv_finalize_select(const float* A_dev, int a_dtype, int64_t B, int64_t S, const rtkv_layer_params* p,
+                         const rtkv_layer_out* out, int64_t F, int kv_dtype, void* workspace_dev,
+                         size_t workspace_bytes, void* stream) {
+  int rc = check_params(p);
+  if (rc) return rc;
+  RTKV_REQUIRE(A_dev && out, "null argument");
+  RTKV_REQUIRE(B >= 1 && S >= 1 && F >= 1, "empty shape");
+  RTKV_REQUIRE(out->scores_dev && out->labels_dev && out->mask_dev && out->kept_index_dev && out->stats_dev,
+               "finalize_select needs scores, labels, mask, kept_index and stats outputs");
+  RTKV_REQUIRE(out->row_capacity >= S, "row_capacity must be >= S (every token may be kept)");
+  if (p->flags & RTKV_EMIT_PACKED) {
+    RTKV_REQUIRE(out->row_offset_dev, "EMIT_PACKED needs row offsets");
+    for (int g = 0; g < 3; ++g)
+      RTKV_REQUIRE(field_width(kv_dtype, p->bits[g]) > 0, "packed codes unsupported for this dtype/bits");
+  }
+  Workspace ws;
+  rc = carve(workspace_dev, workspace_bytes, B, S, ws);
+  if (rc) return rc;
+  FinalizeArgs a = finalize_args(p, B, S);
+  a.A = A_dev;
+  a.a_dtype = a_dtype;
+  a.scores = out->scores_dev;
+  a.labels = out->labels_dev;
+  a.mask = out->mask_dev;
+  a.kept_index = out->kept_index_dev;
+  a.row_offset = out->row_offset_dev;
+  a.row_capacity = out->row_capacity;
+  a.F = F;
+  a.kv_dtype = kv_dtype;
+  a.stats = out->stats_dev;
+  a.mode_scores = 1;
+  a.mode_labels = 1;
+  a.mode_select = (p->flags & RTKV_NO_SELECTION) ? 2 : 1;
+  return launch_select(a, ws.sel, false, (hipStream_t)stream);
+}
+
+int rtkv_quantize_rows_shard(const rtkv_kv_desc* kv, int64_t row0, int64_t S_total, int32_t rank, int32_t nranks,
+                             const int64_t* ranges_dev, const uint8_t* labels_dev, const int32_t* kept_index_dev,
+                             const rtkv_layer_params* p, const rtkv_layer_out* out, void* stream) {
+  int rc = check_params(p);
+  if (rc) return rc;
+  RTKV_REQUIRE(kv && out && kept_index_dev && out->stats_dev, "quantize_rows_shard needs kept_index and stats");
+  RTKV_REQUIRE(row0 >= 0 && S_total >= row0 + kv->S, "shard rows [row0, row0 + S) must lie inside [0, S_total)");
+  RTKV_REQUIRE(out->row_capacity >= S_total, "row_capacity must be >= S_total");
+  QuantArgs q;
+  std::memset(&q, 0, sizeof(q));
+  q.kv = *kv;
+  q.labels = labels_dev;
+  q.kept_index = kept_index_dev;
+  q.stats = out->stats_dev;
+  for (int g = 0; g < 3; ++g) q.bits[g] = p->bits[g];
+  q.out = *out;
+  RTKV_REQUIRE(nranks >= 1 && rank >= 0 && rank < nranks, "rank must be in [0, nranks)");
+  RTKV_REQUIRE(!ranges_dev || !(p->flags & RTKV_EMIT_DEQUANT) || out->o_stride_b >= 0,
+               "local dequant rows (ranges_dev) need an explicit o_stride_b");
+  q.S_glob = S_total;
+  q.row0 = row0;
+  q.pad_owner = (rank == 0 && !ranges_dev) ? 1 : 0;
+  q.shard_rank = rank;
+  q.shard_nranks = nranks;
+  q.shard_ranges = ranges_dev;
+  if (!(p->flags & RTKV_EMIT_DEQUANT)) { q.out.k_out_dev = nullptr; q.out.v_out_dev = nullptr; }
+  if (!(p->flags & RTKV_EMIT_PACKED)) { q.out.packed_k_dev = nullptr; q.out.packed_v_dev = nullptr; }
+  return launch_quant(q, (hipStream_t)stream);
+}
+
+int rtkv_shard_ranges(const int32_t* kept_index_dev, const int64_t* row_offset_dev, const rtkv_layer_stats* stats_dev,
+                      int64_t B, int64_t row_capacity, int64_t S_local, int32_t nranks, int64_t* ranges_dev,
+                      void* stream) {
+  return launch_shard_ranges(kept_index_dev, row_offset_dev, stats_dev, B, row_capacity, S_local, nranks, ranges_dev,
+                             (hipStream_t)stream);
+}
+
 int rtkv_unpack_dequant(const uint8_t* packed_dev, const int64_t* row_offset_dev, const float* scale_zp_dev,
                         int which, const int32_t* kept_index_dev, const uint8_t* labels_dev, int64_t B, int64_t S,
                         int64_t row_capacity, const int64_t* rows_dev, int64_t H, int64_t D, int dtype,

@@ -159,6 +159,10 @@ struct AggExtras {
   size_t zero0_bytes = 0;
   void* zero1 = nullptr;
   size_t zero1_bytes = 0;
+  // sequence shard: W holds rows [row0, row0 + w.S) of an S_total-row matrix (S_total = 0: unsharded).
+  // Only the position of the reduction-order boundary (cascade_limit) depends on it.
+  int64_t row0 = 0;
+  int64_t S_total = 0;
 };
 int launch_aggregation(const rtkv_attn_desc& w, int P, float* A, hipStream_t st, const AggExtras& x = AggExtras());
 int launch_position_bias(int64_t S, float* pos, hipStream_t st);
@@ -197,9 +201,21 @@ struct QuantArgs {
   const rtkv_layer_stats* stats;  // kept counts / max_kept (null when kept_index is null)
   int32_t bits[3];
   rtkv_layer_out out;
+  // Sequence shard (rtkv_quantize_rows_shard): kv holds tokens [row0, row0 + kv.S) of an S_glob-token
+  // selection; only kept rows inside that window are processed, padding rows only when pad_owner.
+  // S_glob = 0: unsharded (S_glob = kv.S, every row processed).
+  int64_t S_glob;
+  int64_t row0;
+  int32_t pad_owner;
+  // Optional rtkv_shard_ranges table: dequantized rows go to LOCAL output row r - first_row(b, rank)
+  // (packed codes and scale/zero-point keep their global positions).
+  int32_t shard_rank, shard_nranks;
+  const int64_t* shard_ranges;
 };
 int launch_quant(const QuantArgs& a, hipStream_t st);
 
+int launch_shard_ranges(const int32_t* kept_index, const int64_t* row_offset, const rtkv_layer_stats* stats, int64_t B,
+                        int64_t cap, int64_t S_local, int nranks, int64_t* ranges, hipStream_t st);
 int launch_gather(const void* src, int64_t B, int64_t S, int64_t row_bytes, const int32_t* kept_index, int64_t cap,
                   int64_t ssb, void* dst, int64_t dsb, int64_t sss, const rtkv_layer_stats* stats, hipStream_t st);
 int launch_unpack(const uint8_t* packed, const int64_t* row_offset, const float* scale_zp, int which,

@@ -278,7 +278,9 @@ static int launch_agg_dt(const rtkv_attn_desc& w, int P, float* A, hipStream_t s
   using S_ = typename Dt<DT>::S;
   constexpr int VEC = 16 / Dt<DT>::kBytes;
   const S_* W = static_cast<const S_*>(w.w_dev);
-  const int64_t lim = cascade_limit(DT, w.S * (int64_t)P);
+  // flattened [S*P] column index of local row i is (row0 + i)*P + p: shift the global boundary
+  const int64_t lim = x.S_total ? cascade_limit(DT, x.S_total * (int64_t)P) - x.row0 * (int64_t)P
+                                : cascade_limit(DT, w.S * (int64_t)P);
   const bool aligned = ((uintptr_t)W % 16 == 0) && (P % VEC == 0) && (w.stride_s % VEC == 0) &&
                        (w.stride_h % VEC == 0) && (w.stride_b % VEC == 0);
   const int H = (int)w.H;

@@ -69,6 +69,43 @@ int launch_gather(const void* src, int64_t B, int64_t S, int64_t row_bytes, cons
   return RTKV_OK;
 }
 
+// ------------------------------------------------------------------------------------ shard ranges
+// ranges[b][j] = {first output row, first packed byte} of rank j's tokens [j*S_local, (j+1)*S_local)
+// (j = nranks: one past the last kept row of batch row b).  kept_index is ascending per batch row.
+__global__ void shard_ranges_kernel(const int32_t* __restrict__ kept_index, const int64_t* __restrict__ row_offset,
+                                    const rtkv_layer_stats* __restrict__ stats, int64_t B, int64_t cap, int64_t S_local,
+                                    int nranks, int64_t* __restrict__ ranges) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= B * (nranks + 1)) return;
+  const int64_t b = t / (nranks + 1);
+  const int j = (int)(t - b * (nranks + 1));
+  const rtkv_batch_stats* bst = reinterpret_cast<const rtkv_batch_stats*>(stats + 1);
+  int64_t base = 0;
+  for (int64_t bb = 0; bb < b; ++bb) base += bst[bb].packed_bytes;
+  const int64_t kept = bst[b].kept;
+  const int64_t bound = (int64_t)j * S_local;
+  int64_t lo = 0, hi = kept;  // first row whose token index >= bound
+  while (lo < hi) {
+    const int64_t mid = (lo + hi) >> 1;
+    if ((int64_t)kept_index[b * cap + mid] < bound) lo = mid + 1;
+    else hi = mid;
+  }
+  if (j == nranks) lo = kept;
+  ranges[t * 2] = lo;
+  ranges[t * 2 + 1] = row_offset ? (lo < kept ? row_offset[b * cap + lo] : base + bst[b].packed_bytes) : 0;
+}
+
+int launch_shard_ranges(const int32_t* kept_index, const int64_t* row_offset, const rtkv_layer_stats* stats, int64_t B,
+                        int64_t cap, int64_t S_local, int nranks, int64_t* ranges, hipStream_t st) {
+  RTKV_REQUIRE(kept_index && stats && ranges, "shard_ranges: null pointer");
+  RTKV_REQUIRE(B >= 1 && cap >= 1 && S_local >= 1 && nranks >= 1, "shard_ranges: bad shape");
+  const int64_t n = B * (nranks + 1);
+  hipLaunchKernelGGL(shard_ranges_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, kept_index, row_offset,
+                     stats, B, cap, S_local, nranks, ranges);
+  RTKV_HIP_CHECK(hipGetLastError());
+  return RTKV_OK;
+}
+
 // ------------------------------------------------------------------------------------ unpack
 template <int DT>
 __global__ __launch_bounds__(256) void unpack_kernel(const uint8_t* __restrict__ packed, const int64_t* __restrict__ row_offset,

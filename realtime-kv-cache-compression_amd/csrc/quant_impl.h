@@ -198,7 +198,9 @@ __global__ __launch_bounds__(256, 2) void quant_rows_kernel(QuantArgs a) {
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int nw = gridDim.x * (blockDim.x >> 6);
   const int B = (int)a.kv.B;
-  const int S = (int)a.kv.S;
+  const bool shard = a.S_glob != 0;
+  const int S = shard ? (int)a.S_glob : (int)a.kv.S;  // tokens of the selection (labels row length)
+  const int row0 = (int)a.row0, row1 = (int)(a.row0 + a.kv.S);
   const int F = (int)(a.kv.H * a.kv.D);
   const int nch = FULL ? NCH * 64 : (F + 7) >> 3;
   const int cap = (int)a.out.row_capacity;
@@ -234,8 +236,12 @@ __global__ __launch_bounds__(256, 2) void quant_rows_kernel(QuantArgs a) {
     int lab = (r < kept_b) ? (int)a.labels[(int64_t)b * S + i] : 0;
     i = __builtin_amdgcn_readfirstlane(i);
     lab = __builtin_amdgcn_readfirstlane(lab);
+    if (shard) {  // another rank's token, or a padding row this rank does not own
+      if (r < kept_b ? (i < row0 || i >= row1) : !a.pad_owner) continue;
+    }
+    const int rloc = a.shard_ranges ? r - (int)a.shard_ranges[((int64_t)b * (a.shard_nranks + 1) + a.shard_rank) * 2] : r;
     S_* orow = emit_deq ? static_cast<S_*>(which ? a.out.v_out_dev : a.out.k_out_dev) + b * osb +
-                              (int64_t)r * a.out.o_stride_s
+                              (int64_t)rloc * a.out.o_stride_s
                         : nullptr;
     const int64_t sz_idx = ((int64_t)b * cap + r) * 4 + which * 2;
     if (r >= kept_b || lab > 2) {  // zero padding row (selective_propagation.py:214-222)
@@ -251,7 +257,7 @@ __global__ __launch_bounds__(256, 2) void quant_rows_kernel(QuantArgs a) {
     const int bits = a.bits[lab];
     const int w = field_width(DT, bits);
     const S_* src = static_cast<const S_*>(which ? a.kv.v_dev : a.kv.k_dev) + b * a.kv.stride_b +
-                    (int64_t)i * a.kv.stride_s;
+                    (int64_t)(i - row0) * a.kv.stride_s;
     // ---- load the whole row once (all chunks in flight), min/max
     Chunk<DT> raw[NCH];
 #pragma unroll
@@ -329,7 +335,9 @@ __global__ __launch_bounds__(256) void quant_rows_generic_kernel(QuantArgs a) {
   const int lane = threadIdx.x & 63;
   const int64_t gw = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
   const int64_t nw = (int64_t)gridDim.x * (blockDim.x >> 6);
-  const int64_t B = a.kv.B, S = a.kv.S, D = a.kv.D, F = a.kv.H * a.kv.D;
+  const bool shard = a.S_glob != 0;
+  const int64_t B = a.kv.B, S = shard ? a.S_glob : a.kv.S, D = a.kv.D, F = a.kv.H * a.kv.D;
+  const int64_t row0 = a.row0, row1 = a.row0 + a.kv.S;
   const int64_t nch = (F + 7) >> 3;
   const int64_t cap = a.out.row_capacity;
   int64_t R = a.kept_index ? a.stats->max_kept : S;
@@ -344,7 +352,9 @@ __global__ __launch_bounds__(256) void quant_rows_generic_kernel(QuantArgs a) {
     const int64_t kept_b = a.kept_index ? bst[b].kept : S;
     const int64_t i = (r < kept_b) ? (a.kept_index ? a.kept_index[b * cap + r] : r) : 0;
     const int lab = (r < kept_b) ? a.labels[b * S + i] : 0;
-    S_* orow = emit_deq ? static_cast<S_*>(which ? a.out.v_out_dev : a.out.k_out_dev) + b * osb + r * a.out.o_stride_s
+    if (shard && (r < kept_b ? (i < row0 || i >= row1) : !a.pad_owner)) continue;
+    const int64_t rloc = a.shard_ranges ? r - a.shard_ranges[(b * (a.shard_nranks + 1) + a.shard_rank) * 2] : r;
+    S_* orow = emit_deq ? static_cast<S_*>(which ? a.out.v_out_dev : a.out.k_out_dev) + b * osb + rloc * a.out.o_stride_s
                         : nullptr;
     auto oaddr = [&](int64_t f) { return (f / D) * a.out.o_stride_h + (f % D); };
     if (r >= kept_b || lab > 2) {
@@ -355,7 +365,7 @@ __global__ __launch_bounds__(256) void quant_rows_generic_kernel(QuantArgs a) {
     }
     const int bits = a.bits[lab];
     const int w = field_width(DT, bits);
-    const S_* src = static_cast<const S_*>(which ? a.kv.v_dev : a.kv.k_dev) + b * a.kv.stride_b + i * a.kv.stride_s;
+    const S_* src = static_cast<const S_*>(which ? a.kv.v_dev : a.kv.k_dev) + b * a.kv.stride_b + (i - row0) * a.kv.stride_s;
     auto load = [&](int64_t f) { return Dt<DT>::load(src[(f / D) * a.kv.stride_h + (f % D)]); };
     float mn = INFINITY, mx = -INFINITY;
     for (int64_t f = lane; f < F; f += 64) { const float v = load(f); mn = fminf(mn, v); mx = fmaxf(mx, v); }
@@ -416,7 +426,8 @@ int launch_quant_dt(const QuantArgs& a, hipStream_t st) {
   const rtkv_kv_desc& kv = a.kv;
   const int64_t F = kv.H * kv.D;
   const int64_t nch = (F + 7) / 8;
-  const int64_t R = a.kept_index ? (a.out.row_capacity < kv.S ? a.out.row_capacity : kv.S) : kv.S;
+  const int64_t Sg = a.S_glob ? a.S_glob : kv.S;
+  const int64_t R = a.kept_index ? (a.out.row_capacity < Sg ? a.out.row_capacity : Sg) : Sg;
   const int64_t tasks = 2 * kv.B * R;
   int64_t blocks = (tasks + 3) / 4;
   if (blocks > 4096) blocks = 4096;
@@ -432,7 +443,7 @@ int launch_quant_dt(const QuantArgs& a, hipStream_t st) {
   const int64_t in_span = (kv.H - 1) * kv.stride_h + kv.D;
   const int64_t out_span = (kv.H - 1) * a.out.o_stride_h + kv.D;
   vec = vec && in_span < ((int64_t)1 << 31) && out_span < ((int64_t)1 << 31) && tasks < ((int64_t)1 << 31) &&
-        kv.S < ((int64_t)1 << 31) && a.out.row_capacity < ((int64_t)1 << 31);
+        Sg < ((int64_t)1 << 31) && a.out.row_capacity < ((int64_t)1 << 31);
   const bool contig = (kv.H == 1 || kv.stride_h == kv.D) && (!a.out.k_out_dev || kv.H == 1 || a.out.o_stride_h == kv.D);
   for (int g = 0; g < 3; ++g) {  // the vector kernel packs widths 2/4/8/16 only
     const int w = field_width(DT, a.bits[g]);

@@ -85,6 +85,10 @@ _SIGS = {
     "rtkv_tensor_quant_params": ([c_p, c_i32, c_i64, c_i64, c_p, c_i32, c_i32, c_p, c_p, c_sz, c_p], c_i32),
     "rtkv_tensor_fake_quant": ([c_p, c_i32, c_i64, c_i64, c_p, c_i32, c_i32, c_p, c_p, c_p], c_i32),
     "rtkv_selfcheck_division": ([c_i32, c_p, c_p], c_i32),
+    "rtkv_attention_aggregation_shard": ([c_p, c_i32, c_i64, c_i64, c_p, c_p], c_i32),
+    "rtkv_finalize_select": ([c_p, c_i32, c_i64, c_i64, c_p, c_p, c_i64, c_i32, c_p, c_sz, c_p], c_i32),
+    "rtkv_quantize_rows_shard": ([c_p, c_i64, c_i64, c_i32, c_i32, c_p, c_p, c_p, c_p, c_p, c_p], c_i32),
+    "rtkv_shard_ranges": ([c_p, c_p, c_p, c_i64, c_i64, c_i64, c_i32, c_p, c_p], c_i32),
     "rtkv_gather_rows": ([c_p, c_i64, c_i64, c_i64, c_p, c_i64, c_i64, c_p, c_i64, c_i64, c_p, c_p], c_i32),
 }
 EXPORTS = tuple(_SIGS)

@@ -1,0 +1,250 @@
+"""Sequence-sharded prefill compression: one process per GPU, ranks own contiguous token chunks.
+
+The reference compresses one layer on one device (unified_compressor.py:95-172, called per layer
+from modified_llama.py:113-117).  Here an S_total-token prefill is split into N chunks of S_local
+tokens (rank j owns tokens [j*S_local, (j+1)*S_local)), and each layer runs as
+
+  1. K1 on the rank's own W rows                       rtkv_attention_aggregation_shard
+  2. all-gather of the per-token prompt mass A          4 B/token, RCCL (torch.distributed)
+  3. scores / classes / selection on the whole A        rtkv_finalize_select (replicated: every rank
+                                                        computes the identical global selection)
+  4. per-rank output row / byte bounds                  rtkv_shard_ranges
+  5. K4 on the rank's own kept K/V rows                 rtkv_quantize_rows_shard: packed codes at
+                                                        their single-GPU byte offsets, dequantized
+                                                        rows into a local [B, S_local, F] buffer
+
+The selection is global (the reference's min-max normalisation and budget are over the whole
+sequence, token_importance.py:71-83, selective_propagation.py:96), so step 2 is the only exchange
+inside a layer.  After the last layer, ``exchange()`` does the one collective of the compressed KV:
+a single host read of every layer's rank bounds, then ONE grouped point-to-point batch in which each
+rank sends its byte ranges of the packed K/V codes and its scale/zero-point rows to every peer
+(xGMI links are point-to-point, so every rank streams to all 7 peers at once instead of hopping
+round a ring).  Every rank then holds every layer's packed KV byte-identical to the single-GPU
+``rtkv_compress_layer`` output.
+
+The device stages are injected (``stages``): ``HipShardStages`` calls librtkv.so; the CPU test
+suite swaps in oracle-backed stages to exercise this orchestration under gloo.
+"""
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass
+from typing import List, Optional
+
+import torch
+import torch.distributed as dist
+
+from . import _lib as L
+from .engine import LayerBuffers, Workspace, attn_desc, kv_desc, params_from_config, prompt_length
+from .selective_propagation import SelectiveTokenPropagator
+
+
+class HipShardStages:
+    """The per-rank device stages (librtkv.so), all stream-ordered and sync-free."""
+
+    def __init__(self, device):
+        self.device = torch.device(device)
+        self.ws = Workspace(self.device)
+
+    def _stream(self):
+        return L.stream_ptr(self.device)
+
+    def aggregate(self, W, P: int, row0: int, S_total: int, A_out: torch.Tensor):
+        L.require_device(W, A_out)
+        wd = attn_desc(W)
+        L.check(L.lib().rtkv_attention_aggregation_shard(ctypes.byref(wd), P, row0, S_total, A_out.data_ptr(),
+                                                          self._stream()), "rtkv_attention_aggregation_shard")
+
+    def finalize(self, A, a_dtype: int, params, bufs: "ShardBuffers"):
+        ws = self.ws.get(bufs.B, bufs.S_total)
+        out = bufs.out_struct()
+        L.check(L.lib().rtkv_finalize_select(A.data_ptr(), a_dtype, bufs.B, bufs.S_total, ctypes.byref(params),
+                                              ctypes.byref(out), bufs.F, L.TORCH_DTYPE_CODE[bufs.dtype],
+                                              ws.data_ptr(), ws.numel(), self._stream()), "rtkv_finalize_select")
+
+    def ranges(self, bufs: "ShardBuffers", world: int):
+        L.check(L.lib().rtkv_shard_ranges(bufs.g.kept_index.data_ptr(), L.ptr(bufs.g.row_offset),
+                                          bufs.g.stats.data_ptr(), bufs.B, bufs.S_total, bufs.S_local, world,
+                                          bufs.ranges.data_ptr(), self._stream()), "rtkv_shard_ranges")
+
+    def quantize(self, K, V, layout: str, row0: int, rank: int, world: int, params, bufs: "ShardBuffers"):
+        L.require_device(K, V)
+        kd = kv_desc(K, V, layout)
+        out = bufs.out_struct()
+        out.o_stride_h = kd.D
+        L.check(L.lib().rtkv_quantize_rows_shard(ctypes.byref(kd), row0, bufs.S_total, rank, world,
+                                                 bufs.ranges.data_ptr(), bufs.g.labels.data_ptr(),
+                                                 bufs.g.kept_index.data_ptr(), ctypes.byref(params),
+                                                 ctypes.byref(out), self._stream()), "rtkv_quantize_rows_shard")
+
+
+class ShardBuffers:
+    """One layer on one rank: the global selection outputs (single-GPU layout, capacity S_total rows),
+    the local dequantized rows, and the rank bounds table."""
+
+    def __init__(self, B: int, S_local: int, world: int, F: int, dtype: torch.dtype, device, bits,
+                 emit_dequant=True, emit_packed=True):
+        self.B, self.S_local, self.world, self.F, self.dtype = B, S_local, world, F, dtype
+        self.S_total = S_local * world
+        dev = torch.device(device)
+        self.g = LayerBuffers(B, self.S_total, F, dtype, dev, bits, emit_dequant=False, emit_packed=emit_packed)
+        self.k_local = torch.empty(B, S_local, F, dtype=dtype, device=dev) if emit_dequant else None
+        self.v_local = torch.empty(B, S_local, F, dtype=dtype, device=dev) if emit_dequant else None
+        self.ranges = torch.zeros(B, world + 1, 2, dtype=torch.int64, device=dev)
+
+    def out_struct(self) -> L.LayerOut:
+        o = self.g.out_struct()
+        o.k_out_dev, o.v_out_dev = L.ptr(self.k_local), L.ptr(self.v_local)
+        o.o_stride_b, o.o_stride_s, o.o_stride_h = self.S_local * self.F, self.F, self.F
+        return o
+
+
+@dataclass
+class ShardLayer:
+    """Host view of one exchanged layer: ranges[b, j] = (first row, first byte) of rank j."""
+    layer_idx: int
+    bufs: ShardBuffers
+    ranges: torch.Tensor  # host int64 [B, world+1, 2]
+
+    def local_rows(self, rank: int, b: int = 0) -> int:
+        return int(self.ranges[b, rank + 1, 0] - self.ranges[b, rank, 0])
+
+    def local_kv(self, rank: int):
+        """This rank's dequantized kept rows, ascending token order, [B, max_b rows_b, F]."""
+        n = max(self.local_rows(rank, b) for b in range(self.bufs.B))
+        return self.bufs.k_local[:, :n], self.bufs.v_local[:, :n]
+
+    def kept(self, b: int = 0) -> int:
+        return int(self.ranges[b, -1, 0])
+
+
+class ShardedPrefillCompressor:
+    """Per-rank driver of a sequence-sharded prefill (same parameters as RealTimePrefillCompressor).
+
+    ``enqueue_layer`` is sync-free; ``exchange`` is the one host sync + the one collective of the
+    compressed KV.  ``compress_layer_kv_cache`` keeps the reference's per-layer method name for the
+    rank's own token chunk (it returns the rank's dequantized rows)."""
+
+    def __init__(self, config, group=None, stages=None, emit_packed: bool = True, emit_dequant: bool = True,
+                 device=None):
+        if not dist.is_initialized():
+            raise RuntimeError("ShardedPrefillCompressor needs torch.distributed to be initialised")
+        self.config = config
+        self.group = group
+        self.rank = dist.get_rank(group)
+        self.world = dist.get_world_size(group)
+        self.device = torch.device(device) if device is not None else (
+            torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() else torch.device("cpu"))
+        self.stages = stages if stages is not None else HipShardStages(self.device)
+        self.emit_packed, self.emit_dequant = emit_packed, emit_dequant
+        self.propagator = SelectiveTokenPropagator(config)
+        self.bits = (int(config.low_precision_bits), int(config.medium_precision_bits),
+                     int(config.high_precision_bits))
+        self._bufs = {}
+        self._pending: List[int] = []
+        self._A = {}
+
+    def _peer_rank(self, j: int) -> int:
+        return dist.get_global_rank(self.group, j) if self.group is not None else j
+
+    def buffers(self, layer_idx: int, B: int, S_local: int, F: int, dtype) -> ShardBuffers:
+        bf = self._bufs.get(layer_idx)
+        if bf is None or (bf.B, bf.S_local, bf.F, bf.dtype) != (B, S_local, F, dtype):
+            bf = ShardBuffers(B, S_local, self.world, F, dtype, self.device, self.bits, self.emit_dequant,
+                              self.emit_packed)
+            self._bufs[layer_idx] = bf
+        return bf
+
+    def params(self, layer_idx: int, S_total: int):
+        flags = (L.EMIT_DEQUANT if self.emit_dequant else 0) | (L.EMIT_PACKED if self.emit_packed else 0)
+        return params_from_config(self.config, layer_idx, prompt_length(S_total),
+                                  self.propagator.get_layer_propagation_ratio(layer_idx), flags)
+
+    def enqueue_layer(self, K, V, W, layer_idx: int, layout: str = "bsf", params=None) -> ShardBuffers:
+        """K, V: this rank's [B, S_local, F] (or [B, H, S_local, D] with layout='bhsd'); W: its
+        [B, H, S_local, >=P] attention rows (prompt columns P of the GLOBAL prompt)."""
+        if layout == "bsf":
+            B, S_local, F = K.shape
+        else:
+            B, H, S_local, D = K.shape
+            F = H * D
+        S_total = S_local * self.world
+        row0 = self.rank * S_local
+        P = prompt_length(S_total)
+        if W.shape[0] != B or W.shape[2] != S_local or W.shape[3] < P:
+            raise ValueError(f"attention rows {tuple(W.shape)} do not match the shard [B={B}, S_local={S_local}, "
+                             f">= P={P}]")
+        p = params if params is not None else self.params(layer_idx, S_total)
+        bufs = self.buffers(layer_idx, B, S_local, F, K.dtype)
+        key = (B, S_local)
+        if key not in self._A:
+            self._A[key] = (torch.empty(B, S_local, dtype=torch.float32, device=self.device),
+                            torch.empty(self.world, B, S_local, dtype=torch.float32, device=self.device),
+                            torch.empty(B, S_total, dtype=torch.float32, device=self.device))
+        A_local, A_parts, A = self._A[key]
+        self.stages.aggregate(W, P, row0, S_total, A_local)
+        dist.all_gather_into_tensor(A_parts.view(-1), A_local.view(-1), group=self.group)
+        if B == 1:
+            A_glob = A_parts.view(1, S_total)  # rank-major = token order
+        else:
+            A.copy_(A_parts.permute(1, 0, 2).reshape(B, S_total))
+            A_glob = A
+        self.stages.finalize(A_glob, L.TORCH_DTYPE_CODE[W.dtype], p, bufs)
+        self.stages.ranges(bufs, self.world)
+        self.stages.quantize(K, V, layout, row0, self.rank, self.world, p, bufs)
+        self._pending.append(layer_idx)
+        return bufs
+
+    def exchange(self) -> List[ShardLayer]:
+        """One host read of every pending layer's rank bounds, then one grouped P2P batch: each rank's
+        packed K/V byte ranges and scale/zero-point rows go to every peer."""
+        layers = list(self._pending)
+        self._pending = []
+        if not layers:
+            return []
+        host = torch.stack([self._bufs[l].ranges for l in layers]).cpu()  # the single sync
+        out = [ShardLayer(l, self._bufs[l], host[k]) for k, l in enumerate(layers)]
+        if self.world == 1 or not self.emit_packed:
+            return out
+        ops = []
+        me = self.rank
+        for sl in out:
+            g = sl.bufs.g
+            cap = sl.bufs.S_total
+            sz = g.scale_zp.view(-1)
+            for b in range(sl.bufs.B):
+                r = sl.ranges[b]
+                spans = []
+                for j in range(self.world):
+                    b0, b1 = int(r[j, 1]), int(r[j + 1, 1])
+                    r0, r1 = int(r[j, 0]), int(r[j + 1, 0])
+                    spans.append(((b0, b1), ((b * cap + r0) * 4, (b * cap + r1) * 4)))
+                for j in range(self.world):
+                    if j == me:
+                        continue
+                    peer = self._peer_rank(j)
+                    for (lo, hi), buf in ((spans[me][0], g.packed_k), (spans[me][0], g.packed_v),
+                                          (spans[me][1], sz)):
+                        if hi > lo:
+                            ops.append(dist.P2POp(dist.isend, buf[lo:hi], peer, self.group))
+                    for (lo, hi), buf in ((spans[j][0], g.packed_k), (spans[j][0], g.packed_v),
+                                          (spans[j][1], sz)):
+                        if hi > lo:
+                            ops.append(dist.P2POp(dist.irecv, buf[lo:hi], peer, self.group))
+        if ops:
+            for w in dist.batch_isend_irecv(ops):
+                w.wait()
+        return out
+
+    # ------------------------------------------------------------------ reference-named entry point
+    def compress_layer_kv_cache(self, key_states, value_states, attention_weights, input_ids, layer_idx):
+        """Rank-local twin of RealTimePrefillCompressor.compress_layer_kv_cache: compresses this rank's
+        token chunk against the global selection and returns its dequantized kept rows, with the
+        exchanged packed KV of the layer in ``info['shard']``."""
+        self.enqueue_layer(key_states, value_states, attention_weights, layer_idx)
+        (sl,) = self.exchange()
+        k, v = sl.local_kv(self.rank)
+        info = {"layer_idx": layer_idx, "shard": sl, "rank": self.rank, "world_size": self.world,
+                "original_length": sl.bufs.S_total, "max_selected_length": max(sl.kept(b) for b in range(sl.bufs.B)),
+                "selection_mask": sl.bufs.g.mask.bool()}
+        return k, v, info

@@ -1,0 +1,99 @@
+"""GPU: the sequence-shard entry points of the C ABI (rtkv_attention_aggregation_shard,
+rtkv_finalize_select, rtkv_shard_ranges, rtkv_quantize_rows_shard) on one device.
+
+N ranks are simulated one after another on cuda:0 (no collective needed: the test concatenates
+the per-rank A itself and copies the rank byte ranges where the exchange would).  The union of the
+ranks' outputs must equal the fused single-GPU rtkv_compress_layer output byte for byte, and each
+rank's local dequantized rows must equal its slice of the single-GPU K'/V'."""
+import numpy as np
+import pytest
+import torch
+
+import synth
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module", autouse=True)
+def gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no ROCm device")
+
+
+def _dev(a, dtype):
+    if dtype == "float32":
+        return torch.from_numpy(np.ascontiguousarray(a)).cuda()
+    return torch.from_numpy(np.ascontiguousarray(a).view(np.int16)).cuda().view(getattr(torch, dtype))
+
+
+@pytest.mark.parametrize("dtype,S_total,world,H,D,ratio", [
+    ("float16", 4096, 2, 32, 128, 0.6),
+    ("float16", 8192, 4, 32, 128, 0.4),
+    ("bfloat16", 3000, 3, 8, 64, 0.8),     # P = 128, S_total*P not a multiple of 32 per shard boundary
+    ("float32", 1500, 5, 4, 64, 0.3),
+    ("float16", 640, 8, 4, 32, 0.05),      # tiny budget: the top-10% fallback across shards
+])
+def test_shards_union_equals_single_gpu(dtype, S_total, world, H, D, ratio):
+    import rtkv
+    from rtkv import _lib as L
+    from rtkv.sharded import HipShardStages, ShardBuffers
+    F = H * D
+    P = rtkv.prompt_length(S_total)
+    K, V = synth.kv(77, 1, S_total, F, dtype)
+    W = synth.attention_slice(77, 1, H, S_total, P, dtype)
+    Kd, Vd, Wd = _dev(K, dtype), _dev(V, dtype), _dev(W, dtype)
+    cfg = rtkv.CompressionConfig(alpha=0.8, beta=0.1, gamma=0.1, theta_h=0.4, theta_m=0.25, num_hidden_layers=1,
+                                 layer_weights=[1.0], high_precision_bits=8, medium_precision_bits=4,
+                                 low_precision_bits=2)
+    flags = L.EMIT_DEQUANT | L.EMIT_PACKED
+    params = rtkv.params_from_config(cfg, 0, P, ratio, flags)
+    bits = (2, 4, 8)
+    # single GPU reference run
+    ref = rtkv.LayerBuffers(1, S_total, F, Kd.dtype, "cuda", bits)
+    ws = rtkv.Workspace("cuda")
+    res = rtkv.compress_layer(Kd, Vd, Wd, params, ref, ws)
+    st = res.stats()
+    k_ref, v_ref = res.kv()
+    # shards
+    S_local = -(-S_total // world)
+    if S_local * world != S_total:
+        pytest.skip("uneven shards are not a configuration of the sharded path")
+    stages = HipShardStages("cuda")
+    A = torch.empty(1, S_total, dtype=torch.float32, device="cuda")
+    for j in range(world):
+        sl = slice(j * S_local, (j + 1) * S_local)
+        stages.aggregate(Wd[:, :, sl], P, j * S_local, S_total, A[:, sl])
+    bufs = [ShardBuffers(1, S_local, world, F, Kd.dtype, "cuda", bits) for _ in range(world)]
+    for j in range(world):
+        stages.finalize(A, L.TORCH_DTYPE_CODE[Wd.dtype], params, bufs[j])
+        stages.ranges(bufs[j], world)
+        sl = slice(j * S_local, (j + 1) * S_local)
+        stages.quantize(Kd[:, sl].contiguous(), Vd[:, sl].contiguous(), "bsf", j * S_local, j, world, params, bufs[j])
+    torch.cuda.synchronize()
+    n = st.max_kept
+    tot = st.total_packed_bytes
+    rg = bufs[0].ranges.cpu()
+    assert int(rg[0, -1, 0]) == n and int(rg[0, -1, 1]) == tot
+    for j in range(world):  # replicated selection
+        g = bufs[j].g
+        assert torch.equal(g.scores, ref.scores)
+        assert torch.equal(g.labels, ref.labels)
+        assert torch.equal(g.mask, ref.mask)
+        assert torch.equal(g.kept_index[:, :n], ref.kept_index[:, :n])
+        assert torch.equal(g.row_offset[:, :n], ref.row_offset[:, :n])
+        assert torch.equal(bufs[j].ranges.cpu(), rg)
+    pk = torch.zeros_like(ref.packed_k)
+    pv = torch.zeros_like(ref.packed_v)
+    sz = torch.zeros_like(ref.scale_zp)
+    for j in range(world):  # what the exchange assembles
+        r0, r1 = int(rg[0, j, 0]), int(rg[0, j + 1, 0])
+        b0, b1 = int(rg[0, j, 1]), int(rg[0, j + 1, 1])
+        g = bufs[j].g
+        pk[b0:b1] = g.packed_k[b0:b1]
+        pv[b0:b1] = g.packed_v[b0:b1]
+        sz[:, r0:r1] = g.scale_zp[:, r0:r1]
+        assert torch.equal(bufs[j].k_local[:, : r1 - r0], k_ref[:, r0:r1]), f"rank {j} local K'"
+        assert torch.equal(bufs[j].v_local[:, : r1 - r0], v_ref[:, r0:r1]), f"rank {j} local V'"
+    assert torch.equal(pk[:tot], ref.packed_k[:tot])
+    assert torch.equal(pv[:tot], ref.packed_v[:tot])
+    assert torch.equal(sz[:, :n], ref.scale_zp[:, :n])
