@@ -49,6 +49,8 @@ def parse():
     ap.add_argument("--no-packed", action="store_true", help="skip the packed-code output")
     ap.add_argument("--cpu-baseline-layers", type=int, default=2, help="layers of the oracle sample (0 = skip)")
     ap.add_argument("--quiet", action="store_true")
+    ap.add_argument("--sharded", action="store_true",
+                    help="use the sequence-sharded driver even at world size 1 (plumbing check)")
     return ap.parse_args()
 
 
@@ -199,6 +201,24 @@ class ShardedJob:
         return n
 
 
+def pmc_traffic(args, kernel="quant_rows_kernel"):
+    """HBM bytes per dispatch of `kernel` from the newest committed PMC summary (profiles/*_pmc.json,
+    written by profiles/summarize.py from separate rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of
+    this script at its default workload), or None for any other workload."""
+    import glob
+    default = (args.seq, args.layers, args.heads, args.head_dim, args.dtype, args.no_packed) == \
+        (16384, 32, 32, 128, "float16", False)
+    files = sorted(glob.glob(os.path.join(REPO, "profiles", "*_pmc.json")))
+    if not default or not files:
+        return None, None
+    with open(files[-1]) as f:
+        doc = json.load(f)
+    for name, v in doc["kernels"].items():
+        if kernel in name:
+            return v["hbm_bytes"], os.path.relpath(files[-1], REPO)
+    return None, None
+
+
 def cpu_baseline(args, job):
     """The C oracle (single thread, a literal restatement of the reference) on a bounded sample:
     the first `cpu_baseline_layers` layers of the same workload, same inputs."""
@@ -237,9 +257,13 @@ def main():
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
     torch.cuda.set_device(local)
     device = torch.device("cuda", local)
-    if world > 1:
+    sharded = world > 1 or args.sharded
+    if sharded:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=device)
+        if not dist.is_initialized():
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            os.environ.setdefault("MASTER_PORT", "29531")
+            dist.init_process_group("nccl", device_id=device, rank=rank, world_size=world)
         job = ShardedJob(args, device, rank, world)
     else:
         dist = None
@@ -273,9 +297,9 @@ def main():
     reps = 3
     k_ms = [0.0, 0.0, 0.0]
     for _ in range(reps):
-        job.step(events=events) if world == 1 else job.step()
+        job.step(events=events) if not sharded else job.step()
         torch.cuda.synchronize(device)
-        if world == 1:
+        if not sharded:
             for evs in events:
                 for k in range(3):
                     k_ms[k] += evs[k].elapsed_time(evs[k + 1])
@@ -304,16 +328,19 @@ def main():
                        "model": "Llama-2-7B (KV shapes only)", "global_batch": 1, "seq_len": job.S * world,
                        "parallelism": f"sequence-shard x{world}" if world > 1 else "single GPU"},
         }
-        if world > 1:
+        if sharded:
             line["exchange"] = {"received_bytes_per_rank_per_step": job.exchanged_bytes(),
                                 "kind": "one grouped RCCL send/recv batch of packed K/V codes + scale/zp "
                                         "(exact byte ranges, all peers at once)",
                                 "per_layer_collective": "RCCL all-gather of A (4 B/token)"}
-        if world == 1:
+        if not sharded:
             per_launch_ms = k_ms[2] / (reps * args.layers)
             achieved = sum(k4_bytes) / args.layers / (per_launch_ms / 1e3) / 1e9
+            traffic, src = pmc_traffic(args)
             line["roofline"] = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
-                                "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                                "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                                "traffic_source": src,
+                                "algorithmic_bytes_per_launch": round(sum(k4_bytes) / args.layers),
                                 "kernel": "quant_rows_kernel (K4)", "avg_launch_us": round(per_launch_ms * 1e3, 2)}
             line["kernel_us_per_layer"] = {"K1_aggregation": round(k_ms[0] / (reps * args.layers) * 1e3, 2),
                                            "K2_finalize": round(k_ms[1] / (reps * args.layers) * 1e3, 2),
