@@ -49,6 +49,9 @@ def parse():
     ap.add_argument("--no-packed", action="store_true", help="skip the packed-code output")
     ap.add_argument("--cpu-baseline-layers", type=int, default=2, help="layers of the oracle sample (0 = skip)")
     ap.add_argument("--quiet", action="store_true")
+    ap.add_argument("--importance", default="w", choices=["w", "qk"],
+                    help="w: the reference's attention-weights input (prompt slice); qk: fused mode "
+                         "(Q + prompt keys + row LSE, K1' on MFMA)")
     ap.add_argument("--sharded", action="store_true",
                     help="use the sequence-sharded driver even at world size 1 (plumbing check)")
     return ap.parse_args()
@@ -66,6 +69,24 @@ def synth_layer(l: int, S: int, H: int, D: int, P: int, dtype, device, gen, row0
     raw = raw * causal
     W = raw / raw.sum(-1, keepdim=True) * torch.rand(1, H, S, 1, generator=gen, device=device)
     return K, V, W.to(dtype)
+
+
+def synth_qk(S: int, H: int, D: int, K, dtype, device, gen, causal=True):
+    """Fused-mode inputs for one layer: Q [1,H,S,D] ~ N(0,1) and the exact fp32 row LSE of the causal
+    softmax(Q·Kᵀ/√d) over all S keys (setup only; computed in row chunks)."""
+    Q = torch.randn(1, H, S, D, generator=gen, device=device, dtype=torch.float32).to(dtype)
+    Kh = K.view(1, S, H, D).permute(0, 2, 1, 3)
+    lse = torch.empty(1, H, S, dtype=torch.float32, device=device)
+    step = 2048
+    for i0 in range(0, S, step):
+        i1 = min(S, i0 + step)
+        x = torch.matmul(Q[:, :, i0:i1].float(), Kh.float().transpose(2, 3)) * (1.0 / D ** 0.5)
+        if causal:
+            x.masked_fill_(torch.arange(S, device=device)[None, :] > torch.arange(i0, i1, device=device)[:, None],
+                           float("-inf"))
+        lse[:, :, i0:i1] = torch.logsumexp(x, dim=-1)
+        del x
+    return Q, lse
 
 
 class Job:
@@ -92,7 +113,13 @@ class Job:
         gen.manual_seed(1234 + 7919 * rank)
         self.inputs, self.bufs, self.params = [], [], []
         for l in range(args.layers):
-            self.inputs.append(synth_layer(l, self.S, self.H, self.D, self.P, self.dtype, device, gen))
+            K, V, W = synth_layer(l, self.S, self.H, self.D, self.P, self.dtype, device, gen)
+            if args.importance == "qk":
+                Q, lse = synth_qk(self.S, self.H, self.D, K, self.dtype, device, gen)
+                self.inputs.append((K, V, Q, lse))
+                del W
+            else:
+                self.inputs.append((K, V, W))
             self.bufs.append(rtkv.LayerBuffers(1, self.S, self.F, self.dtype, device, self.bits,
                                                emit_dequant=True, emit_packed=self.emit_packed))
             self.params.append(rtkv.params_from_config(self.cfg, l, self.P, prop.get_layer_propagation_ratio(l), flags))
@@ -105,19 +132,28 @@ class Job:
         import rtkv
         from rtkv import _lib as L
         import ctypes
+        qk = self.args.importance == "qk"
         for l in range(self.args.layers):
-            K, V, W = self.inputs[l]
-            if events is None:
-                rtkv.compress_layer(K, V, W, self.params[l], self.bufs[l], self.ws)
+            if qk:
+                K, V, Q, lse = self.inputs[l]
+                if events is None:
+                    rtkv.compress_layer_qk(K, V, Q, lse, self.params[l], self.bufs[l], self.ws)
+                    continue
+                kd, wd = rtkv.engine.kv_desc(K, V), rtkv.engine.qk_desc(Q, K, lse)
+                fn = L.lib().rtkv_compress_layer_qk_events
             else:
+                K, V, W = self.inputs[l]
+                if events is None:
+                    rtkv.compress_layer(K, V, W, self.params[l], self.bufs[l], self.ws)
+                    continue
                 kd, wd = rtkv.engine.kv_desc(K, V), rtkv.engine.attn_desc(W)
-                out = self.bufs[l].out_struct()
-                out.o_stride_h = kd.D
-                ev = (ctypes.c_void_p * 4)(*[e.cuda_event for e in events[l]])
-                L.check(L.lib().rtkv_compress_layer_events(ctypes.byref(kd), ctypes.byref(wd),
-                                                           ctypes.byref(self.params[l]), ctypes.byref(out),
-                                                           self.ws.buf.data_ptr(), self.ws.buf.numel(),
-                                                           L.stream_ptr(self.device), ev), "compress_layer_events")
+                fn = L.lib().rtkv_compress_layer_events
+            out = self.bufs[l].out_struct()
+            out.o_stride_h = kd.D
+            ev = (ctypes.c_void_p * 4)(*[e.cuda_event for e in events[l]])
+            L.check(fn(ctypes.byref(kd), ctypes.byref(wd), ctypes.byref(self.params[l]), ctypes.byref(out),
+                       self.ws.buf.data_ptr(), self.ws.buf.numel(), L.stream_ptr(self.device), ev),
+                    "compress_layer_events")
 
     def layer_bytes(self):
         """Algorithmic HBM bytes per layer: total and the K4 (quantize+pack+compact) part."""
@@ -127,7 +163,10 @@ class Job:
         for l in range(self.args.layers):
             st = decode_stats(self.bufs[l].stats.cpu().numpy().tobytes(), 1)
             Sp, pk = st.max_kept, st.total_packed_bytes
-            w_read = self.H * self.S * self.P * e               # prompt columns of W
+            if self.args.importance == "qk":                     # Q + row LSE + prompt keys
+                w_read = self.H * self.S * self.D * e + 4 * self.H * self.S + self.P * self.F * e
+            else:
+                w_read = self.H * self.S * self.P * e               # prompt columns of W
             kv_read = 2 * Sp * self.F * e                        # kept rows of K and V, read once
             deq = 2 * Sp * self.F * e                            # dequantized K', V'
             packed = (2 * pk + Sp * 16) if self.emit_packed else 0   # codes + scale/zp
@@ -206,8 +245,8 @@ def pmc_traffic(args, kernel="quant_rows_kernel"):
     written by profiles/summarize.py from separate rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of
     this script at its default workload), or None for any other workload."""
     import glob
-    default = (args.seq, args.layers, args.heads, args.head_dim, args.dtype, args.no_packed) == \
-        (16384, 32, 32, 128, "float16", False)
+    default = (args.seq, args.layers, args.heads, args.head_dim, args.dtype, args.no_packed, args.importance) == \
+        (16384, 32, 32, 128, "float16", False, "w")
     files = sorted(glob.glob(os.path.join(REPO, "profiles", "*_pmc.json")))
     if not default or not files:
         return None, None
@@ -222,7 +261,7 @@ def pmc_traffic(args, kernel="quant_rows_kernel"):
 def cpu_baseline(args, job):
     """The C oracle (single thread, a literal restatement of the reference) on a bounded sample:
     the first `cpu_baseline_layers` layers of the same workload, same inputs."""
-    if args.cpu_baseline_layers <= 0:
+    if args.cpu_baseline_layers <= 0 or args.importance != "w":
         return None
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     import numpy as np
@@ -322,7 +361,7 @@ def main():
             "vs_baseline": None,
             "dtype": {"float16": "f16", "bfloat16": "bf16", "float32": "f32"}[args.dtype],
             "data": "synthetic (seeded torch RNG; K,V ~ N(0,1), W = causal u^4-softmax-like prompt slice)",
-            "config": {"workload": f"Llama-2-7B prefill KV compression, {args.layers} layers, "
+            "config": {"workload": f"Llama-2-7B prefill KV compression{' (fused Q/LSE importance)' if args.importance == 'qk' else ''}, {args.layers} layers, "
                                    f"S={job.S * world} ({job.S}/rank), {args.heads}x{args.head_dim}, "
                                    f"P={job.P}, bits 8/4/2, ratios .8/.6/.4, dequant+packed outputs",
                        "model": "Llama-2-7B (KV shapes only)", "global_batch": 1, "seq_len": job.S * world,
@@ -346,6 +385,13 @@ def main():
                                            "K2_finalize": round(k_ms[1] / (reps * args.layers) * 1e3, 2),
                                            "K4_quant_pack": round(per_launch_ms * 1e3, 2)}
             line["cpu_baseline"] = cpu_baseline(args, job)
+            if args.importance == "qk":  # K1' on MFMA: the Q·K_P^T contraction against the dense f16 peak
+                k1_ms = k_ms[0] / (reps * args.layers)
+                flops = 2.0 * job.H * job.S * job.P * job.D
+                tf = flops / (k1_ms / 1e3) / 1e12
+                line["k1_mfma"] = {"bound": "mfma", "achieved": round(tf, 2), "peak": 2500.0, "unit": "TFLOP/s",
+                                   "frac": round(tf / 2500.0, 4), "avg_launch_us": round(k1_ms * 1e3, 2),
+                                   "hbm_GBs": round((job.H * job.S * job.D * 2 + 4 * job.H * job.S) / (k1_ms / 1e3) / 1e9, 1)}
         print(json.dumps(line), flush=True)
     if dist is not None:
         dist.barrier()

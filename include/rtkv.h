@@ -104,6 +104,27 @@ typedef struct rtkv_kv_desc {
   int64_t stride_b, stride_s, stride_h;
 } rtkv_kv_desc;
 
+/* Fused importance input (no attention matrix): queries, the P prompt keys and the row log-sum-exp
+ * of the model's softmax.  W[b,h,i,p] = exp(q[b,h,i]·k[b,h/(H/Hkv),p]·scale − lse[b,h,i]) for p < P
+ * (and p <= row0 + i when causal), which is the reference's
+ * softmax(Q·Kᵀ/√d + mask) (modified_llama.py:88-94) restricted to the prompt columns.
+ * q[b,h,i,d] at q_dev + b*q_stride_b + h*q_stride_h + i*q_stride_s + d; k likewise with p for i;
+ * lse[b,h,i] at lse_dev + b*lse_stride_b + h*lse_stride_h + i (fp32). */
+typedef struct rtkv_qk_desc {
+  const void* q_dev;
+  const void* k_dev;
+  const float* lse_dev;
+  int32_t dtype;                       /* RTKV_F16 or RTKV_BF16 (MFMA operands) */
+  int32_t causal;
+  int64_t B, H, Hkv, S, D;
+  int64_t q_stride_b, q_stride_h, q_stride_s;
+  int64_t k_stride_b, k_stride_h, k_stride_s;
+  int64_t lse_stride_b, lse_stride_h;
+  float scale;                         /* 1/sqrt(head_dim) in the reference (modified_llama.py:89) */
+  int32_t reserved;
+  int64_t row0;                        /* global position of query row 0 (sequence shards), else 0 */
+} rtkv_qk_desc;
+
 /* Per-batch-row statistics (device-resident; one entry per batch row after the header). */
 typedef struct rtkv_batch_stats {
   int64_t class_count[3];    /* tokens per class, dynamic_quantization.py:50-57 */
@@ -290,6 +311,22 @@ int rtkv_quantize_rows_shard(const rtkv_kv_desc* kv, int64_t row0, int64_t S_tot
 int rtkv_shard_ranges(const int32_t* kept_index_dev, const int64_t* row_offset_dev,
                       const rtkv_layer_stats* stats_dev, int64_t B, int64_t row_capacity, int64_t S_local,
                       int32_t nranks, int64_t* ranges_dev, void* stream);
+
+/* ------------------------------------------------------------------------------------------------
+ * Fused importance mode (MFMA): the aggregation A from Q, K_prompt and the row LSE instead of W.
+ * A is fp32 (W is not rounded to the input dtype: the reference model runs in fp32); parity with the
+ * W path is a tolerance, not bit-exact.  Replaces compute_attention_aggregation
+ * (token_importance.py:21-47) fed by the materialised softmax of modified_llama.py:88-94.
+ * ---------------------------------------------------------------------------------------------- */
+int rtkv_importance_qk_lse(const rtkv_qk_desc* q, int32_t prompt_len, float* A_dev, void* stream);
+
+/* rtkv_compress_layer with the fused importance mode (K1' on MFMA, then K2 and K4 unchanged). */
+int rtkv_compress_layer_qk(const rtkv_kv_desc* kv, const rtkv_qk_desc* q, const rtkv_layer_params* p,
+                           const rtkv_layer_out* out, void* workspace_dev, size_t workspace_bytes,
+                           void* stream);
+int rtkv_compress_layer_qk_events(const rtkv_kv_desc* kv, const rtkv_qk_desc* q, const rtkv_layer_params* p,
+                                  const rtkv_layer_out* out, void* workspace_dev, size_t workspace_bytes,
+                                  void* stream, void* const events[4]);
 
 /* Reconstruct dequantized rows from packed codes (+ scale/zp, labels of the kept rows); bit-identical
  * to the RTKV_EMIT_DEQUANT output.  rows_per_batch[b] rows of batch row b are decoded.

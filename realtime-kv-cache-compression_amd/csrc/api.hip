@@ -189,13 +189,15 @@ int rtkv_quantize_rows(const rtkv_kv_desc* kv, const uint8_t* labels_dev, const 
   return launch_quant(q, (hipStream_t)stream);
 }
 
-int rtkv_compress_layer_events(const rtkv_kv_desc* kv, const rtkv_attn_desc* w, const rtkv_layer_params* p,
-                               const rtkv_layer_out* out, void* workspace_dev, size_t workspace_bytes, void* stream,
-                               void* const events[4]) {
+// The fused layer: K1 (W aggregation, or K1' on MFMA when q != null) → K2 → K4.
+static int compress_layer_impl(const rtkv_kv_desc* kv, const rtkv_attn_desc* w, const rtkv_qk_desc* qk,
+                               const rtkv_layer_params* p, const rtkv_layer_out* out, void* workspace_dev,
+                               size_t workspace_bytes, void* stream, void* const events[4]) {
   int rc = check_params(p);
   if (rc) return rc;
-  RTKV_REQUIRE(kv && w && out, "null descriptor");
-  RTKV_REQUIRE(kv->B == w->B && kv->S == w->S, "K/V and attention weights disagree on B or S");
+  RTKV_REQUIRE(kv && (w || qk) && out, "null descriptor");
+  if (w) RTKV_REQUIRE(kv->B == w->B && kv->S == w->S, "K/V and attention weights disagree on B or S");
+  if (qk) RTKV_REQUIRE(kv->B == qk->B && kv->S == qk->S, "K/V and queries disagree on B or S");
   RTKV_REQUIRE(out->scores_dev && out->labels_dev && out->mask_dev && out->kept_index_dev && out->stats_dev,
                "compress_layer needs scores, labels, mask, kept_index and stats outputs");
   RTKV_REQUIRE(out->row_capacity >= kv->S, "row_capacity must be >= S (every token may be kept)");
@@ -230,14 +232,20 @@ int rtkv_compress_layer_events(const rtkv_kv_desc* kv, const rtkv_attn_desc* w, 
   x.zero0_bytes = select_zero_bytes(kv->B);
   x.zero1 = out->stats_dev;
   x.zero1_bytes = rtkv_stats_bytes(kv->B);
-  rc = launch_aggregation(*w, p->prompt_len, ws.A, st, x);
+  if (w) {
+    rc = launch_aggregation(*w, p->prompt_len, ws.A, st, x);
+  } else {
+    x.S_total = kv->S;
+    x.row0 = 0;
+    rc = launch_qk_importance(*qk, p->prompt_len, ws.A, st, x, &nparts);
+  }
   if (rc) return rc;
   if ((rc = mark(1))) return rc;
   a.A = ws.A;
   a.A_part = ws.Apart;
   a.A_nparts = nparts;
   a.T2 = ws.T2;
-  a.a_dtype = w->dtype;
+  a.a_dtype = w ? w->dtype : RTKV_F32;
   a.scores = out->scores_dev;
   a.labels = out->labels_dev;
   a.mask = out->mask_dev;
@@ -258,9 +266,34 @@ int rtkv_compress_layer_events(const rtkv_kv_desc* kv, const rtkv_attn_desc* w, 
   return mark(3);
 }
 
+int rtkv_compress_layer_events(const rtkv_kv_desc* kv, const rtkv_attn_desc* w, const rtkv_layer_params* p,
+                               const rtkv_layer_out* out, void* workspace_dev, size_t workspace_bytes, void* stream,
+                               void* const events[4]) {
+  RTKV_REQUIRE(w != nullptr, "null attention descriptor");
+  return compress_layer_impl(kv, w, nullptr, p, out, workspace_dev, workspace_bytes, stream, events);
+}
+
 int rtkv_compress_layer(const rtkv_kv_desc* kv, const rtkv_attn_desc* w, const rtkv_layer_params* p,
                         const rtkv_layer_out* out, void* workspace_dev, size_t workspace_bytes, void* stream) {
   return rtkv_compress_layer_events(kv, w, p, out, workspace_dev, workspace_bytes, stream, nullptr);
+}
+
+int rtkv_compress_layer_qk_events(const rtkv_kv_desc* kv, const rtkv_qk_desc* q, const rtkv_layer_params* p,
+                                  const rtkv_layer_out* out, void* workspace_dev, size_t workspace_bytes, void* stream,
+                                  void* const events[4]) {
+  RTKV_REQUIRE(q != nullptr, "null query descriptor");
+  return compress_layer_impl(kv, nullptr, q, p, out, workspace_dev, workspace_bytes, stream, events);
+}
+
+int rtkv_compress_layer_qk(const rtkv_kv_desc* kv, const rtkv_qk_desc* q, const rtkv_layer_params* p,
+                           const rtkv_layer_out* out, void* workspace_dev, size_t workspace_bytes, void* stream) {
+  return rtkv_compress_layer_qk_events(kv, q, p, out, workspace_dev, workspace_bytes, stream, nullptr);
+}
+
+int rtkv_importance_qk_lse(const rtkv_qk_desc* q, int32_t prompt_len, float* A_dev, void* stream) {
+  RTKV_REQUIRE(q != nullptr, "null query descriptor");
+  AggExtras x;
+  return launch_qk_importance(*q, prompt_len, A_dev, (hipStream_t)stream, x, nullptr);
 }
 
 // ---------------------------------------------------------------------------------- sequence shards

@@ -164,7 +164,19 @@ struct AggExtras {
   int64_t row0 = 0;
   int64_t S_total = 0;
 };
+// The K1 grid clears the selection scratch of the next kernels (4-byte words, grid-strided).
+__device__ __forceinline__ void zero_regions(const AggExtras& x) {
+  const int64_t nb = (int64_t)gridDim.x * gridDim.y;
+  const int64_t id = (int64_t)blockIdx.y * gridDim.x + blockIdx.x;
+  for (int r = 0; r < 2; ++r) {
+    uint32_t* p = static_cast<uint32_t*>(r ? x.zero1 : x.zero0);
+    const int64_t words = (int64_t)((r ? x.zero1_bytes : x.zero0_bytes) / 4);
+    if (!p) continue;
+    for (int64_t w = id * blockDim.x + threadIdx.x; w < words; w += nb * blockDim.x) p[w] = 0u;
+  }
+}
 int launch_aggregation(const rtkv_attn_desc& w, int P, float* A, hipStream_t st, const AggExtras& x = AggExtras());
+int launch_qk_importance(const rtkv_qk_desc& q, int P, float* A, hipStream_t st, const AggExtras& x, int* nparts);
 int launch_position_bias(int64_t S, float* pos, hipStream_t st);
 int launch_minmax_normalize(const void* x, int dt, int64_t B, int64_t S, void* out, hipStream_t st);
 

@@ -71,18 +71,6 @@ __device__ __forceinline__ void unpack_vec(const typename VecT<DT, VEC>::T& v, f
   }
 }
 
-// The K1 grid clears the selection scratch of the next kernels (4-byte words, grid-strided).
-__device__ __forceinline__ void zero_regions(const AggExtras& x) {
-  const int64_t nb = (int64_t)gridDim.x * gridDim.y;
-  const int64_t id = (int64_t)blockIdx.y * gridDim.x + blockIdx.x;
-  for (int r = 0; r < 2; ++r) {
-    uint32_t* p = static_cast<uint32_t*>(r ? x.zero1 : x.zero0);
-    const int64_t words = (int64_t)((r ? x.zero1_bytes : x.zero0_bytes) / 4);
-    if (!p) continue;
-    for (int64_t w = id * blockDim.x + threadIdx.x; w < words; w += nb * blockDim.x) p[w] = 0u;
-  }
-}
-
 // Fast path: P % VEC == 0, 16-byte aligned rows.  Thread → one VEC-wide chunk of one token row.
 template <int DT, int VEC>
 __global__ __launch_bounds__(256) void aggregation_vec_kernel(const typename Dt<DT>::S* __restrict__ W,

@@ -8,7 +8,8 @@ from . import _lib
 from .base_config import CompressionConfig
 from .compression_layers import AdaptiveQuantization, CompressedKVCache, unpack_layer
 from .dynamic_quantization import DynamicPrecisionQuantizer
-from .engine import LayerBuffers, LayerResult, Workspace, compress_layer, params_from_config, prompt_length
+from .engine import (LayerBuffers, LayerResult, Workspace, compress_layer, compress_layer_qk, importance_qk_lse,
+                     params_from_config, prompt_length)
 from .selective_propagation import SelectiveTokenPropagator
 from .token_importance import LayerWiseImportanceTracker, PromptGuidedImportanceScorer
 from .unified_compressor import CompressionHook, RealTimePrefillCompressor, UnifiedCompressor
@@ -17,7 +18,8 @@ __all__ = [
     "CompressionConfig", "RealTimePrefillCompressor", "UnifiedCompressor", "CompressionHook",
     "PromptGuidedImportanceScorer", "LayerWiseImportanceTracker", "DynamicPrecisionQuantizer",
     "SelectiveTokenPropagator", "CompressedKVCache", "AdaptiveQuantization", "unpack_layer",
-    "LayerBuffers", "LayerResult", "Workspace", "compress_layer", "params_from_config", "prompt_length",
+    "LayerBuffers", "LayerResult", "Workspace", "compress_layer", "compress_layer_qk", "importance_qk_lse",
+    "params_from_config", "prompt_length",
 ]
 
 __version__ = "0.1.0"

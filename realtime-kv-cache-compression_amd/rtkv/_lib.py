@@ -43,6 +43,15 @@ class KVDesc(ctypes.Structure):
                 ("H", c_i64), ("D", c_i64), ("stride_b", c_i64), ("stride_s", c_i64), ("stride_h", c_i64)]
 
 
+class QKDesc(ctypes.Structure):
+    _fields_ = [("q_dev", c_p), ("k_dev", c_p), ("lse_dev", c_p), ("dtype", c_i32), ("causal", c_i32),
+                ("B", c_i64), ("H", c_i64), ("Hkv", c_i64), ("S", c_i64), ("D", c_i64),
+                ("q_stride_b", c_i64), ("q_stride_h", c_i64), ("q_stride_s", c_i64),
+                ("k_stride_b", c_i64), ("k_stride_h", c_i64), ("k_stride_s", c_i64),
+                ("lse_stride_b", c_i64), ("lse_stride_h", c_i64), ("scale", c_f), ("reserved", c_i32),
+                ("row0", c_i64)]
+
+
 class BatchStats(ctypes.Structure):
     _fields_ = [("class_count", c_i64 * 3), ("kept", c_i64), ("kept_class", c_i64 * 3), ("cost_units", c_i64),
                 ("packed_bytes", c_i64), ("fallback", c_i32), ("reserved", c_i32), ("kept_score_sum", c_d)]
@@ -89,6 +98,9 @@ _SIGS = {
     "rtkv_finalize_select": ([c_p, c_i32, c_i64, c_i64, c_p, c_p, c_i64, c_i32, c_p, c_sz, c_p], c_i32),
     "rtkv_quantize_rows_shard": ([c_p, c_i64, c_i64, c_i32, c_i32, c_p, c_p, c_p, c_p, c_p, c_p], c_i32),
     "rtkv_shard_ranges": ([c_p, c_p, c_p, c_i64, c_i64, c_i64, c_i32, c_p, c_p], c_i32),
+    "rtkv_importance_qk_lse": ([c_p, c_i32, c_p, c_p], c_i32),
+    "rtkv_compress_layer_qk": ([c_p, c_p, c_p, c_p, c_p, c_sz, c_p], c_i32),
+    "rtkv_compress_layer_qk_events": ([c_p, c_p, c_p, c_p, c_p, c_sz, c_p, c_p], c_i32),
     "rtkv_gather_rows": ([c_p, c_i64, c_i64, c_i64, c_p, c_i64, c_i64, c_p, c_i64, c_i64, c_p, c_p], c_i32),
 }
 EXPORTS = tuple(_SIGS)

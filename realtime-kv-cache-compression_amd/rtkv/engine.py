@@ -76,6 +76,42 @@ def kv_desc(K: torch.Tensor, V: torch.Tensor, layout: str = "bsf", heads: Option
     return d
 
 
+def qk_desc(Q: torch.Tensor, K: torch.Tensor, lse: torch.Tensor, scale: Optional[float] = None,
+            causal: bool = True, k_layout: str = "bsf", kv_heads: Optional[int] = None, row0: int = 0) -> L.QKDesc:
+    """Fused importance input: Q [B,H,S,D] (model layout, unit d stride), keys whose first P rows are
+    the prompt keys — K [B,S,Hkv*D] ('bsf', the reference's compress_layer_kv_cache input) or
+    [B,Hkv,S,D] ('bhsd') — and the row log-sum-exp lse [B,H,S] (fp32) of the model's softmax."""
+    if Q.dim() != 4 or Q.stride(-1) != 1:
+        raise ValueError("queries must be [B, H, S, D] with unit head_dim stride")
+    B, H, S, D = Q.shape
+    if K.dtype != Q.dtype:
+        raise ValueError("queries and keys must share a dtype")
+    if lse.dtype != torch.float32 or tuple(lse.shape) != (B, H, S) or lse.stride(-1) != 1:
+        raise ValueError(f"lse must be float32 [B, H, S] = {(B, H, S)} with unit stride")
+    d = L.QKDesc()
+    d.q_dev, d.k_dev, d.lse_dev = Q.data_ptr(), K.data_ptr(), lse.data_ptr()
+    d.dtype = L.dtype_code(Q)
+    d.causal = int(bool(causal))
+    d.B, d.H, d.S, d.D = B, H, S, D
+    d.q_stride_b, d.q_stride_h, d.q_stride_s = Q.stride(0), Q.stride(1), Q.stride(2)
+    if k_layout == "bsf":
+        if K.dim() != 3 or K.stride(-1) != 1 or K.shape[2] % D:
+            raise ValueError("bsf keys must be [B, S, Hkv*D] with unit stride")
+        d.Hkv = K.shape[2] // D
+        d.k_stride_b, d.k_stride_h, d.k_stride_s = K.stride(0), D, K.stride(1)
+    elif k_layout == "bhsd":
+        if K.dim() != 4 or K.stride(-1) != 1 or K.shape[3] != D:
+            raise ValueError("bhsd keys must be [B, Hkv, S, D] with unit stride")
+        d.Hkv = K.shape[1]
+        d.k_stride_b, d.k_stride_h, d.k_stride_s = K.stride(0), K.stride(1), K.stride(2)
+    else:
+        raise ValueError(k_layout)
+    d.lse_stride_b, d.lse_stride_h = lse.stride(0), lse.stride(1)
+    d.scale = float(scale) if scale is not None else 1.0 / float(D) ** 0.5
+    d.row0 = int(row0)
+    return d
+
+
 @dataclass
 class LayerStats:
     max_kept: int
@@ -181,6 +217,37 @@ class LayerResult:
         n = self.B * st.max_kept * self.bufs.F
         shape = (self.B, st.max_kept, self.bufs.F)
         return self.bufs.k_out[:n].view(shape), self.bufs.v_out[:n].view(shape)
+
+
+def compress_layer_qk(K, V, Q, lse, params: L.LayerParams, bufs: LayerBuffers, workspace: Workspace,
+                      layout: str = "bsf", causal: bool = True, scale: Optional[float] = None,
+                      stream: Optional[int] = None) -> LayerResult:
+    """compress_layer in the fused importance mode: K1' computes A from Q, the prompt keys (the first
+    P rows of K) and the row LSE on MFMA; K2 and K4 are unchanged."""
+    L.require_device(K, V, Q, lse)
+    kd = kv_desc(K, V, layout)
+    qd = qk_desc(Q, K, lse, scale=scale, causal=causal, k_layout=layout)
+    if qd.B != kd.B or qd.S != kd.S:
+        raise ValueError(f"queries {tuple(Q.shape)} do not match key states {tuple(K.shape)}")
+    ws = workspace.get(kd.B, kd.S)
+    out = bufs.out_struct()
+    out.o_stride_h = kd.D
+    st = L.stream_ptr(K.device) if stream is None else stream
+    rc = L.lib().rtkv_compress_layer_qk(ctypes.byref(kd), ctypes.byref(qd), ctypes.byref(params), ctypes.byref(out),
+                                        ws.data_ptr(), ws.numel(), st)
+    L.check(rc, "rtkv_compress_layer_qk")
+    return LayerResult(bufs, kd.B)
+
+
+def importance_qk_lse(Q, K, lse, prompt_len: int, causal: bool = True, scale: Optional[float] = None,
+                      k_layout: str = "bsf") -> torch.Tensor:
+    """A [B, S] (fp32) of the fused importance mode alone (rtkv_importance_qk_lse)."""
+    L.require_device(Q, K, lse)
+    qd = qk_desc(Q, K, lse, scale=scale, causal=causal, k_layout=k_layout)
+    A = torch.empty(qd.B, qd.S, dtype=torch.float32, device=Q.device)
+    L.check(L.lib().rtkv_importance_qk_lse(ctypes.byref(qd), int(prompt_len), A.data_ptr(), L.stream_ptr(Q.device)),
+            "rtkv_importance_qk_lse")
+    return A
 
 
 def compress_layer(K, V, W, params: L.LayerParams, bufs: LayerBuffers, workspace: Workspace,

@@ -15,7 +15,7 @@ import torch
 
 from . import _lib as L
 from .dynamic_quantization import F16_OVERFLOW_MSG, DynamicPrecisionQuantizer
-from .engine import LayerBuffers, Workspace, compress_layer, params_from_config, prompt_length
+from .engine import LayerBuffers, Workspace, compress_layer, compress_layer_qk, params_from_config, prompt_length
 from .selective_propagation import SelectiveTokenPropagator
 from .token_importance import LayerWiseImportanceTracker
 
@@ -45,19 +45,30 @@ class RealTimePrefillCompressor:
         return (int(c.low_precision_bits), int(c.medium_precision_bits), int(c.high_precision_bits))
 
     def compress_layer_kv_cache(self, key_states: torch.Tensor, value_states: torch.Tensor,
-                                attention_weights: torch.Tensor, input_ids: torch.Tensor,
-                                layer_idx: int) -> Tuple[torch.Tensor, torch.Tensor, Dict]:
+                                attention_weights: Optional[torch.Tensor], input_ids: torch.Tensor,
+                                layer_idx: int, query_states: Optional[torch.Tensor] = None,
+                                attention_lse: Optional[torch.Tensor] = None,
+                                causal: bool = True) -> Tuple[torch.Tensor, torch.Tensor, Dict]:
         """K, V [B,S,F] + attention [B,H,S,S] (or its [B,H,S,P] prompt columns) → (K', V', info).
 
         K', V' are the dequantized kept rows in ascending token order, zero-padded across the batch,
-        in the input dtype — bit-identical to the reference."""
+        in the input dtype — bit-identical to the reference.
+
+        Fused importance mode (extension): pass attention_weights=None with
+        query_states [B,H,S,D] and attention_lse [B,H,S] (fp32 row log-sum-exp of the model's
+        softmax); the prompt-attention mass is then computed on MFMA from Q, the first P keys and the
+        LSE (rtkv_compress_layer_qk) — within tolerance of the W path, not bit-exact."""
         start_time = time.time()
-        L.require_device(key_states, value_states, attention_weights)
+        fused = attention_weights is None
+        if fused and (query_states is None or attention_lse is None):
+            raise ValueError("attention_weights=None needs query_states and attention_lse (fused importance mode)")
+        L.require_device(key_states, value_states, *((query_states, attention_lse) if fused else (attention_weights,)))
         K = key_states if key_states.stride(-1) == 1 else key_states.contiguous()
         V = value_states if value_states.stride() == K.stride() else value_states.contiguous()
         if V.stride() != K.stride():
             K, V = K.contiguous(), V.contiguous()
-        W = attention_weights if attention_weights.stride(-1) == 1 else attention_weights.contiguous()
+        if not fused:
+            W = attention_weights if attention_weights.stride(-1) == 1 else attention_weights.contiguous()
         B, S, F = K.shape
         P = prompt_length(S)
         ratio = self.propagator.get_layer_propagation_ratio(layer_idx)
@@ -69,7 +80,11 @@ class RealTimePrefillCompressor:
         params = params_from_config(self.config, layer_idx, P, ratio, flags)
         bufs = LayerBuffers(B, S, F, K.dtype, K.device, bits, emit_dequant=True, emit_packed=emit_packed)
         ws = self._workspaces.setdefault(K.device, Workspace(K.device))
-        res = compress_layer(K, V, W, params, bufs, ws)
+        if fused:
+            Q = query_states if query_states.stride(-1) == 1 else query_states.contiguous()
+            res = compress_layer_qk(K, V, Q, attention_lse.contiguous(), params, bufs, ws, causal=causal)
+        else:
+            res = compress_layer(K, V, W, params, bufs, ws)
         st = res.stats()  # the one host sync of the layer
         if st.error_flags & L.FLAG_F16_QMAX_OVERFLOW:
             raise RuntimeError(F16_OVERFLOW_MSG)
