@@ -9,19 +9,22 @@
 // The reference model runs in fp32, so W is kept in fp32 here (no rounding to the
 // input dtype) and A is produced as fp32; parity is a tolerance (north_star: 1e-3 rel on scores).
 //
-// The Q·K_Pᵀ contraction runs on MFMA (v_mfma_f32_32x32x16_{f16,bf16}): a workgroup owns 32 query
-// rows; its 4 waves split the heads (h ≡ wave mod 4) and each wave computes the full 32 × P tile
-// (P ≤ 128: up to four 32×32 accumulators) per head, k-stepping over D in 16s.  Fragment maps
-// (cdna_hip_programming.md §3): lane l, r = l & 31, hh = l >> 5 holds A[row r][k 8hh..8hh+7] and
-// B[k 8hh..8hh+7][col r]; the accumulator holds col r, rows (reg & 3) + 8(reg >> 2) + 4hh.  The
-// exp and the head sum stay in registers; one LDS reduction over the 4 waves ends the block.
+// Work decomposition (gfx950, wave64): a workgroup owns 64 query rows of one batch row, one wave
+// per 16 rows, and walks the heads.  Per head the P×D prompt-key tile is staged in LDS once
+// (double-buffered, shared by the 4 waves) and each wave computes its 16 × P logits with
+// v_mfma_f32_16x16x32_{f16,bf16} (NT column tiles of 16, KS k-steps of 32), then
+// exp2(x·scale·log2e − lse·log2e) and the head sum in registers.  Next head's keys and query
+// fragments are loaded from HBM while the current head computes.  Fragment maps
+// (cdna_hip_programming.md §3): lane l holds A[row l&15][k 8(l>>4)..+7] and
+// B[k 8(l>>4)..+7][col l&15]; the accumulator holds col l&15, rows 4(l>>4) + reg.
+// Waves own disjoint rows, so the only reduction is over the 16 columns held across lanes.
 #include "common.h"
 
 namespace rtkv {
 
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
-typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 struct QKArgs {
   rtkv_qk_desc q;
@@ -33,108 +36,161 @@ struct QKArgs {
 template <int DT> struct Frag;
 template <> struct Frag<RTKV_F16> {
   using T = f16x8;
-  __device__ __forceinline__ static f32x16 mfma(T a, T b, f32x16 c) {
-    return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
+  __device__ __forceinline__ static f32x4 mfma(T a, T b, f32x4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
   }
 };
 template <> struct Frag<RTKV_BF16> {
   using T = bf16x8;
-  __device__ __forceinline__ static f32x16 mfma(T a, T b, f32x16 c) {
-    return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+  __device__ __forceinline__ static f32x4 mfma(T a, T b, f32x4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
   }
 };
 
-constexpr int kQKRows = 32;   // query rows per workgroup
-constexpr int kQKWaves = 4;   // head split
+constexpr int kQKRows = 64;   // query rows per workgroup (4 waves × 16)
 
-template <int DT, int NT>
+// NT: column tiles of 16 (P ≤ 16·NT); KS: k-steps of 32 (D = 32·KS).
+template <int DT, int NT, int KS>
 __global__ __launch_bounds__(256) void qk_importance_kernel(QKArgs g) {
   using FT = typename Frag<DT>::T;
   using S_ = typename Dt<DT>::S;
-  const rtkv_qk_desc& q = g.q;
-  __shared__ float red[kQKWaves][kQKRows];
+  constexpr int D = 32 * KS;
+  constexpr int PT = 16 * NT;                 // padded prompt rows in LDS
+  constexpr int PITCH = D * 2 + 16;           // LDS row pitch in bytes (16-byte pad: spreads banks)
+  constexpr int CH = D / 8;                   // 16-byte chunks per key row
+  constexpr int LPT = (PT * CH + 255) / 256;  // key chunks each thread stages per head
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];  // 2 × PT × PITCH
   __shared__ float tokA[kQKRows];
+  const rtkv_qk_desc& q = g.q;
   zero_regions(g.ex);
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int r = lane & 31, hh = lane >> 5;
+  const int c16 = lane & 15, kg = lane >> 4;
   const int b = blockIdx.y;
-  const int64_t i0 = (int64_t)blockIdx.x * kQKRows;
-  const int H = (int)q.H, grp = (int)(q.H / q.Hkv), P = g.P, D = (int)q.D;
-  const int64_t S = q.S;
-  // this lane's A-operand row and its 16 accumulator rows
-  const int64_t arow = i0 + r < S ? i0 + r : S - 1;
-  int64_t crow[16];
-#pragma unroll
-  for (int reg = 0; reg < 16; ++reg) crow[reg] = i0 + (reg & 3) + 8 * (reg >> 2) + 4 * hh;
+  const int S = (int)q.S, H = (int)q.H, grp = (int)(q.H / q.Hkv), P = g.P;
+  const int i0 = blockIdx.x * kQKRows;
+  const int wrow0 = i0 + wave * 16;                 // first row of this wave
+  const int arow = min(wrow0 + c16, S - 1);         // A-operand row of this lane
+  const int crow0 = wrow0 + 4 * kg;                 // accumulator rows crow0 + reg
   const float l2e = 1.4426950408889634f;
   const float sc = q.scale * l2e;
-  float hs[NT][16];
-#pragma unroll
-  for (int t = 0; t < NT; ++t)
-#pragma unroll
-    for (int reg = 0; reg < 16; ++reg) hs[t][reg] = 0.f;
+  // rows/columns needing a mask (wave-uniform): causal rows below P, rows past S, columns past P
+  const bool masked = (q.causal && q.row0 + wrow0 < PT - 1) || wrow0 + 16 > S || P < PT;
 
-  const S_* Qb = static_cast<const S_*>(q.q_dev) + b * q.q_stride_b + arow * q.q_stride_s + 8 * hh;
-  const S_* Kb = static_cast<const S_*>(q.k_dev) + b * q.k_stride_b + 8 * hh;
-  for (int h = wave; h < H; h += kQKWaves) {
-    const S_* qrow = Qb + (int64_t)h * q.q_stride_h;
-    const S_* kbase = Kb + (int64_t)(h / grp) * q.k_stride_h;
-    f32x16 acc[NT];
+  const S_* Qb = static_cast<const S_*>(q.q_dev) + b * q.q_stride_b + (int64_t)arow * q.q_stride_s + 8 * kg;
+  const S_* Kb = static_cast<const S_*>(q.k_dev) + b * q.k_stride_b;
+  const float* Lb = q.lse_dev + b * q.lse_stride_b;
+
+  // staging of one head's prompt keys: thread chunk e → (row e / CH, chunk e % CH)
+  uint4 kreg[LPT];
+  auto load_keys = [&](int h) {
+    const S_* kh = Kb + (int64_t)(h / grp) * q.k_stride_h;
 #pragma unroll
-    for (int t = 0; t < NT; ++t) acc[t] = f32x16{};
-    for (int s = 0; s < D; s += 16) {
-      const FT a = *reinterpret_cast<const FT*>(qrow + s);
-#pragma unroll
-      for (int t = 0; t < NT; ++t) {
-        const int p = t * 32 + r;
-        const FT bf = p < P ? *reinterpret_cast<const FT*>(kbase + (int64_t)p * q.k_stride_s + s) : FT{};
-        acc[t] = Frag<DT>::mfma(a, bf, acc[t]);
-      }
+    for (int k = 0; k < LPT; ++k) {
+      const int e = threadIdx.x + k * 256;
+      const int p = e / CH, c = e % CH;
+      kreg[k] = (e < PT * CH && p < P) ? *reinterpret_cast<const uint4*>(kh + (int64_t)p * q.k_stride_s + c * 8)
+                                       : make_uint4(0, 0, 0, 0);
     }
-    // W = exp(x·scale − lse) = exp2(x·scale·log2e − lse·log2e); masked columns / rows contribute 0
-    const float* lrow = q.lse_dev + b * q.lse_stride_b + (int64_t)h * q.lse_stride_h;
-    float lse2[16];
+  };
+  auto store_keys = [&](int buf) {
+    uint8_t* base = lds + buf * (PT * PITCH);
 #pragma unroll
-    for (int reg = 0; reg < 16; ++reg) lse2[reg] = crow[reg] < S ? lrow[crow[reg]] * l2e : 0.f;
+    for (int k = 0; k < LPT; ++k) {
+      const int e = threadIdx.x + k * 256;
+      if (e < PT * CH) *reinterpret_cast<uint4*>(base + (e / CH) * PITCH + (e % CH) * 16) = kreg[k];
+    }
+  };
+  FT areg[KS];
+  auto load_q = [&](int h) {
+    const S_* qh = Qb + (int64_t)h * q.q_stride_h;
+#pragma unroll
+    for (int s = 0; s < KS; ++s) areg[s] = *reinterpret_cast<const FT*>(qh + 32 * s);
+  };
+
+  f32x4 hs[NT];
+#pragma unroll
+  for (int t = 0; t < NT; ++t) hs[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  load_keys(0);
+  store_keys(0);
+  load_q(0);
+  __syncthreads();
+  for (int h = 0; h < H; ++h) {
+    const int buf = h & 1;
+    FT acur[KS];
+#pragma unroll
+    for (int s = 0; s < KS; ++s) acur[s] = areg[s];
+    const f32x4 lse = *reinterpret_cast<const f32x4*>(Lb + (int64_t)h * q.lse_stride_h + (crow0 + 3 < S ? crow0 : 0));
+    if (h + 1 < H) {  // next head in flight while this one computes
+      load_keys(h + 1);
+      load_q(h + 1);
+    }
+    const uint8_t* kl = lds + buf * (PT * PITCH) + c16 * PITCH + kg * 16;
+    f32x4 acc[NT];
 #pragma unroll
     for (int t = 0; t < NT; ++t) {
-      const int p = t * 32 + r;
+      acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int reg = 0; reg < 16; ++reg) {
-        const bool ok = p < P && crow[reg] < S && (!q.causal || p <= q.row0 + crow[reg]);
-        const float w = __builtin_amdgcn_exp2f(acc[t][reg] * sc - lse2[reg]);
-        hs[t][reg] += ok ? w : 0.f;
+      for (int s = 0; s < KS; ++s) {
+        const FT bf = *reinterpret_cast<const FT*>(kl + t * 16 * PITCH + s * 64);
+        acc[t] = Frag<DT>::mfma(acur[s], bf, acc[t]);
       }
     }
-  }
-  // Σ over the P columns: the tiles in-lane, then the 32 lanes of each half (one column each)
-  float rs[16];
+    // lse of rows crow0..crow0+3 (rows past S read a clamped window and are masked below)
+    float l2[4];
+    if (crow0 + 3 < S) {
 #pragma unroll
-  for (int reg = 0; reg < 16; ++reg) {
+      for (int r = 0; r < 4; ++r) l2[r] = lse[r] * l2e;
+    } else {
+      const float* lr = Lb + (int64_t)h * q.lse_stride_h;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) l2[r] = crow0 + r < S ? lr[crow0 + r] * l2e : 0.f;
+    }
+    if (!masked) {
+#pragma unroll
+      for (int t = 0; t < NT; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) hs[t][r] += __builtin_amdgcn_exp2f(acc[t][r] * sc - l2[r]);
+    } else {
+#pragma unroll
+      for (int t = 0; t < NT; ++t) {
+        const int p = 16 * t + c16;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int i = crow0 + r;
+          const bool ok = p < P && i < S && (!q.causal || (int64_t)p <= q.row0 + i);
+          const float w = __builtin_amdgcn_exp2f(acc[t][r] * sc - l2[r]);
+          hs[t][r] += ok ? w : 0.f;
+        }
+      }
+    }
+    if (h + 1 < H) {  // buf^1 was last read in iteration h-1, before the barrier that ended it
+      store_keys(buf ^ 1);
+      __syncthreads();
+    }
+  }
+  // Σ over the P columns: tiles in-lane, then the 16 lanes of each row group
+  float rs[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
     float v = 0.f;
 #pragma unroll
-    for (int t = 0; t < NT; ++t) v += hs[t][reg];
+    for (int t = 0; t < NT; ++t) v += hs[t][r];
 #pragma unroll
-    for (int o = 1; o < 32; o <<= 1) v += __shfl_xor(v, o, 64);
-    rs[reg] = v;
+    for (int o = 1; o < 16; o <<= 1) v += __shfl_xor(v, o, 64);
+    rs[r] = v / (float)H;
   }
-  if (r == 0) {
+  if (c16 == 0) {
 #pragma unroll
-    for (int reg = 0; reg < 16; ++reg) red[wave][(reg & 3) + 8 * (reg >> 2) + 4 * hh] = rs[reg];
-  }
-  __syncthreads();
-  if (threadIdx.x < kQKRows) {
-    const int64_t i = i0 + threadIdx.x;
-    float v = 0.f;
-#pragma unroll
-    for (int w = 0; w < kQKWaves; ++w) v += red[w][threadIdx.x];
-    v = v / (float)H;
-    tokA[threadIdx.x] = v;
-    if (i < S) {
-      g.A[(int64_t)b * S + i] = v;
-      if (g.ex.t2 && b == 0) {
-        const int64_t n = g.ex.row0 + i + 1;  // global position (sequence shards)
-        g.ex.t2[i] = g.ex.beta * ((g.ex.S_total > 1) ? torch_logf((uint32_t)n) / g.ex.logS : 0.f);
+    for (int r = 0; r < 4; ++r) {
+      const int i = crow0 + r;
+      tokA[wave * 16 + 4 * kg + r] = rs[r];
+      if (i < S) {
+        g.A[(int64_t)b * S + i] = rs[r];
+        if (g.ex.t2 && b == 0) {
+          const int64_t n = g.ex.row0 + i + 1;  // global position (sequence shards)
+          g.ex.t2[i] = g.ex.beta * ((g.ex.S_total > 1) ? torch_logf((uint32_t)n) / g.ex.logS : 0.f);
+        }
       }
     }
   }
@@ -149,30 +205,46 @@ __global__ __launch_bounds__(256) void qk_importance_kernel(QKArgs g) {
   }
 }
 
-template <int DT>
-static int launch_qk_dt(const QKArgs& a, dim3 grid, hipStream_t st) {
-  const int nt = (a.P + 31) / 32;
-  switch (nt) {
-    case 1: hipLaunchKernelGGL((qk_importance_kernel<DT, 1>), grid, dim3(256), 0, st, a); break;
-    case 2: hipLaunchKernelGGL((qk_importance_kernel<DT, 2>), grid, dim3(256), 0, st, a); break;
-    case 3: hipLaunchKernelGGL((qk_importance_kernel<DT, 3>), grid, dim3(256), 0, st, a); break;
-    default: hipLaunchKernelGGL((qk_importance_kernel<DT, 4>), grid, dim3(256), 0, st, a); break;
+template <int DT, int NT, int KS>
+static int launch_qk_tpl(const QKArgs& a, dim3 grid, hipStream_t st) {
+  constexpr size_t lds = 2 * (size_t)(16 * NT) * (64 * KS + 16);
+  static bool attr = false;
+  if (!attr) {
+    RTKV_HIP_CHECK(hipFuncSetAttribute((const void*)qk_importance_kernel<DT, NT, KS>,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    attr = true;
   }
+  hipLaunchKernelGGL((qk_importance_kernel<DT, NT, KS>), grid, dim3(256), lds, st, a);
   RTKV_HIP_CHECK(hipGetLastError());
   return RTKV_OK;
 }
 
+template <int DT>
+static int launch_qk_dt(const QKArgs& a, dim3 grid, hipStream_t st) {
+  const int nt = a.P <= 32 ? 2 : (a.P <= 64 ? 4 : 8);
+  const int ks = (int)(a.q.D / 32);
+#define RTKV_QK(N, K) \
+  if (nt == N && ks == K) return launch_qk_tpl<DT, N, K>(a, grid, st);
+  RTKV_QK(2, 1) RTKV_QK(4, 1) RTKV_QK(8, 1)
+  RTKV_QK(2, 2) RTKV_QK(4, 2) RTKV_QK(8, 2)
+  RTKV_QK(2, 4) RTKV_QK(4, 4) RTKV_QK(8, 4)
+#undef RTKV_QK
+  RTKV_REQUIRE(false, "importance_qk_lse: unsupported head_dim");
+}
+
 int launch_qk_importance(const rtkv_qk_desc& q, int P, float* A, hipStream_t st, const AggExtras& x, int* nparts) {
   RTKV_REQUIRE(q.q_dev && q.k_dev && q.lse_dev && A, "importance_qk_lse: null pointer");
-  RTKV_REQUIRE(q.B >= 1 && q.B <= 65535 && q.H >= 1 && q.S >= 1 && q.Hkv >= 1, "importance_qk_lse: bad shape");
+  RTKV_REQUIRE(q.B >= 1 && q.B <= 65535 && q.H >= 1 && q.S >= 4 && q.Hkv >= 1, "importance_qk_lse: bad shape (S >= 4)");
   RTKV_REQUIRE(q.H % q.Hkv == 0, "importance_qk_lse: H must be a multiple of Hkv");
-  RTKV_REQUIRE(q.D >= 16 && q.D % 16 == 0 && q.D <= 512, "importance_qk_lse: head_dim must be a multiple of 16 (<= 512)");
+  RTKV_REQUIRE(q.D == 32 || q.D == 64 || q.D == 128, "importance_qk_lse: head_dim must be 32, 64 or 128");
   RTKV_REQUIRE(P >= 1 && P <= 128, "importance_qk_lse: prompt_len must be in [1, 128]");
   RTKV_REQUIRE(q.dtype == RTKV_F16 || q.dtype == RTKV_BF16, "importance_qk_lse: Q/K must be float16 or bfloat16");
   RTKV_REQUIRE(q.q_stride_s % 8 == 0 && q.q_stride_h % 8 == 0 && q.q_stride_b % 8 == 0 && q.k_stride_s % 8 == 0 &&
                    q.k_stride_h % 8 == 0 && q.k_stride_b % 8 == 0 && ((uintptr_t)q.q_dev % 16) == 0 &&
                    ((uintptr_t)q.k_dev % 16) == 0,
                "importance_qk_lse: Q/K rows must be 16-byte aligned");
+  RTKV_REQUIRE(((uintptr_t)q.lse_dev % 16) == 0 && q.lse_stride_h % 4 == 0 && q.lse_stride_b % 4 == 0,
+               "importance_qk_lse: lse rows must be 16-byte aligned");
   RTKV_REQUIRE(q.S < ((int64_t)1 << 31) && q.row0 >= 0, "importance_qk_lse: bad row range");
   QKArgs a;
   a.q = q;
