@@ -464,3 +464,4 @@ def test_full_size_properties(S, dtype, ratio):
         sc, zp = orc.quant_params(K[0, i], synth.DTYPES[dtype], bits)
         _, ref = orc.fake_quant(K[0, i], synth.DTYPES[dtype], bits, sc, zp)
         assert np.array_equal(k2h[r], ref)
+

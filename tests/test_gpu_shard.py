@@ -32,6 +32,7 @@ def _dev(a, dtype):
     ("bfloat16", 3000, 3, 8, 64, 0.8),     # P = 128, S_total*P not a multiple of 32 per shard boundary
     ("float32", 1500, 5, 4, 64, 0.3),
     ("float16", 640, 8, 4, 32, 0.05),      # tiny budget: the top-10% fallback across shards
+    ("float16", 32768, 2, 8, 64, 0.5),     # S_total above the single-workgroup K2 limit
 ])
 def test_shards_union_equals_single_gpu(dtype, S_total, world, H, D, ratio):
     import rtkv
