@@ -186,6 +186,125 @@ __global__ __launch_bounds__(256) void aggregation_vec_kernel(const typename Dt<
   }
 }
 
+// Register path for fp16/bf16 with P = 8·CPR (CPR = 16 for P = 128): thread (token, chunk) holds the
+// 8 head means of its 16-byte chunk, and the inner sum over the prompt columns runs across the CPR
+// lanes of the token with wave shuffles in exactly PyTorch's order (no LDS, no barrier):
+//   y_m[l]   = x[16m + l] + x[16m + 8 + l]          (chunks 2m, 2m+1: one 16-wide Vectorized<Half>)
+//   part_k   = Σ_j y_{4j+k} (sequential), tail m >= 4·nq into part 0, then part0+part1+part2+part3
+//   A        = Σ_l lanes[l] (l = 0..7, sequential)                       (vectorized_inner_sum, ILP 4)
+template <int DT, int CPR>
+__global__ __launch_bounds__(256) void aggregation_shfl_kernel(const typename Dt<DT>::S* __restrict__ W, int H,
+                                                               int64_t S, int64_t sb, int64_t sh, int64_t ss,
+                                                               int64_t lim, float* __restrict__ A, AggExtras ex) {
+  using S_ = typename Dt<DT>::S;
+  using V = uint4;
+  constexpr int P = 8 * CPR;
+  constexpr int TT = 256 / CPR;  // tokens per block
+  constexpr int NV = CPR / 2;    // 16-column groups
+  constexpr int NQ = NV / 4;
+  __shared__ float red[2][4];
+  zero_regions(ex);
+  const int b = blockIdx.y;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int tok = threadIdx.x / CPR, ch = threadIdx.x % CPR;
+  const int64_t i = (int64_t)blockIdx.x * TT + tok;
+  const bool valid = i < S;
+  const int64_t ic = valid ? i : S - 1;  // clamped row (its loads are discarded)
+  const S_* base = W + b * sb + ic * ss + ch * 8;
+  float a0[8], a1[8], a2[8], a3[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) a0[k] = a1[k] = a2[k] = a3[k] = 0.f;
+  int h = 0;
+  while (h + 16 <= H) {
+    V v[16];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) v[j] = *reinterpret_cast<const V*>(base + (int64_t)(h + j) * sh);
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      float x[8];
+      unpack_vec<DT, 8>(v[j], x);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) a0[k] += x[k];
+    }
+    h += 16;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) { a1[k] += a0[k]; a0[k] = 0.f; }
+    if ((h & (15 << 4)) == 0) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) { a2[k] += a1[k]; a1[k] = 0.f; }
+      if ((h & (15 << 8)) == 0) {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) { a3[k] += a2[k]; a2[k] = 0.f; }
+      }
+    }
+  }
+  for (; h < H; ++h) {
+    float x[8];
+    unpack_vec<DT, 8>(*reinterpret_cast<const V*>(base + (int64_t)h * sh), x);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) a0[k] += x[k];
+  }
+  const float fH = (float)H;
+  float m[8];  // head means of columns ch*8 .. ch*8+7, rounded to the dtype
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    float s = a0[k];
+    s += a1[k];
+    s += a2[k];
+    s += a3[k];
+    const int64_t col = ic * P + ch * 8 + k;
+    if (col >= lim) {  // columns past the 32-aligned block: row_sum (ilp 4) order
+      const S_* colp = W + b * sb + ic * ss + ch * 8 + k;
+      s = row_sum_ilp4([&](int hh) { return Dt<DT>::load(colp[(int64_t)hh * sh]); }, H);
+    }
+    m[k] = Dt<DT>::rnd(s / fH);
+  }
+  // y_m on even chunks (m = ch / 2): this chunk + the next one
+  float y[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) y[k] = m[k] + __shfl_xor(m[k], 1, 64);
+  // part_k (k = 0..3) on chunk 2k: Σ_{j < NQ} y_{4j+k} in order, then the tail groups into part 0
+  const int tl = lane - ch;  // lane of this token's chunk 0
+  float part[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    float acc = 0.f;
+#pragma unroll
+    for (int j = 0; j < NQ; ++j) acc += __shfl(y[k], tl + 2 * (4 * j + (ch >> 1 & 3)), 64);
+    part[k] = acc;
+  }
+  // chunk 0 folds: part0 (+ tail groups) + part1 + part2 + part3, then the 8 vector lanes
+  float fin = 0.f;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    float p0 = part[k];
+#pragma unroll
+    for (int mm = 4 * NQ; mm < NV; ++mm) p0 += __shfl(y[k], tl + 2 * mm, 64);
+    const float p1 = __shfl(part[k], tl + 2, 64), p2 = __shfl(part[k], tl + 4, 64), p3 = __shfl(part[k], tl + 6, 64);
+    p0 += p1;
+    p0 += p2;
+    p0 += p3;
+    fin += p0;
+  }
+  const float Ai = Dt<DT>::rnd(fin);
+  float mn = INFINITY, mx = -INFINITY;
+  if (ch == 0 && valid) {
+    A[(int64_t)b * S + i] = Ai;
+    if (ex.t2 && b == 0) ex.t2[i] = ex.beta * ((S > 1) ? torch_logf((uint32_t)(i + 1)) / ex.logS : 0.f);
+    mn = mx = Ai;
+  }
+  if (ex.part) {  // block (min, max) of A for the score normalisation (token_importance.py:71-83)
+    mn = wave_min(mn);
+    mx = wave_max(mx);
+    if (lane == 0) { red[0][wave] = mn; red[1][wave] = mx; }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      ex.part[((int64_t)b * gridDim.x + blockIdx.x) * 2] = fminf(fminf(red[0][0], red[0][1]), fminf(red[0][2], red[0][3]));
+      ex.part[((int64_t)b * gridDim.x + blockIdx.x) * 2 + 1] = fmaxf(fmaxf(red[1][0], red[1][1]), fmaxf(red[1][2], red[1][3]));
+    }
+  }
+}
+
 // Generic path: any P / strides / alignment (scalar loads; the cfg1 P = 102 case lands here).
 template <int DT>
 __global__ __launch_bounds__(256) void aggregation_scalar_kernel(const typename Dt<DT>::S* __restrict__ W,
@@ -272,6 +391,16 @@ static int launch_agg_dt(const rtkv_attn_desc& w, int P, float* A, hipStream_t s
   const bool aligned = ((uintptr_t)W % 16 == 0) && (P % VEC == 0) && (w.stride_s % VEC == 0) &&
                        (w.stride_h % VEC == 0) && (w.stride_b % VEC == 0);
   const int H = (int)w.H;
+  if constexpr (DT != RTKV_F32) {
+    if (aligned && P == 128) {  // register path (Llama prompts: P = 128)
+      dim3 grid((unsigned)((w.S + 15) / 16), (unsigned)w.B);
+      if (x.nparts) *x.nparts = (int)grid.x;
+      hipLaunchKernelGGL((aggregation_shfl_kernel<DT, 16>), grid, dim3(256), 0, st, W, H, w.S, w.stride_b,
+                         w.stride_h, w.stride_s, lim, A, x);
+      RTKV_HIP_CHECK(hipGetLastError());
+      return RTKV_OK;
+    }
+  }
   if (aligned) {
     const int cpr = P / VEC;
     int TT = 256 / cpr;
