@@ -48,104 +48,122 @@ template <> struct Frag<RTKV_BF16> {
 };
 
 constexpr int kQKRows = 64;   // query rows per workgroup (4 waves × 16)
+constexpr int kQKStages = 3;  // LDS ring depth (heads in flight)
+
+// LDS-DMA of one 16-byte chunk per lane: the wave writes 1 KiB lane-linear at lds_base (M0).
+__device__ __forceinline__ void glds16(const void* g, void* lds_base) {
+  __builtin_amdgcn_global_load_lds(g, (__attribute__((address_space(3))) void*)lds_base, 16, 0, 0);
+}
+__device__ __forceinline__ void glds4(const void* g, void* lds_base) {
+  __builtin_amdgcn_global_load_lds(g, (__attribute__((address_space(3))) void*)lds_base, 4, 0, 0);
+}
 
 // NT: column tiles of 16 (P ≤ 16·NT); KS: k-steps of 32 (D = 32·KS).
+//
+// Per head h the workgroup stages, by LDS-DMA into ring slot h % 3: the P×D prompt keys (kv head
+// h/g), its 64 query rows and their 64 LSE values.  Rows are 2·D bytes, chunk c of row r sits at
+// physical chunk c ^ (r & (CH-1)) (the swizzle is applied on the global source address: the DMA
+// writes lane-linear), which makes the fragment reads conflict-free.  Two heads stay in flight while
+// one is computed (counted vmcnt, raw s_barrier: a __syncthreads would drain the DMA queue).
 template <int DT, int NT, int KS>
 __global__ __launch_bounds__(256) void qk_importance_kernel(QKArgs g) {
   using FT = typename Frag<DT>::T;
   using S_ = typename Dt<DT>::S;
   constexpr int D = 32 * KS;
-  constexpr int PT = 16 * NT;                 // padded prompt rows in LDS
-  constexpr int PITCH = D * 2 + 16;           // LDS row pitch in bytes (16-byte pad: spreads banks)
-  constexpr int CH = D / 8;                   // 16-byte chunks per key row
-  constexpr int LPT = (PT * CH + 255) / 256;  // key chunks each thread stages per head
-  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];  // 2 × PT × PITCH
+  constexpr int PT = 16 * NT;                      // padded prompt rows
+  constexpr int RB = 2 * D;                        // bytes per row
+  constexpr int CH = RB / 16;                      // 16-byte chunks per row
+  constexpr int RPI = 1024 / RB;                   // rows per DMA wave-instruction
+  constexpr int KEY_BYTES = PT * RB, Q_BYTES = kQKRows * RB;
+  constexpr int STAGE = KEY_BYTES + Q_BYTES + kQKRows * 4;
+  constexpr int KI = KEY_BYTES / 1024 / 4;         // key DMA instructions per wave per head
+  constexpr int QI = Q_BYTES / 1024 / 4;           // query DMA instructions per wave per head
+  constexpr int OPS = KI + QI + 1;                 // DMA ops per wave per head (+1: LSE)
+  static_assert(KI >= 1 && QI >= 1, "tile too small for 4 waves");
+  extern __shared__ __attribute__((aligned(1024))) uint8_t lds[];  // kQKStages × STAGE
   __shared__ float tokA[kQKRows];
   const rtkv_qk_desc& q = g.q;
   zero_regions(g.ex);
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int c16 = lane & 15, kg = lane >> 4;
   const int b = blockIdx.y;
   const int S = (int)q.S, H = (int)q.H, grp = (int)(q.H / q.Hkv), P = g.P;
   const int i0 = blockIdx.x * kQKRows;
   const int wrow0 = i0 + wave * 16;                 // first row of this wave
-  const int arow = min(wrow0 + c16, S - 1);         // A-operand row of this lane
   const int crow0 = wrow0 + 4 * kg;                 // accumulator rows crow0 + reg
   const float l2e = 1.4426950408889634f;
   const float sc = q.scale * l2e;
-  // rows/columns needing a mask (wave-uniform): causal rows below P, rows past S, columns past P
   const bool masked = (q.causal && q.row0 + wrow0 < PT - 1) || wrow0 + 16 > S || P < PT;
 
-  const S_* Qb = static_cast<const S_*>(q.q_dev) + b * q.q_stride_b + (int64_t)arow * q.q_stride_s + 8 * kg;
+  const S_* Qb = static_cast<const S_*>(q.q_dev) + b * q.q_stride_b;
   const S_* Kb = static_cast<const S_*>(q.k_dev) + b * q.k_stride_b;
   const float* Lb = q.lse_dev + b * q.lse_stride_b;
+  // this lane's DMA source row/chunk within an instruction (lane-linear destination)
+  const int lrow = lane / CH, lpc = lane % CH;
 
-  // staging of one head's prompt keys: thread chunk e → (row e / CH, chunk e % CH)
-  uint4 kreg[LPT];
-  auto load_keys = [&](int h) {
+  auto issue = [&](int h) {
+    uint8_t* st = lds + (h % kQKStages) * STAGE;
     const S_* kh = Kb + (int64_t)(h / grp) * q.k_stride_h;
 #pragma unroll
-    for (int k = 0; k < LPT; ++k) {
-      const int e = threadIdx.x + k * 256;
-      const int p = e / CH, c = e % CH;
-      kreg[k] = (e < PT * CH && p < P) ? *reinterpret_cast<const uint4*>(kh + (int64_t)p * q.k_stride_s + c * 8)
-                                       : make_uint4(0, 0, 0, 0);
+    for (int k = 0; k < KI; ++k) {
+      const int r = (wave * KI + k) * RPI + lrow;          // key row (prompt position)
+      const int c = lpc ^ (r & (CH - 1));                  // logical chunk stored at slot lpc
+      const int pr = r < P ? r : P - 1;                    // rows past P: any valid row (masked)
+      glds16(kh + (int64_t)pr * q.k_stride_s + c * 8, st + (wave * KI + k) * 1024);
     }
-  };
-  auto store_keys = [&](int buf) {
-    uint8_t* base = lds + buf * (PT * PITCH);
-#pragma unroll
-    for (int k = 0; k < LPT; ++k) {
-      const int e = threadIdx.x + k * 256;
-      if (e < PT * CH) *reinterpret_cast<uint4*>(base + (e / CH) * PITCH + (e % CH) * 16) = kreg[k];
-    }
-  };
-  FT areg[KS];
-  auto load_q = [&](int h) {
     const S_* qh = Qb + (int64_t)h * q.q_stride_h;
 #pragma unroll
-    for (int s = 0; s < KS; ++s) areg[s] = *reinterpret_cast<const FT*>(qh + 32 * s);
+    for (int k = 0; k < QI; ++k) {
+      const int r = (wave * QI + k) * RPI + lrow;          // query row within the block
+      const int c = lpc ^ (r & (CH - 1));
+      const int gr = i0 + r < S ? i0 + r : S - 1;
+      glds16(qh + (int64_t)gr * q.q_stride_s + c * 8, st + KEY_BYTES + (wave * QI + k) * 1024);
+    }
+    {  // this wave's 16 LSE values (lanes 16..63 idle)
+      const int gr = wrow0 + c16 < S ? wrow0 + c16 : S - 1;
+      if (lane < 16) glds4(Lb + (int64_t)h * q.lse_stride_h + gr, st + KEY_BYTES + Q_BYTES + wave * 64);
+    }
   };
 
   f32x4 hs[NT];
 #pragma unroll
   for (int t = 0; t < NT; ++t) hs[t] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  load_keys(0);
-  store_keys(0);
-  load_q(0);
-  __syncthreads();
+  issue(0);
+  if (H > 1) issue(1);
   for (int h = 0; h < H; ++h) {
-    const int buf = h & 1;
-    FT acur[KS];
-#pragma unroll
-    for (int s = 0; s < KS; ++s) acur[s] = areg[s];
-    const f32x4 lse = *reinterpret_cast<const f32x4*>(Lb + (int64_t)h * q.lse_stride_h + (crow0 + 3 < S ? crow0 : 0));
-    if (h + 1 < H) {  // next head in flight while this one computes
-      load_keys(h + 1);
-      load_q(h + 1);
+    __builtin_amdgcn_s_barrier();      // every wave is done with head h-1: its slot is free
+    if (h + 2 < H) {
+      issue(h + 2);
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * OPS) : "memory");  // head h landed (this wave)
+    } else if (h + 1 < H) {
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(OPS) : "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
-    const uint8_t* kl = lds + buf * (PT * PITCH) + c16 * PITCH + kg * 16;
+    __builtin_amdgcn_s_barrier();      // ... and every other wave's pieces of head h too
+    const uint8_t* st = lds + (h % kQKStages) * STAGE;
+    const uint8_t* qrow = st + KEY_BYTES + (wave * 16 + c16) * RB;
+    const int qsw = (wave * 16 + c16) & (CH - 1);
+    FT a[KS];
+#pragma unroll
+    for (int s_ = 0; s_ < KS; ++s_) a[s_] = *reinterpret_cast<const FT*>(qrow + (((4 * s_ + kg) ^ qsw) * 16));
     f32x4 acc[NT];
 #pragma unroll
     for (int t = 0; t < NT; ++t) {
       acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+      const int kr = 16 * t + c16;
+      const uint8_t* krow = st + kr * RB;
 #pragma unroll
-      for (int s = 0; s < KS; ++s) {
-        const FT bf = *reinterpret_cast<const FT*>(kl + t * 16 * PITCH + s * 64);
-        acc[t] = Frag<DT>::mfma(acur[s], bf, acc[t]);
+      for (int s_ = 0; s_ < KS; ++s_) {
+        const FT bf = *reinterpret_cast<const FT*>(krow + (((4 * s_ + kg) ^ (kr & (CH - 1))) * 16));
+        acc[t] = Frag<DT>::mfma(a[s_], bf, acc[t]);
       }
     }
-    // lse of rows crow0..crow0+3 (rows past S read a clamped window and are masked below)
+    const f32x4 lse = *reinterpret_cast<const f32x4*>(st + KEY_BYTES + Q_BYTES + wave * 64 + kg * 16);
     float l2[4];
-    if (crow0 + 3 < S) {
 #pragma unroll
-      for (int r = 0; r < 4; ++r) l2[r] = lse[r] * l2e;
-    } else {
-      const float* lr = Lb + (int64_t)h * q.lse_stride_h;
-#pragma unroll
-      for (int r = 0; r < 4; ++r) l2[r] = crow0 + r < S ? lr[crow0 + r] * l2e : 0.f;
-    }
+    for (int r = 0; r < 4; ++r) l2[r] = lse[r] * l2e;
     if (!masked) {
 #pragma unroll
       for (int t = 0; t < NT; ++t)
@@ -163,10 +181,6 @@ __global__ __launch_bounds__(256) void qk_importance_kernel(QKArgs g) {
           hs[t][r] += ok ? w : 0.f;
         }
       }
-    }
-    if (h + 1 < H) {  // buf^1 was last read in iteration h-1, before the barrier that ended it
-      store_keys(buf ^ 1);
-      __syncthreads();
     }
   }
   // Σ over the P columns: tiles in-lane, then the 16 lanes of each row group
@@ -207,7 +221,7 @@ __global__ __launch_bounds__(256) void qk_importance_kernel(QKArgs g) {
 
 template <int DT, int NT, int KS>
 static int launch_qk_tpl(const QKArgs& a, dim3 grid, hipStream_t st) {
-  constexpr size_t lds = 2 * (size_t)(16 * NT) * (64 * KS + 16);
+  constexpr size_t lds = (size_t)kQKStages * ((size_t)(16 * NT) * (64 * KS) + (size_t)kQKRows * (64 * KS) + kQKRows * 4);
   static bool attr = false;
   if (!attr) {
     RTKV_HIP_CHECK(hipFuncSetAttribute((const void*)qk_importance_kernel<DT, NT, KS>,
@@ -221,11 +235,12 @@ static int launch_qk_tpl(const QKArgs& a, dim3 grid, hipStream_t st) {
 
 template <int DT>
 static int launch_qk_dt(const QKArgs& a, dim3 grid, hipStream_t st) {
-  const int nt = a.P <= 32 ? 2 : (a.P <= 64 ? 4 : 8);
   const int ks = (int)(a.q.D / 32);
+  int nt = a.P <= 32 ? 2 : (a.P <= 64 ? 4 : 8);
+  if (nt * ks < 4) nt = 4 / ks;  // at least one 4 KiB key DMA round per head
 #define RTKV_QK(N, K) \
   if (nt == N && ks == K) return launch_qk_tpl<DT, N, K>(a, grid, st);
-  RTKV_QK(2, 1) RTKV_QK(4, 1) RTKV_QK(8, 1)
+  RTKV_QK(4, 1) RTKV_QK(8, 1)
   RTKV_QK(2, 2) RTKV_QK(4, 2) RTKV_QK(8, 2)
   RTKV_QK(2, 4) RTKV_QK(4, 4) RTKV_QK(8, 4)
 #undef RTKV_QK
