@@ -273,6 +273,8 @@ LAYER_CASES = [
     ("cfg3_l0", COVERAGE, 32, 0, 1, 32, 32, 128, 16384, "float16"),
     ("cfg3_l20", PUBLISHED, 32, 20, 1, 32, 32, 128, 16384, "float16"),
     ("cfg2_quant", COVERAGE, 32, 0, 1, 32, 32, 128, 4096, "float16"),
+    ("cfg5_13b_l39", COVERAGE, 40, 39, 1, 40, 40, 128, 8192, "bfloat16"),    # Llama-2-13B rows (F = 5120)
+    ("cfg5_13b_l20", PUBLISHED, 40, 20, 1, 40, 40, 128, 4096, "float16"),
 ]
 
 
