@@ -369,8 +369,8 @@ def main():
         }
         if sharded:
             line["exchange"] = {"received_bytes_per_rank_per_step": job.exchanged_bytes(),
-                                "kind": "one grouped RCCL send/recv batch of packed K/V codes + scale/zp "
-                                        "(exact byte ranges, all peers at once)",
+                                "kind": "grouped RCCL send/recv (one group per layer, enqueued back to back) of packed "
+                                        "K/V codes + scale/zp (exact byte ranges, all peers at once)",
                                 "per_layer_collective": "RCCL all-gather of A (4 B/token)"}
         if not sharded:
             per_launch_ms = k_ms[2] / (reps * args.layers)

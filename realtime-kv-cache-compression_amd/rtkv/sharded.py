@@ -15,9 +15,10 @@ tokens (rank j owns tokens [j*S_local, (j+1)*S_local)), and each layer runs as
 
 The selection is global (the reference's min-max normalisation and budget are over the whole
 sequence, token_importance.py:71-83, selective_propagation.py:96), so step 2 is the only exchange
-inside a layer.  After the last layer, ``exchange()`` does the one collective of the compressed KV:
-a single host read of every layer's rank bounds, then ONE grouped point-to-point batch in which each
-rank sends its byte ranges of the packed K/V codes and its scale/zero-point rows to every peer
+inside a layer.  After the last layer, ``exchange()`` does the one exchange of the compressed KV:
+a single host read of every layer's rank bounds, then one grouped point-to-point launch per layer
+(all enqueued back to back, waited once) in which each rank sends its byte ranges of the packed K/V
+codes and its scale/zero-point rows to every peer
 (xGMI links are point-to-point, so every rank streams to all 7 peers at once instead of hopping
 round a ring).  Every rank then holds every layer's packed KV byte-identical to the single-GPU
 ``rtkv_compress_layer`` output.
@@ -196,7 +197,7 @@ class ShardedPrefillCompressor:
         return bufs
 
     def exchange(self) -> List[ShardLayer]:
-        """One host read of every pending layer's rank bounds, then one grouped P2P batch: each rank's
+        """One host read of every pending layer's rank bounds, then one grouped P2P launch per layer: each rank's
         packed K/V byte ranges and scale/zero-point rows go to every peer."""
         layers = list(self._pending)
         self._pending = []
@@ -206,9 +207,10 @@ class ShardedPrefillCompressor:
         out = [ShardLayer(l, self._bufs[l], host[k]) for k, l in enumerate(layers)]
         if self.world == 1 or not self.emit_packed:
             return out
-        ops = []
+        works = []
         me = self.rank
         for sl in out:
+            ops = []
             g = sl.bufs.g
             cap = sl.bufs.S_total
             sz = g.scale_zp.view(-1)
@@ -231,9 +233,10 @@ class ShardedPrefillCompressor:
                                           (spans[j][1], sz)):
                         if hi > lo:
                             ops.append(dist.P2POp(dist.irecv, buf[lo:hi], peer, self.group))
-        if ops:
-            for w in dist.batch_isend_irecv(ops):
-                w.wait()
+            if ops:  # one grouped launch per layer: every peer pair of the layer at once
+                works.extend(dist.batch_isend_irecv(ops))
+        for w in works:
+            w.wait()
         return out
 
     # ------------------------------------------------------------------ reference-named entry point
