@@ -67,6 +67,15 @@ __host__ __device__ inline int field_width(int dt, int bits) {
   return bits > prec ? bits + 1 : bits;
 }
 
+// ------------------------------------------------------------------------------------ streaming
+// Non-temporal 16-byte load: data read exactly once (K/V rows, attention columns) does not displace
+// cache lines other kernels of the layer re-read.
+typedef unsigned int rtkv_u32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ uint4 load16_nt(const void* p) {
+  const rtkv_u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const rtkv_u32x4*>(p));
+  return make_uint4(v.x, v.y, v.z, v.w);
+}
+
 // ------------------------------------------------------------------------------------ keys
 // Order-preserving uint32 key of an fp32 score (larger key = larger score; -0 folded onto +0 so
 // that equal scores compare equal, as in the reference's `>` comparator).

@@ -218,7 +218,7 @@ __global__ __launch_bounds__(256) void aggregation_shfl_kernel(const typename Dt
   while (h + 16 <= H) {
     V v[16];
 #pragma unroll
-    for (int j = 0; j < 16; ++j) v[j] = *reinterpret_cast<const V*>(base + (int64_t)(h + j) * sh);
+    for (int j = 0; j < 16; ++j) v[j] = load16_nt(base + (int64_t)(h + j) * sh);
 #pragma unroll
     for (int j = 0; j < 16; ++j) {
       float x[8];

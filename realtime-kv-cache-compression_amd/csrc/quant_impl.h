@@ -53,6 +53,34 @@ template <int DT> __device__ __forceinline__ Chunk<DT> f32_to_chunk(const float 
   return c;
 }
 
+// Streaming (non-temporal) store of a chunk: the outputs are not re-read by this layer, so they
+// bypass cache allocation instead of evicting the next kernel's inputs.
+typedef unsigned int nt_u32x2 __attribute__((ext_vector_type(2)));
+typedef unsigned int nt_u32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void nt_store16(void* dst, uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
+  __builtin_nontemporal_store(nt_u32x4{a, b, c, d}, reinterpret_cast<nt_u32x4*>(dst));
+}
+template <int DT> __device__ __forceinline__ void store_chunk_nt(Chunk<DT>* dst, const Chunk<DT>& c) {
+  if constexpr (DT == RTKV_F32) {
+    nt_store16(&dst->a, __float_as_uint(c.a.x), __float_as_uint(c.a.y), __float_as_uint(c.a.z), __float_as_uint(c.a.w));
+    nt_store16(&dst->b, __float_as_uint(c.b.x), __float_as_uint(c.b.y), __float_as_uint(c.b.z), __float_as_uint(c.b.w));
+  } else {
+    nt_store16(&dst->a, c.a.x, c.a.y, c.a.z, c.a.w);
+  }
+}
+
+template <int DT> __device__ __forceinline__ Chunk<DT> load_chunk_nt(const typename Dt<DT>::S* p) {
+  Chunk<DT> c;
+  if constexpr (DT == RTKV_F32) {
+    const uint4 a = load16_nt(p), b = load16_nt(p + 4);
+    c.a = make_float4(__uint_as_float(a.x), __uint_as_float(a.y), __uint_as_float(a.z), __uint_as_float(a.w));
+    c.b = make_float4(__uint_as_float(b.x), __uint_as_float(b.y), __uint_as_float(b.z), __uint_as_float(b.w));
+  } else {
+    c.a = load16_nt(p);
+  }
+  return c;
+}
+
 // Little-endian accumulation of 8 codes of w bits (w <= 17) into 3 × 64-bit words.
 __device__ __forceinline__ void pack8(const uint32_t (&q)[8], int w, uint64_t& p0, uint64_t& p1, uint64_t& p2) {
   p0 = p1 = p2 = 0;
@@ -155,13 +183,13 @@ template <int W> __device__ __forceinline__ void pack_store(uint8_t* dst, const 
     uint32_t v = 0;
 #pragma unroll
     for (int e = 0; e < 8; ++e) v |= q[e] << (2 * e);
-    if (aligned) *reinterpret_cast<uint16_t*>(dst) = (uint16_t)v;
+    if (aligned) __builtin_nontemporal_store((uint16_t)v, reinterpret_cast<uint16_t*>(dst));
     else { dst[0] = (uint8_t)v; dst[1] = (uint8_t)(v >> 8); }
   } else if constexpr (W == 4) {
     uint32_t v = 0;
 #pragma unroll
     for (int e = 0; e < 8; ++e) v |= q[e] << (4 * e);
-    if (aligned) *reinterpret_cast<uint32_t*>(dst) = v;
+    if (aligned) __builtin_nontemporal_store(v, reinterpret_cast<uint32_t*>(dst));
     else {
 #pragma unroll
       for (int k = 0; k < 4; ++k) dst[k] = (uint8_t)(v >> (8 * k));
@@ -169,14 +197,14 @@ template <int W> __device__ __forceinline__ void pack_store(uint8_t* dst, const 
   } else if constexpr (W == 8) {
     const uint32_t lo = q[0] | (q[1] << 8) | (q[2] << 16) | (q[3] << 24);
     const uint32_t hi = q[4] | (q[5] << 8) | (q[6] << 16) | (q[7] << 24);
-    if (aligned) *reinterpret_cast<uint2*>(dst) = make_uint2(lo, hi);
+    if (aligned) __builtin_nontemporal_store(nt_u32x2{lo, hi}, reinterpret_cast<nt_u32x2*>(dst));
     else {
 #pragma unroll
       for (int k = 0; k < 8; ++k) dst[k] = (uint8_t)((k < 4 ? lo : hi) >> (8 * (k & 3)));
     }
   } else {  // W == 16
     const uint4 v = make_uint4(q[0] | (q[1] << 16), q[2] | (q[3] << 16), q[4] | (q[5] << 16), q[6] | (q[7] << 16));
-    if (aligned) *reinterpret_cast<uint4*>(dst) = v;
+    if (aligned) nt_store16(dst, v.x, v.y, v.z, v.w);
     else {
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
@@ -262,7 +290,7 @@ __global__ __launch_bounds__(256, 2) void quant_rows_kernel(QuantArgs a) {
     Chunk<DT> raw[NCH];
 #pragma unroll
     for (int k = 0; k < NCH; ++k)
-      if (valid(k)) raw[k] = *reinterpret_cast<const Chunk<DT>*>(src + in_off[k]);
+      if (valid(k)) raw[k] = load_chunk_nt<DT>(src + in_off[k]);
     float mn = INFINITY, mx = -INFINITY, anz = INFINITY;
 #pragma unroll
     for (int k = 0; k < NCH; ++k) {
@@ -308,7 +336,7 @@ __global__ __launch_bounds__(256, 2) void quant_rows_kernel(QuantArgs a) {
           qi[e] = (uint32_t)q;
         }
         if (emit_pk) pack_store<W>(pk + c * W, qi, aligned);
-        if (emit_deq) *reinterpret_cast<Chunk<DT>*>(orow + out_off[k]) = f32_to_chunk<DT>(d);
+        if (emit_deq) store_chunk_nt<DT>(reinterpret_cast<Chunk<DT>*>(orow + out_off[k]), f32_to_chunk<DT>(d));
       }
     };
     auto by_width = [&](auto ftag) {
