@@ -208,6 +208,7 @@ struct FinalizeArgs {
   float ctx;               // (float)min(1, P/S)
   rtkv_layer_stats* stats;
   int mode_scores, mode_labels, mode_select;
+  int fb_group;            // 1: select the top-10% fallback group alongside (set by launch_select)
 };
 // K2 pipeline (select.hip).  sel_ws: select_workspace_bytes(B, S) bytes; `zeroed` = its first
 // select_zero_bytes(B) bytes and the stats are already zero (K1 clears them in rtkv_compress_layer).

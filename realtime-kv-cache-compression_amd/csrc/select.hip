@@ -289,7 +289,7 @@ __global__ __launch_bounds__(kNT) void sel_scores_kernel(SelArgs g) {
     if (a.mode_select) {
       const uint32_t key = score_key(s);
       hist_add(h1, lcoarse, l, key >> 16, valid);
-      hist_add(h1, lcoarse, 3, key >> 16, valid);
+      if (a.fb_group) hist_add(h1, lcoarse, 3, key >> 16, valid);
     }
   }
   if (a.mode_select) coarse_flush(h1, lcoarse);
@@ -361,7 +361,7 @@ __global__ __launch_bounds__(kNT) void sel_scores_kernel(SelArgs g) {
     int64_t kf = (int64_t)((double)S * 0.1);  // topk(max(1, int(S * 0.1)))
     if (kf < 1) kf = 1;
     q_need[3] = kf;
-    q_mode[3] = kf >= S ? SEL_ALL : SEL_PARTIAL;
+    q_mode[3] = !a.fb_group ? SEL_NONE : (kf >= S ? SEL_ALL : SEL_PARTIAL);
     st->quota[3] = kf;
   }
   __syncthreads();
@@ -408,7 +408,7 @@ __global__ __launch_bounds__(kNT) void sel_refine_kernel(SelArgs g) {
     const bool pc = valid && ((mode_l >> (2 * l)) & 3) == SEL_PARTIAL && (key >> 16) == pre[l];
     const bool pa = valid && ((mode_l >> 6) & 3) == SEL_PARTIAL && (key >> 16) == pre[3];
     hist_add(h2, lcoarse, l, key & 0xffffu, pc);
-    hist_add(h2, lcoarse, 3, key & 0xffffu, pa);
+    if (a.fb_group) hist_add(h2, lcoarse, 3, key & 0xffffu, pa);
   }
   coarse_flush(h2, lcoarse);
   if (!arrive_last(&st->done_b, gridDim.x, &s_flag)) return;
@@ -1003,6 +1003,16 @@ int launch_select(const FinalizeArgs& f, void* sel_ws, bool zeroed, hipStream_t 
   RTKV_REQUIRE(!f.mode_select || f.mask, "select: selection needs a mask buffer");
   SelArgs g;
   g.f = f;
+  // The emergency fallback (selective_propagation.py:205-211) runs only when no token fits the
+  // budget.  If U = floor(8·S·ratio) covers the widest class, every non-empty class keeps at least
+  // one token, so the fallback group need not be histogrammed at all (the common case).
+  {
+    const double u8 = 8.0 * ((double)f.S * f.p.propagation_ratio);
+    int wmax = 0;
+    for (int k = 0; k < 3; ++k) wmax = f.p.bits[k] > wmax ? f.p.bits[k] : wmax;
+    const bool possible = f.mode_select == 1 && !(f.p.flags & RTKV_NO_FALLBACK) && !(u8 >= (double)wmax);
+    g.f.fb_group = (possible || !f.mode_labels) ? 1 : 0;  // caller classes: keep the general bookkeeping
+  }
   g.L = carve_select(sel_ws, f.B, f.S);
   if (!zeroed) {
     RTKV_HIP_CHECK(hipMemsetAsync(sel_ws, 0, select_zero_bytes(f.B), st));
