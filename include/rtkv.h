@@ -58,7 +58,9 @@ enum rtkv_layer_flag {
   RTKV_EMIT_DEQUANT = 1,   /* write the dequantized K'/V' (the reference's return value) */
   RTKV_EMIT_PACKED = 2,    /* write bit-packed integer codes + per-row scale/zero-point */
   RTKV_NO_SELECTION = 4,   /* keep every token (quantization only, BASELINE config 2) */
-  RTKV_NO_FALLBACK = 8     /* skip the top-10% emergency fallback (select_tokens_with_budget alone) */
+  RTKV_NO_FALLBACK = 8,    /* skip the top-10% emergency fallback (select_tokens_with_budget alone) */
+  RTKV_SELECT_PIPELINE = 16 /* use the multi-workgroup selection pipeline even where the one-workgroup
+                              selection applies (B = 1, S <= 32768); same results, for cross-checks */
 };
 
 /* ------------------------------------------------------------------------------------------------

@@ -228,8 +228,9 @@ static int compress_layer_impl(const rtkv_kv_desc* kv, const rtkv_attn_desc* w, 
   x.logS = a.logS;
   x.part = ws.Apart;
   x.nparts = &nparts;
-  x.zero0 = ws.sel;
-  x.zero0_bytes = select_zero_bytes(kv->B);
+  x.zero0 = ws.sel;  // the selection scratch that must start zeroed (fast path: counter + histograms)
+  x.zero0_bytes = (select_fast_shape(kv->B, kv->S) && !(p->flags & RTKV_SELECT_PIPELINE)) ? select_fast_zero_bytes()
+                                                                                         : select_zero_bytes(kv->B);
   x.zero1 = out->stats_dev;
   x.zero1_bytes = rtkv_stats_bytes(kv->B);
   if (w) {

@@ -76,6 +76,15 @@ __device__ __forceinline__ uint4 load16_nt(const void* p) {
   return make_uint4(v.x, v.y, v.z, v.w);
 }
 
+// Cross-workgroup hand-off accesses (MI355X_MICROARCH.md "Valid forms"): relaxed agent-scope
+// atomic loads/stores lower to global_load/store ... sc1 (bypass L1, write through L2).
+template <typename T> __device__ __forceinline__ void st_sc1(T* p, T v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+template <typename T> __device__ __forceinline__ T ld_sc1(const T* p) {
+  return __hip_atomic_load(const_cast<T*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 // ------------------------------------------------------------------------------------ keys
 // Order-preserving uint32 key of an fp32 score (larger key = larger score; -0 folded onto +0 so
 // that equal scores compare equal, as in the reference's `>` comparator).
@@ -215,6 +224,13 @@ struct FinalizeArgs {
 size_t select_workspace_bytes(int64_t B, int64_t S);
 size_t select_zero_bytes(int64_t B);
 int launch_select(const FinalizeArgs& a, void* sel_ws, bool zeroed, hipStream_t st);
+// Two-launch K2 (select_fast.hip) for B = 1, S <= 32768; launch_select takes it whenever it is
+// eligible.  It needs select_fast_zero_bytes() of zeroed workspace (K1 clears them).
+bool select_fast_shape(int64_t B, int64_t S);
+bool select_fast_eligible(const FinalizeArgs& a);
+size_t select_fast_zero_bytes();
+size_t select_fast_workspace_bytes(int64_t S);
+int launch_select_fast(const FinalizeArgs& a, void* sel_ws, bool zeroed, hipStream_t st);
 
 struct QuantArgs {
   rtkv_kv_desc kv;

@@ -489,7 +489,9 @@ __global__ __launch_bounds__(1024) void minmax_normalize_kernel(const typename D
   const float eps = Dt<DT>::rnd(1e-8f);
   for (int64_t i = threadIdx.x; i < S; i += blockDim.x) {
     const float v = Dt<DT>::load(xb[i]);
-    const float n = (den > eps) ? Dt<DT>::rnd(Dt<DT>::rnd(v - mn) / den) : 0.f;
+    float qn = Dt<DT>::rnd(v - mn) / den;
+    asm volatile("" : "+v"(qn));  // keep the fp32 IEEE division (LLVM would narrow it to an inexact f16 one)
+    const float n = (den > eps) ? Dt<DT>::rnd(qn) : 0.f;
     out[(int64_t)b * S + i] = Dt<DT>::store(n);
   }
 }

@@ -81,12 +81,6 @@ __host__ __device__ inline int sel_nb(int64_t S) { return (int)((S + kBT - 1) / 
 // ------------------------------------------------------------------------------------ helpers
 __device__ __forceinline__ uint64_t lanemask_lt() { return (1ull << (threadIdx.x & 63)) - 1ull; }
 
-template <typename T> __device__ __forceinline__ void st_sc1(T* p, T v) {
-  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-template <typename T> __device__ __forceinline__ T ld_sc1(const T* p) {
-  return __hip_atomic_load(const_cast<T*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
 
 // Every wave drains its stores, the block meets, one lane counts in; true in every thread of the
 // last block to arrive (which then acquires).
@@ -974,7 +968,9 @@ __global__ __launch_bounds__(kGT) void sel_general_kernel(SelArgs g) {
 // ------------------------------------------------------------------------------------ launcher
 size_t select_workspace_bytes(int64_t B, int64_t S) {
   const size_t nb = (size_t)sel_nb(S);
-  return 256 + ((B * sizeof(SelState) + 255) / 256) * 256 + sel_hist_words(B) * 4 + B * nb * sizeof(SelPartial) + 256;
+  const size_t pipe = 256 + ((B * sizeof(SelState) + 255) / 256) * 256 + sel_hist_words(B) * 4 + B * nb * sizeof(SelPartial) + 256;
+  const size_t fast = select_fast_workspace_bytes(S);  // select_fast.hip shares the region
+  return pipe > fast ? pipe : fast;
 }
 
 static SelLayout carve_select(void* ws, int64_t B, int64_t S) {
@@ -1001,6 +997,7 @@ int launch_select(const FinalizeArgs& f, void* sel_ws, bool zeroed, hipStream_t 
   RTKV_REQUIRE(!f.mode_scores || f.A, "select: null aggregation input");
   RTKV_REQUIRE(f.S < ((int64_t)1 << 31), "select: S must be < 2^31");
   RTKV_REQUIRE(!f.mode_select || f.mask, "select: selection needs a mask buffer");
+  if (select_fast_eligible(f)) return launch_select_fast(f, sel_ws, zeroed, st);
   SelArgs g;
   g.f = f;
   // The emergency fallback (selective_propagation.py:205-211) runs only when no token fits the

@@ -1,0 +1,824 @@
+// select_fast.hip — K2 for one batch row (B = 1, S <= 32768: every reference configuration that
+// fits one GPU) in two launches instead of select.hip's four, with every per-token pass spread over
+// the whole grid.  Same outputs, bit for bit (scores, classes, mask, kept_index, row_offset,
+// statistics).
+//
+// Reference (per batch row), as in select.hip:
+//   scores      token_importance.py:134-176   s = α·N·w_l + β·log(i+1)/log(S) + γ·min(1, P/S)
+//   min-max     token_importance.py:49-85     (global min/max of A: K1 per-block partials)
+//   classes     dynamic_quantization.py:21-60
+//   selection   selective_propagation.py:68-161  greedy in closed form: top n_g of each class
+//   fallback    selective_propagation.py:205-211  topk(max(1, int(0.1·S))) if nothing selected
+//   compaction  selective_propagation.py:214-232  kept rows in ascending original index
+//
+// F1  fsel_score_kernel: G = ceil(S/1024) workgroups of 1024 threads, one token per thread.
+//     Scores and classes; per-workgroup class counts and score sums; a 4096-bin histogram per
+//     class over a FIXED linear binning of the score range (any monotone map of the score works:
+//     the histogram only has to tell which bin holds each class's threshold), and every token's
+//     (key, index) appended to a 64-entry slot list of its bin (slot = the histogram atomic's
+//     return value).  The LAST workgroup to arrive: quotas n_g from the class counts (the greedy
+//     in closed form), per partially kept class the bin where the count from the top reaches n_g,
+//     and the exact threshold from that bin's slot list (≤ 64 entries, one wave): key T and the
+//     number of tokens at T to take in index order.  A bin with more than 64 tokens (heavy ties)
+//     takes the exact rescan path: all S keys in registers, ≤ 3 LDS-histogram rounds.
+// F2  fsel_compact_kernel: the same G workgroups, one token per thread.  Keep decisions from
+//     (mode, T, ties) per class; per-workgroup aggregates (surely kept tokens per class, ties per
+//     group) published with sc1 stores + a flag; each workgroup sums its predecessors' aggregates
+//     (decoupled look-back: every aggregate is published before any is awaited, and workgroups are
+//     dispatched in index order, so the wait always ends), then ranks its tokens with block scans:
+//     mask, kept_index, row_offset.  The last workgroup writes the row statistics.
+//
+// Cross-workgroup hand-offs (MI355X_MICROARCH.md "Valid forms"): sc1 stores of every handed-off
+// word, every storing wave drains with s_waitcnt vmcnt(0), one lane signals (agent-scope atomic add,
+// or an sc1 flag store); the consumer reads with sc1 loads.
+#include "common.h"
+
+#ifdef RTKV_SELECT_PROBE  // diagnostic build (tools/k2_probe.hip): phase timestamps of the last F1 workgroup
+__device__ unsigned long long g_k2_probe[16];
+__device__ unsigned long long g_k2_clock[16];
+#define K2_PROBE(k) do { if (threadIdx.x == 0) { g_k2_probe[k] = __builtin_amdgcn_s_memrealtime(); g_k2_clock[k] = __builtin_amdgcn_s_memtime(); } } while (0)
+#else
+#define K2_PROBE(k) do { } while (0)
+#endif
+
+namespace rtkv {
+
+namespace {
+
+constexpr int kST = 1024;          // threads per workgroup
+constexpr int kSW = kST / kWave;   // waves
+constexpr int kBinBits = 12;
+constexpr int kNBin = 1 << kBinBits;
+constexpr int kGrp = 4;            // classes LOW, MEDIUM, HIGH + "all tokens" (fallback)
+constexpr int kCap = 64;           // slot list entries per bin (one per lane of a wave)
+constexpr int kMaxS = 32 * kST;    // 32 tokens per thread in the rescan path
+constexpr int kMaxG = kMaxS / kST; // workgroups
+enum { M_NONE = 0, M_ALL = 1, M_PART = 2 };
+
+struct FastPartial {               // per F1 workgroup, sc1 stores
+  uint32_t cnt[3];
+  uint32_t pad;
+  double ssum;
+};
+struct FastAgg {                   // per F2 workgroup, sc1 stores
+  uint64_t sure3;                  // 3 x 16-bit: kept tokens per class, ties at T excluded
+  uint64_t ties4;                  // 4 x 16-bit: tokens at each partial group's T
+  double ksum;                     // Σ scores of the kept tokens (ties included)
+  double m2;                       // Σ (s - mean)^2
+  uint64_t kept3;                  // 3 x 16-bit: kept tokens per class, ties included
+  uint64_t pad[3];
+};
+struct FastSel {                   // F1's last workgroup -> F2
+  int32_t mode[kGrp];
+  uint32_t thr[kGrp];              // threshold key T of each partial group
+  int32_t ties[kGrp];              // tokens at T to take, in index order
+  int32_t fallback;
+  int32_t pad;
+  double mean;                     // score mean (for Σ (s - mean)^2)
+  double ssum;
+  int64_t ccount[3];
+};
+struct FastHead {                  // zeroed before F1 (K1 or a memset)
+  uint32_t done1, done2;
+  uint32_t smin_c, smax;           // score keys: ~min and max (atomic max from zero)
+  uint32_t pad[60];
+  uint32_t flag[kMaxG];            // F2 aggregates published
+  uint32_t pad2[64 - kMaxG];
+};
+struct FastLayout {
+  FastHead* head;                  // zeroed
+  uint32_t* hist;                  // [kGrp][kNBin] (zeroed)
+  FastPartial* part;               // [G]
+  FastAgg* agg;                    // [G]
+  FastSel* sel;
+  uint64_t* slots;                 // [kGrp][kNBin][kCap] of (key << 32 | index)
+};
+
+struct FastArgs {
+  FinalizeArgs f;
+  FastLayout L;
+  float bin_lo[kGrp];              // bin(s) = clamp(floor((s - lo) * inv), 0, kNBin - 1): monotone in s
+  float bin_inv[kGrp];
+  int hist_fb;                     // histogram the fallback group too (fallback possible)
+};
+
+__device__ __forceinline__ float key_score(uint32_t k) {
+  const uint32_t u = (k & 0x80000000u) ? (k & 0x7fffffffu) : ~k;
+  return __builtin_bit_cast(float, u);
+}
+
+// Monotone non-decreasing in the order-preserving key of s (NaNs: sign-bit ones below every
+// number, the others above, as in score_key).
+__device__ __forceinline__ int bin_of(float s, float lo, float inv) {
+  const float x = floorf((s - lo) * inv);
+  if (x != x) return (__builtin_bit_cast(uint32_t, s) >> 31) ? 0 : kNBin - 1;
+  return x <= 0.f ? 0 : (x >= (float)(kNBin - 1) ? kNBin - 1 : (int)x);
+}
+
+// Hide a value's provenance from the optimiser at a phase boundary, so that per-token values derived
+// from it (the 2-bit groups) are recomputed in each phase instead of being kept live across phases.
+template <typename T> __device__ __forceinline__ void opaque(T& v) { asm volatile("" : "+v"(v)); }
+
+__device__ __forceinline__ uint32_t fld(uint64_t v, int g) { return (uint32_t)(v >> (16 * g)) & 0xffffu; }
+
+// Exclusive block scan of a packed uint64 (independent 16-bit fields whose block totals stay
+// < 65536); *total = the block total.  `sh` is a [kSW] LDS array private to this call site.
+__device__ __forceinline__ uint64_t block_excl_scan(uint64_t v, uint64_t* sh, uint64_t* total) {
+  const int lane = threadIdx.x & (kWave - 1), wid = threadIdx.x / kWave;
+  const uint64_t inc = wave_inclusive_scan(v);
+  if (lane == kWave - 1) sh[wid] = inc;
+  __syncthreads();
+  // lanes 0..15 scan the 16 wave totals; lane wid-1 holds the base of this wave, lane 15 the total
+  uint64_t ws = sh[lane & (kSW - 1)];
+#pragma unroll
+  for (int o = 1; o < kSW; o <<= 1) {
+    const uint64_t n = __shfl_up(ws, o, kWave);
+    if ((lane & (kSW - 1)) >= o) ws += n;
+  }
+  *total = __shfl(ws, kSW - 1, kWave);
+  const uint64_t base = wid > 0 ? __shfl(ws, wid - 1, kWave) : 0ull;
+  return base + inc - v;
+}
+
+__device__ __forceinline__ int64_t row_bytes(const FinalizeArgs& a, int lab) {
+  return (a.F * field_width(a.kv_dtype < 0 ? RTKV_F32 : a.kv_dtype, a.p.bits[lab]) + 7) / 8;
+}
+
+__device__ __forceinline__ float bin_lo_of(const FastArgs& g, int q) {
+  return q == 3 ? g.bin_lo[3] : (q == 2 ? g.bin_lo[2] : (q == 1 ? g.bin_lo[1] : g.bin_lo[0]));
+}
+__device__ __forceinline__ float bin_inv_of(const FastArgs& g, int q) {
+  return q == 3 ? g.bin_inv[3] : (q == 2 ? g.bin_inv[2] : (q == 1 ? g.bin_inv[1] : g.bin_inv[0]));
+}
+
+__device__ __forceinline__ int class_of(float s, const rtkv_layer_params& p) {
+  return (s >= p.theta_h) ? 2 : ((s >= p.theta_m && s < p.theta_h) ? 1 : 0);  // dynamic_quantization.py:41-45
+}
+
+// ------------------------------------------------------------------------------------ rescan path
+// Exact threshold of every group in `heavy` (a threshold bin with more than kCap tokens: heavy
+// ties) from all S keys held in registers: candidates = the group's tokens in its threshold bin,
+// then ≤ 3 rounds of key-range LDS histograms (span −12 bits per round).  need[q]: tokens to take
+// from the candidates on entry, tokens at the threshold key on exit.
+template <int TPT>
+__device__ __forceinline__ void rescan_thresholds(const FastArgs& g, uint32_t* hist_lds, int heavy, bool fallback,
+                                                  const int (&bstar)[kGrp], int (&need)[kGrp], uint32_t (&thr)[kGrp]) {
+  const FinalizeArgs& a = g.f;
+  __shared__ uint64_t s_scan[4][kSW];
+  __shared__ uint32_t s_key[2 * kGrp][kSW];
+  __shared__ uint32_t s_pick[2][kGrp][2];
+  const int t = threadIdx.x, lane = t & (kWave - 1), wid = t / kWave;
+  const int S = (int)a.S;
+  const int i0 = t * TPT;
+  const int nv = S - i0 < 0 ? 0 : (S - i0 > TPT ? TPT : S - i0);
+  float sv[TPT];
+#pragma unroll
+  for (int k = 0; k < TPT; ++k) sv[k] = ld_sc1(a.scores + (i0 + k < S ? i0 + k : S - 1));
+  uint32_t key[TPT];
+  uint64_t grp = 0;  // 2 bits per token: its group
+  uint32_t cand = 0;
+  uint32_t kmn[kGrp], kmx[kGrp];
+#pragma unroll
+  for (int q = 0; q < kGrp; ++q) { kmn[q] = 0xffffffffu; kmx[q] = 0u; }
+#pragma unroll
+  for (int k = 0; k < TPT; ++k) {
+    const float s = sv[k];
+    const int e = fallback ? 3 : class_of(s, a.p);
+    grp |= (uint64_t)e << (2 * k);
+    key[k] = score_key(s);
+    bool c = false;
+#pragma unroll
+    for (int q = 0; q < kGrp; ++q) {
+      const bool cq = (k < nv) & (e == q) & (((heavy >> q) & 1) != 0) & (bin_of(s, g.bin_lo[q], g.bin_inv[q]) == bstar[q]);
+      kmn[q] = cq ? min(kmn[q], key[k]) : kmn[q];
+      kmx[q] = cq ? max(kmx[q], key[k]) : kmx[q];
+      c |= cq;
+    }
+    cand |= (uint32_t)c << k;
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1)
+#pragma unroll
+    for (int q = 0; q < kGrp; ++q) {
+      kmn[q] = min(kmn[q], (uint32_t)__shfl_xor((int)kmn[q], o, kWave));
+      kmx[q] = max(kmx[q], (uint32_t)__shfl_xor((int)kmx[q], o, kWave));
+    }
+  if (lane == 0) {
+#pragma unroll
+    for (int q = 0; q < kGrp; ++q) { s_key[q][wid] = kmn[q]; s_key[kGrp + q][wid] = kmx[q]; }
+  }
+  __syncthreads();
+  uint32_t lo[kGrp], hi[kGrp];
+  {
+    const int src = lane & (kSW - 1);
+#pragma unroll
+    for (int q = 0; q < kGrp; ++q) { kmn[q] = s_key[q][src]; kmx[q] = s_key[kGrp + q][src]; }
+#pragma unroll
+    for (int o = kSW / 2; o > 0; o >>= 1)
+#pragma unroll
+      for (int q = 0; q < kGrp; ++q) {
+        kmn[q] = min(kmn[q], (uint32_t)__shfl_xor((int)kmn[q], o, kWave));
+        kmx[q] = max(kmx[q], (uint32_t)__shfl_xor((int)kmx[q], o, kWave));
+      }
+#pragma unroll
+    for (int q = 0; q < kGrp; ++q) { lo[q] = kmn[q]; hi[q] = kmx[q]; }
+  }
+#pragma unroll 1
+  for (int round = 0; round < 4; ++round) {
+    int act = 0, sh[kGrp];
+#pragma unroll
+    for (int q = 0; q < kGrp; ++q) {
+      if (((heavy >> q) & 1) && lo[q] != hi[q]) act |= 1 << q;
+      const int bl = 32 - __clz((int)(hi[q] - lo[q]));
+      sh[q] = bl > kBinBits ? bl - kBinBits : 0;
+    }
+    if (!act) break;
+    opaque(grp);
+    for (int w = t; w < kGrp * kNBin / 4; w += kST) reinterpret_cast<uint4*>(hist_lds)[w] = make_uint4(0u, 0u, 0u, 0u);
+    if (t < kGrp) { s_pick[round & 1][t][0] = 0u; s_pick[round & 1][t][1] = 0u; }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < TPT; ++k) {
+      const int e = (int)((grp >> (2 * k)) & 3u);
+      bool in = false;
+      uint32_t off = 0u;
+#pragma unroll
+      for (int q = 0; q < kGrp; ++q) {  // per-group compares combined by masks: no per-token indexing
+        const bool iq = (((cand >> k) & 1u) != 0) & (e == q) & (((act >> q) & 1) != 0) & (key[k] >= lo[q]) &
+                        (key[k] <= hi[q]);
+        in |= iq;
+        off = iq ? (uint32_t)(q * kNBin) + ((key[k] - lo[q]) >> sh[q]) : off;
+      }
+      if (in) atomicAdd(&hist_lds[off], 1u);
+    }
+    __syncthreads();
+    uint32_t c[kGrp][4];
+    uint64_t pk = 0;
+#pragma unroll
+    for (int q = 0; q < kGrp; ++q) {
+      const uint4 h4 = (act >> q) & 1 ? reinterpret_cast<const uint4*>(hist_lds + q * kNBin)[kNBin / 4 - 1 - t]
+                                      : make_uint4(0u, 0u, 0u, 0u);
+      c[q][0] = h4.w; c[q][1] = h4.z; c[q][2] = h4.y; c[q][3] = h4.x;
+      pk |= (uint64_t)(c[q][0] + c[q][1] + c[q][2] + c[q][3]) << (16 * q);
+    }
+    uint64_t tot;
+    const uint64_t ex = block_excl_scan(pk, s_scan[round], &tot);
+#pragma unroll
+    for (int q = 0; q < kGrp; ++q) {
+      if (!((act >> q) & 1)) continue;
+      int run = (int)fld(ex, q);
+      if (run < need[q] && need[q] <= run + (int)fld(pk, q)) {
+        bool found = false;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          if (!found && run + (int)c[q][j] >= need[q]) {
+            s_pick[round & 1][q][0] = (uint32_t)(kNBin - 1 - 4 * t - j);
+            s_pick[round & 1][q][1] = (uint32_t)run;
+            found = true;
+          }
+          run += c[q][j];
+        }
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < kGrp; ++q) {
+      if (!((act >> q) & 1)) continue;
+      const uint64_t nlo = (uint64_t)lo[q] + ((uint64_t)s_pick[round & 1][q][0] << sh[q]);
+      const uint64_t nhi = nlo + ((1ull << sh[q]) - 1ull);
+      need[q] -= (int)s_pick[round & 1][q][1];
+      lo[q] = (uint32_t)nlo;
+      hi[q] = nhi < (uint64_t)hi[q] ? (uint32_t)nhi : hi[q];
+    }
+  }
+#pragma unroll
+  for (int q = 0; q < kGrp; ++q)
+    if ((heavy >> q) & 1) thr[q] = lo[q];
+}
+
+// ------------------------------------------------------------------------------------ thresholds
+// The last F1 workgroup: quotas, threshold bins, exact thresholds.  Writes FastSel.
+template <int TPT>
+__device__ __forceinline__ void select_thresholds(const FastArgs& g, uint32_t* hist_lds) {
+  const FinalizeArgs& a = g.f;
+  __shared__ uint64_t s_scan[kSW];
+  __shared__ uint32_t s_pick[kGrp][3];
+  __shared__ uint32_t s_thr[kGrp];
+  __shared__ int s_tie[kGrp];
+  const int t = threadIdx.x, lane = t & (kWave - 1), wid = t / kWave;
+  const int S = (int)a.S;
+  const int G = (S + kST - 1) / kST;
+  K2_PROBE(0);
+  // ---- partials of the F1 workgroups (lane l of every wave reads workgroup l; G <= 32)
+  uint32_t c0 = 0, c1 = 0, c2 = 0;
+  double ssum = 0.0;
+  if (lane < G) {
+    const FastPartial* pp = g.L.part + lane;
+    c0 = ld_sc1(&pp->cnt[0]);
+    c1 = ld_sc1(&pp->cnt[1]);
+    c2 = ld_sc1(&pp->cnt[2]);
+    ssum = ld_sc1(&pp->ssum);
+  }
+#pragma unroll
+  for (int o = kWave / 2; o > 0; o >>= 1) {  // lanes >= G hold zeros
+    c0 += __shfl_xor(c0, o, kWave);
+    c1 += __shfl_xor(c1, o, kWave);
+    c2 += __shfl_xor(c2, o, kWave);
+    ssum += __shfl_xor(ssum, o, kWave);
+  }
+  const int64_t ccount[3] = {(int64_t)c0, (int64_t)c1, (int64_t)c2};
+  // ---- quotas: the greedy in closed form (selective_propagation.py:93-131), every thread
+  int mode[kGrp];
+  int need[kGrp];
+  {
+    const double u8 = 8.0 * ((double)S * a.p.propagation_ratio);
+    const int64_t U = (u8 >= 0.0) ? (u8 >= 9.0e18 ? (int64_t)9000000000000000000LL : (int64_t)floor(u8)) : -1;
+    int64_t used = 0, kept = 0;
+#pragma unroll
+    for (int k = 2; k >= 0; --k) {
+      const int64_t N = ccount[k], bb = a.p.bits[k];
+      int64_t n;
+      if (a.mode_select == 2) n = N;
+      else if (U < 0) n = 0;
+      else if (bb <= 0) n = N;
+      else {
+        const int64_t fit = (U - used) / bb;
+        n = fit < N ? fit : N;
+      }
+      used += n * (bb > 0 ? bb : 0);
+      kept += n;
+      need[k] = (int)n;
+      mode[k] = (n == 0) ? M_NONE : (n == N ? M_ALL : M_PART);
+    }
+    int64_t kf = (int64_t)((double)S * 0.1);
+    if (kf < 1) kf = 1;
+    const bool fb = a.mode_select == 1 && !(a.p.flags & RTKV_NO_FALLBACK) && kept == 0;
+    need[3] = (int)kf;
+    mode[3] = !fb ? M_NONE : (kf >= S ? M_ALL : M_PART);
+  }
+  const bool fallback = mode[3] != M_NONE;
+  int part = 0;
+#pragma unroll
+  for (int q = 0; q < kGrp; ++q) part |= (mode[q] == M_PART) << q;
+  uint32_t thr[kGrp] = {0u, 0u, 0u, 0u};
+  if (part) {
+    // ---- the bin holding each partial group's threshold: thread t owns descending bins 4t..4t+3
+    uint32_t c[kGrp][4];
+    uint64_t pk = 0;
+#pragma unroll
+    for (int q = 0; q < kGrp; ++q) {
+      const uint32_t* hq = g.L.hist + q * kNBin + (kNBin - 4 - 4 * t);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) c[q][j] = ((part >> q) & 1) ? ld_sc1(hq + 3 - j) : 0u;
+      pk |= (uint64_t)(c[q][0] + c[q][1] + c[q][2] + c[q][3]) << (16 * q);
+    }
+    if (t < kGrp) { s_pick[t][0] = 0u; s_pick[t][1] = 0u; s_pick[t][2] = 0u; }
+    uint64_t tot;
+    const uint64_t ex = block_excl_scan(pk, s_scan, &tot);
+#pragma unroll
+    for (int q = 0; q < kGrp; ++q) {
+      if (!((part >> q) & 1)) continue;
+      int run = (int)fld(ex, q);
+      if (run < need[q] && need[q] <= run + (int)fld(pk, q)) {
+        bool found = false;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          if (!found && run + (int)c[q][j] >= need[q]) {
+            s_pick[q][0] = (uint32_t)(kNBin - 1 - 4 * t - j);
+            s_pick[q][1] = (uint32_t)run;          // tokens of the group in higher bins
+            s_pick[q][2] = c[q][j];                // tokens in the bin
+            found = true;
+          }
+          run += c[q][j];
+        }
+      }
+    }
+    __syncthreads();
+    int bstar[kGrp] = {0, 0, 0, 0};
+    int heavy = 0;
+#pragma unroll
+    for (int q = 0; q < kGrp; ++q) {
+      if (!((part >> q) & 1)) continue;
+      bstar[q] = (int)s_pick[q][0];
+      need[q] -= (int)s_pick[q][1];
+      if ((int)s_pick[q][2] > kCap) heavy |= 1 << q;
+    }
+    K2_PROBE(1);
+    // ---- light bins: wave q ranks its group's slot list (≤ 64 entries, one per lane)
+    if (wid < kGrp && ((part >> wid) & 1) && !((heavy >> wid) & 1)) {
+      const int q = wid;
+      const int n = (int)s_pick[q][2];
+      const uint64_t* sl = g.L.slots + ((size_t)q * kNBin + (size_t)bstar[q]) * kCap;
+      const uint64_t e = lane < n ? ld_sc1(sl + lane) : 0ull;
+      const uint32_t k = (uint32_t)(e >> 32), idx = (uint32_t)e;
+      // rank = entries ahead of this one in (key desc, index asc) order
+      int rank = 0;
+      for (int j = 0; j < n; ++j) {
+        const uint64_t o = __shfl(e, j, kWave);
+        const uint32_t ok = (uint32_t)(o >> 32), oi = (uint32_t)o;
+        rank += (ok > k) | ((ok == k) & (oi < idx));
+      }
+      const int r = need[q];  // 1 <= r <= n
+      const uint64_t hit = __ballot(lane < n && rank == r - 1);
+      const int src = hit ? (__ffsll((unsigned long long)hit) - 1) : 0;
+      const uint32_t T = (uint32_t)__shfl((int)k, src, kWave);
+      const uint64_t above = __ballot(lane < n && k > T);
+      if (lane == 0) { s_thr[q] = T; s_tie[q] = r - __popcll(above); }
+    }
+    if (heavy) rescan_thresholds<TPT>(g, hist_lds, heavy, fallback, bstar, need, thr);
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < kGrp; ++q) {
+      if (!((part >> q) & 1) || ((heavy >> q) & 1)) continue;
+      thr[q] = s_thr[q];
+      need[q] = s_tie[q];
+    }
+  }
+  K2_PROBE(2);
+  if (t != 0) return;
+  FastSel* fs = g.L.sel;
+  for (int q = 0; q < kGrp; ++q) {
+    fs->mode[q] = mode[q];
+    fs->thr[q] = thr[q];
+    fs->ties[q] = need[q];
+  }
+  fs->fallback = fallback ? 1 : 0;
+  fs->mean = ssum / (double)S;
+  fs->ssum = ssum;
+  for (int q = 0; q < 3; ++q) fs->ccount[q] = ccount[q];
+}
+
+// ------------------------------------------------------------------------------------ F1
+template <int TPT, bool HAS_T2, int DT>
+__global__ __launch_bounds__(kST) void fsel_score_kernel(FastArgs g) {
+  const FinalizeArgs& a = g.f;
+  extern __shared__ uint32_t hist_lds[];   // [kGrp][kNBin] (the rescan path's rounds)
+  __shared__ float s_mm[2][kSW];
+  __shared__ double s_sum[kSW];
+  __shared__ uint32_t s_c[5][kSW];
+  __shared__ int s_flag;
+  const int t = threadIdx.x, lane = t & (kWave - 1), wid = t / kWave;
+  const int S = (int)a.S;
+  // ---- global min/max of A (token_importance.py:71-83): K1's per-block partials, or the row
+  float mn = INFINITY, mx = -INFINITY;
+  if (a.A_part) {
+    for (int k = t; k < a.A_nparts; k += kST) { mn = fminf(mn, a.A_part[2 * k]); mx = fmaxf(mx, a.A_part[2 * k + 1]); }
+  } else {
+    for (int k = t; k < S; k += kST) { mn = fminf(mn, a.A[k]); mx = fmaxf(mx, a.A[k]); }
+  }
+  mn = wave_min(mn);
+  mx = wave_max(mx);
+  if (lane == 0) { s_mm[0][wid] = mn; s_mm[1][wid] = mx; }
+  __syncthreads();
+  mn = s_mm[0][lane & (kSW - 1)];
+  mx = s_mm[1][lane & (kSW - 1)];
+#pragma unroll
+  for (int o = kSW / 2; o > 0; o >>= 1) { mn = fminf(mn, __shfl_xor(mn, o, kWave)); mx = fmaxf(mx, __shfl_xor(mx, o, kWave)); }
+  const float den = Dt<DT>::rnd(mx - mn), eps = Dt<DT>::rnd(1e-8f);
+  // ---- this thread's token: score, class, histogram bin + slot
+  const int i = blockIdx.x * kST + t;
+  const bool valid = i < S;
+  float s = 0.f;
+  int l = 0;
+  if (valid) {
+    const float Ai = a.A[i];
+    // Every op is an fp32 op rounded to the dtype (PyTorch CPU).  The barriers keep it so for f16:
+    // without them LLVM narrows fptrunc(fdiv(fpext h, fpext h)) to an f16 division (not correctly
+    // rounded on gfx950) and fptrunc(fmul(fpext h, f32)) to v_fma_mix (one rounding instead of two).
+    float qn = Dt<DT>::rnd(Ai - mn) / den;
+    opaque(qn);
+    const float N = (den > eps) ? Dt<DT>::rnd(qn) : 0.f;
+    float p1 = N * a.p.alpha;
+    opaque(p1);
+    float p2 = Dt<DT>::rnd(p1) * a.p.layer_weight;
+    opaque(p2);
+    const float t1 = Dt<DT>::rnd(p2);
+    const float t2 = HAS_T2 ? a.T2[i] : a.p.beta * ((S > 1) ? torch_logf((uint32_t)(i + 1)) / a.logS : 0.f);
+    s = t1 + t2;
+    s = s + a.p.gamma * a.ctx;
+    l = class_of(s, a.p);
+    st_sc1(a.scores + i, s);
+    a.labels[i] = (uint8_t)l;
+    if (a.mode_select == 1) {
+      const uint64_t entry = ((uint64_t)score_key(s) << 32) | (uint32_t)i;
+      const int b = l * kNBin + bin_of(s, bin_lo_of(g, l), bin_inv_of(g, l));
+      const uint32_t slot = atomicAdd(&g.L.hist[b], 1u);
+      if (slot < kCap) st_sc1(g.L.slots + (size_t)b * kCap + slot, entry);
+      if (g.hist_fb) {
+        const int b3 = 3 * kNBin + bin_of(s, g.bin_lo[3], g.bin_inv[3]);
+        const uint32_t slot3 = atomicAdd(&g.L.hist[b3], 1u);
+        if (slot3 < kCap) st_sc1(g.L.slots + (size_t)b3 * kCap + slot3, entry);
+      }
+    }
+  }
+  // ---- workgroup partials: class counts, score sum, score key range
+  const uint64_t b0 = __ballot(valid && l == 0), b1 = __ballot(valid && l == 1), b2 = __ballot(valid && l == 2);
+  const double sw = wave_sum(valid ? (double)s : 0.0);
+  uint32_t kmn = valid ? score_key(s) : 0xffffffffu, kmx = valid ? score_key(s) : 0u;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    kmn = min(kmn, (uint32_t)__shfl_xor((int)kmn, o, kWave));
+    kmx = max(kmx, (uint32_t)__shfl_xor((int)kmx, o, kWave));
+  }
+  if (lane == 0) {
+    s_c[0][wid] = __popcll(b0); s_c[1][wid] = __popcll(b1); s_c[2][wid] = __popcll(b2);
+    s_c[3][wid] = kmn; s_c[4][wid] = kmx;
+    s_sum[wid] = sw;
+  }
+  __syncthreads();
+  if (wid == 0) {
+    const int src = lane & (kSW - 1);
+    uint32_t c0 = s_c[0][src], c1 = s_c[1][src], c2 = s_c[2][src], m0 = s_c[3][src], m1 = s_c[4][src];
+    double ss = s_sum[src];
+#pragma unroll
+    for (int o = kSW / 2; o > 0; o >>= 1) {
+      c0 += __shfl_xor(c0, o, kWave);
+      c1 += __shfl_xor(c1, o, kWave);
+      c2 += __shfl_xor(c2, o, kWave);
+      m0 = min(m0, (uint32_t)__shfl_xor((int)m0, o, kWave));
+      m1 = max(m1, (uint32_t)__shfl_xor((int)m1, o, kWave));
+      ss += __shfl_xor(ss, o, kWave);
+    }
+    if (lane == 0) {
+      FastPartial* pp = g.L.part + blockIdx.x;
+      st_sc1(&pp->cnt[0], c0);
+      st_sc1(&pp->cnt[1], c1);
+      st_sc1(&pp->cnt[2], c2);
+      st_sc1(&pp->ssum, ss);
+      atomicMax(&g.L.head->smin_c, ~m0);  // minima complemented: the head starts at 0
+      atomicMax(&g.L.head->smax, m1);
+    }
+  }
+  // ---- the last workgroup to arrive finds the thresholds for the whole row
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (t == 0) {
+    const uint32_t old = __hip_atomic_fetch_add(&g.L.head->done1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    s_flag = (old + 1 == gridDim.x);
+    if (s_flag) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+  }
+  __syncthreads();
+  if (!s_flag) return;
+  select_thresholds<TPT>(g, hist_lds);
+}
+
+// ------------------------------------------------------------------------------------ F2
+__global__ __launch_bounds__(kST) void fsel_compact_kernel(FastArgs g) {
+  const FinalizeArgs& a = g.f;
+  __shared__ uint64_t s_scan[2][kSW];
+  __shared__ uint64_t s_r[2][kSW];
+  __shared__ double s_d[2][kSW];
+  __shared__ uint64_t s_base[3];
+  __shared__ int s_flag;
+  const int t = threadIdx.x, lane = t & (kWave - 1), wid = t / kWave;
+  const int S = (int)a.S;
+  const int blk = blockIdx.x;
+  const FastSel& fs = *g.L.sel;
+  int mode[kGrp], tq[kGrp];
+  uint32_t thr[kGrp];
+#pragma unroll
+  for (int q = 0; q < kGrp; ++q) { mode[q] = fs.mode[q]; thr[q] = fs.thr[q]; tq[q] = fs.ties[q]; }
+  const bool fallback = fs.fallback != 0;
+  // the class of group q's tokens at its threshold: q for a class; for the fallback group, the class
+  // of the threshold score (equal scores have equal classes)
+  const int tcls3 = class_of(key_score(thr[3]), a.p);
+  // ---- this thread's token
+  const int i = blk * kST + t;
+  const bool valid = i < S;
+  float s = 0.f;
+  int l = 0;
+  if (valid) { s = a.scores[i]; l = a.labels[i]; }
+  const uint32_t key = score_key(s);
+  const int e = valid ? (fallback ? 3 : l) : 4;
+  bool sure = false;  // kept regardless of the tie order
+  uint64_t tie = 0;
+#pragma unroll
+  for (int q = 0; q < kGrp; ++q) {
+    const bool mine = e == q;
+    sure |= mine & ((mode[q] == M_ALL) | ((mode[q] == M_PART) & (key > thr[q])));
+    tie |= (mine & (mode[q] == M_PART) & (key == thr[q])) ? 1ull << (16 * q) : 0ull;
+  }
+  const uint64_t sure3 = (valid & sure) ? 1ull << (16 * l) : 0ull;
+  // ---- workgroup aggregates: surely kept per class, ties per group (published before any wait)
+  const uint64_t as = wave_sum(sure3), at = wave_sum(tie);
+  if (lane == 0) { s_r[0][wid] = as; s_r[1][wid] = at; }
+  __syncthreads();
+  if (wid == 0) {
+    uint64_t x = s_r[0][lane & (kSW - 1)], y = s_r[1][lane & (kSW - 1)];
+#pragma unroll
+    for (int o = kSW / 2; o > 0; o >>= 1) { x += __shfl_xor(x, o, kWave); y += __shfl_xor(y, o, kWave); }
+    if (lane == 0) {
+      st_sc1(&g.L.agg[blk].sure3, x);
+      st_sc1(&g.L.agg[blk].ties4, y);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      st_sc1(&g.L.head->flag[blk], 1u);
+    }
+    // look-back: lane p < blk waits for workgroup p's aggregate
+    uint64_t ps = 0, pt = 0;
+    if (lane < blk) {
+      while (ld_sc1(&g.L.head->flag[lane]) == 0u) __builtin_amdgcn_s_sleep(1);
+      ps = ld_sc1(&g.L.agg[lane].sure3);
+      pt = ld_sc1(&g.L.agg[lane].ties4);
+    }
+    // ties that predecessor p takes: those of its ties whose row-wide rank is below the quota
+    const uint64_t before = wave_inclusive_scan(pt) - pt;
+    uint64_t taken = 0;  // per class
+#pragma unroll
+    for (int q = 0; q < kGrp; ++q) {
+      const int b4 = (int)fld(before, q), mine_t = (int)fld(pt, q);
+      int take = tq[q] - b4;
+      take = take < 0 ? 0 : (take > mine_t ? mine_t : take);
+      taken += (uint64_t)take << (16 * (q < 3 ? q : tcls3));
+    }
+    ps = wave_sum(ps);
+    taken = wave_sum(taken);
+    pt = wave_sum(pt);
+    if (lane == 0) { s_base[0] = ps + taken; s_base[1] = pt; }
+  }
+  __syncthreads();
+  const uint64_t kept_before = s_base[0], ties_before = s_base[1];
+  // ---- ties: ranks in index order across the whole row
+  uint64_t tie_tot;
+  const uint64_t tie_rank = block_excl_scan(tie, s_scan[0], &tie_tot) + ties_before;
+  bool take = false;
+#pragma unroll
+  for (int q = 0; q < kGrp; ++q) take |= (((tie >> (16 * q)) & 1ull) != 0) & ((int)fld(tie_rank, q) < tq[q]);
+  const bool kept = valid & (sure | take);
+  const uint64_t k3 = kept ? 1ull << (16 * l) : 0ull;
+  uint64_t kept_tot;
+  const uint64_t rank3 = block_excl_scan(k3, s_scan[1], &kept_tot) + kept_before;
+  int64_t rb[3];
+#pragma unroll
+  for (int q = 0; q < 3; ++q) rb[q] = row_bytes(a, q);
+  if (valid) {
+    a.mask[i] = kept ? 1 : 0;
+    if (kept) {
+      const int64_t row = (int64_t)fld(rank3, 0) + fld(rank3, 1) + fld(rank3, 2);
+      if (row < a.row_capacity) {
+        a.kept_index[row] = i;
+        if (a.row_offset)
+          a.row_offset[row] = (int64_t)fld(rank3, 0) * rb[0] + (int64_t)fld(rank3, 1) * rb[1] + (int64_t)fld(rank3, 2) * rb[2];
+      }
+    }
+  }
+  // ---- statistics partials: Σ kept scores, Σ (s - mean)^2, kept per class
+  const double d = (double)s - fs.mean;
+  const double ks = wave_sum(kept ? (double)s : 0.0), m2 = wave_sum(valid ? d * d : 0.0);
+  if (lane == 0) { s_d[0][wid] = ks; s_d[1][wid] = m2; }
+  __syncthreads();
+  if (wid == 0) {
+    double x = s_d[0][lane & (kSW - 1)], y = s_d[1][lane & (kSW - 1)];
+#pragma unroll
+    for (int o = kSW / 2; o > 0; o >>= 1) { x += __shfl_xor(x, o, kWave); y += __shfl_xor(y, o, kWave); }
+    if (lane == 0) {
+      st_sc1(&g.L.agg[blk].ksum, x);
+      st_sc1(&g.L.agg[blk].m2, y);
+      st_sc1(&g.L.agg[blk].kept3, kept_tot);
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (t == 0) {
+    const uint32_t old = __hip_atomic_fetch_add(&g.L.head->done2, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    s_flag = (old + 1 == gridDim.x);
+  }
+  __syncthreads();
+  if (!s_flag || wid != 0) return;
+  // ---- the last workgroup: row statistics (the fields select.hip's C1/C2 write)
+  const int G = gridDim.x;
+  double ksum = 0.0, m2s = 0.0;
+  uint64_t kt = 0;
+  if (lane < G) {
+    ksum = ld_sc1(&g.L.agg[lane].ksum);
+    m2s = ld_sc1(&g.L.agg[lane].m2);
+    kt = ld_sc1(&g.L.agg[lane].kept3);
+  }
+#pragma unroll
+  for (int o = kWave / 2; o > 0; o >>= 1) {
+    ksum += __shfl_xor(ksum, o, kWave);
+    m2s += __shfl_xor(m2s, o, kWave);
+    kt += __shfl_xor(kt, o, kWave);
+  }
+  if (lane != 0) return;
+  rtkv_layer_stats* hs = a.stats;
+  rtkv_batch_stats* bs = reinterpret_cast<rtkv_batch_stats*>(hs + 1);
+  int64_t kept_n = 0, units = 0, pbytes = 0;
+  for (int q = 0; q < 3; ++q) {
+    const int64_t n = fld(kt, q);
+    bs->class_count[q] = fs.ccount[q];
+    bs->kept_class[q] = n;
+    kept_n += n;
+    units += n * a.p.bits[q];
+    pbytes += n * rb[q];
+  }
+  bs->kept = kept_n;
+  bs->cost_units = units;
+  bs->packed_bytes = pbytes;
+  bs->fallback = fallback ? 1 : 0;
+  bs->reserved = 0;
+  bs->kept_score_sum = ksum;
+  hs->max_kept = kept_n;
+  hs->total_packed_bytes = pbytes;
+  hs->score_sum = fs.ssum;
+  hs->score_m2 = m2s;
+  hs->score_min = key_score(~ld_sc1(&g.L.head->smin_c));
+  hs->score_max = key_score(ld_sc1(&g.L.head->smax));
+  int flags = 0;
+  if (a.kv_dtype == RTKV_F16)
+    for (int q = 0; q < 3; ++q)
+      if (fs.ccount[q] > 0 && a.p.bits[q] >= 16) flags |= RTKV_FLAG_F16_QMAX_OVERFLOW;
+  hs->error_flags = flags;
+  hs->B = 1;
+}
+
+}  // namespace
+
+// ------------------------------------------------------------------------------------ host
+bool select_fast_shape(int64_t B, int64_t S) { return B == 1 && S >= 1 && S <= kMaxS; }
+
+bool select_fast_eligible(const FinalizeArgs& f) {
+  return select_fast_shape(f.B, f.S) && !(f.p.flags & RTKV_SELECT_PIPELINE) && f.mode_scores && f.mode_labels &&
+         (f.mode_select == 1 || f.mode_select == 2) && f.mask && f.kept_index;
+}
+
+// Workspace: [FastHead][hist][partials][aggregates][sel][slots]; the first select_fast_zero_bytes()
+// must be zero before F1 (K1 clears them in rtkv_compress_layer).
+size_t select_fast_zero_bytes() { return sizeof(FastHead) + (size_t)kGrp * kNBin * 4; }
+size_t select_fast_workspace_bytes(int64_t) {
+  return select_fast_zero_bytes() + kMaxG * sizeof(FastPartial) + kMaxG * sizeof(FastAgg) + 256 +
+         (size_t)kGrp * kNBin * kCap * 8;
+}
+
+template <int TPT, bool HAS_T2, int DT> static int launch_f1(const FastArgs& g, int G, hipStream_t st) {
+  const size_t lds = (size_t)kGrp * kNBin * sizeof(uint32_t);
+  static bool attr = false;  // per instantiation
+  if (!attr) {
+    RTKV_HIP_CHECK(hipFuncSetAttribute((const void*)fsel_score_kernel<TPT, HAS_T2, DT>,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    attr = true;
+  }
+  hipLaunchKernelGGL((fsel_score_kernel<TPT, HAS_T2, DT>), dim3(G), dim3(kST), lds, st, g);
+  RTKV_HIP_CHECK(hipGetLastError());
+  return RTKV_OK;
+}
+
+template <int TPT, bool HAS_T2> static int launch_f1_dt(const FastArgs& g, int G, hipStream_t st) {
+  switch (g.f.a_dtype) {
+    case RTKV_F16: return launch_f1<TPT, HAS_T2, RTKV_F16>(g, G, st);
+    case RTKV_BF16: return launch_f1<TPT, HAS_T2, RTKV_BF16>(g, G, st);
+    default: return launch_f1<TPT, HAS_T2, RTKV_F32>(g, G, st);
+  }
+}
+
+int launch_select_fast(const FinalizeArgs& f, void* ws, bool zeroed, hipStream_t st) {
+  RTKV_REQUIRE(select_fast_eligible(f), "select_fast: not eligible");
+  FastArgs g;
+  g.f = f;
+  char* p = static_cast<char*>(ws);
+  g.L.head = reinterpret_cast<FastHead*>(p);
+  p += sizeof(FastHead);
+  g.L.hist = reinterpret_cast<uint32_t*>(p);
+  p += (size_t)kGrp * kNBin * 4;
+  g.L.part = reinterpret_cast<FastPartial*>(p);
+  p += kMaxG * sizeof(FastPartial);
+  g.L.agg = reinterpret_cast<FastAgg*>(p);
+  p += kMaxG * sizeof(FastAgg);
+  g.L.sel = reinterpret_cast<FastSel*>(p);
+  p += 256;
+  g.L.slots = reinterpret_cast<uint64_t*>(p);
+  // Fixed score binning.  s = t1 + t2 + t3 with t1 = α·w·N (N in [0, 1]), t2 = β·pos (pos in
+  // [0, 1]), t3 = γ·ctx: any range works for correctness (bins are clamped, the map stays
+  // monotone); this one spreads the scores over the bins.
+  const double aw = (double)f.p.alpha * (double)f.p.layer_weight, be = f.p.beta, t3 = (double)f.p.gamma * f.ctx;
+  double smin = (aw < 0 ? aw : 0.0) + (be < 0 ? be : 0.0) + t3, smax = (aw > 0 ? aw : 0.0) + (be > 0 ? be : 0.0) + t3;
+  const double pad = 1e-3 * (smax - smin) + 1e-6;
+  smin -= pad;
+  smax += pad;
+  const double th = f.p.theta_h, tm = f.p.theta_m;
+  const double lo[kGrp] = {smin, tm > smin ? tm : smin, th > smin ? th : smin, smin};
+  const double hi[kGrp] = {tm < smax ? tm : smax, th < smax ? th : smax, smax, smax};
+  for (int q = 0; q < kGrp; ++q) {
+    g.bin_lo[q] = (float)lo[q];
+    g.bin_inv[q] = hi[q] > lo[q] ? (float)(kNBin / (hi[q] - lo[q])) : 0.f;
+  }
+  {
+    const double u8 = 8.0 * ((double)f.S * f.p.propagation_ratio);
+    int wmax = 0;
+    for (int k = 0; k < 3; ++k) wmax = f.p.bits[k] > wmax ? f.p.bits[k] : wmax;
+    g.hist_fb = (f.mode_select == 1 && !(f.p.flags & RTKV_NO_FALLBACK) && !(u8 >= (double)wmax)) ? 1 : 0;
+  }
+  if (!zeroed) RTKV_HIP_CHECK(hipMemsetAsync(ws, 0, select_fast_zero_bytes(), st));  // else K1 cleared them
+  const int G = (int)((f.S + kST - 1) / kST);
+  int rc;
+  if (f.S <= 16 * kST) rc = f.T2 ? launch_f1_dt<16, true>(g, G, st) : launch_f1_dt<16, false>(g, G, st);
+  else rc = f.T2 ? launch_f1_dt<32, true>(g, G, st) : launch_f1_dt<32, false>(g, G, st);
+  if (rc) return rc;
+  hipLaunchKernelGGL(fsel_compact_kernel, dim3(G), dim3(kST), 0, st, g);
+  RTKV_HIP_CHECK(hipGetLastError());
+  return RTKV_OK;
+}
+
+}  // namespace rtkv
