@@ -26,7 +26,7 @@
 //     group) published with sc1 stores + a flag; each workgroup sums its predecessors' aggregates
 //     (decoupled look-back: every aggregate is published before any is awaited, and workgroups are
 //     dispatched in index order, so the wait always ends), then ranks its tokens with block scans:
-//     mask, kept_index, row_offset.  The last workgroup writes the row statistics.
+//     mask, kept_index, row_offset; its kept-token statistics are added atomically.
 //
 // Cross-workgroup hand-offs (MI355X_MICROARCH.md "Valid forms"): sc1 stores of every handed-off
 // word, every storing wave drains with s_waitcnt vmcnt(0), one lane signals (agent-scope atomic add,
@@ -63,10 +63,7 @@ struct FastPartial {               // per F1 workgroup, sc1 stores
 struct FastAgg {                   // per F2 workgroup, sc1 stores
   uint64_t sure3;                  // 3 x 16-bit: kept tokens per class, ties at T excluded
   uint64_t ties4;                  // 4 x 16-bit: tokens at each partial group's T
-  double ksum;                     // Σ scores of the kept tokens (ties included)
-  double m2;                       // Σ (s - mean)^2
-  uint64_t kept3;                  // 3 x 16-bit: kept tokens per class, ties included
-  uint64_t pad[3];
+  uint64_t pad[6];
 };
 struct FastSel {                   // F1's last workgroup -> F2
   int32_t mode[kGrp];
@@ -79,7 +76,7 @@ struct FastSel {                   // F1's last workgroup -> F2
   int64_t ccount[3];
 };
 struct FastHead {                  // zeroed before F1 (K1 or a memset)
-  uint32_t done1, done2;
+  uint32_t done1, pad0;
   uint32_t smin_c, smax;           // score keys: ~min and max (atomic max from zero)
   uint32_t pad[60];
   uint32_t flag[kMaxG];            // F2 aggregates published
@@ -436,6 +433,20 @@ __device__ __forceinline__ void select_thresholds(const FastArgs& g, uint32_t* h
   }
   K2_PROBE(2);
   if (t != 0) return;
+  // statistics known here; F2's workgroups add the kept-token ones (stats zeroed before F1)
+  rtkv_layer_stats* hs = a.stats;
+  rtkv_batch_stats* bs = reinterpret_cast<rtkv_batch_stats*>(hs + 1);
+  for (int q = 0; q < 3; ++q) bs->class_count[q] = ccount[q];
+  bs->fallback = fallback ? 1 : 0;
+  hs->score_sum = ssum;
+  hs->score_min = key_score(~ld_sc1(&g.L.head->smin_c));
+  hs->score_max = key_score(ld_sc1(&g.L.head->smax));
+  int flags = 0;
+  if (a.kv_dtype == RTKV_F16)
+    for (int q = 0; q < 3; ++q)
+      if (ccount[q] > 0 && a.p.bits[q] >= 16) flags |= RTKV_FLAG_F16_QMAX_OVERFLOW;
+  hs->error_flags = flags;
+  hs->B = 1;
   FastSel* fs = g.L.sel;
   for (int q = 0; q < kGrp; ++q) {
     fs->mode[q] = mode[q];
@@ -572,7 +583,6 @@ __global__ __launch_bounds__(kST) void fsel_compact_kernel(FastArgs g) {
   __shared__ uint64_t s_r[2][kSW];
   __shared__ double s_d[2][kSW];
   __shared__ uint64_t s_base[3];
-  __shared__ int s_flag;
   const int t = threadIdx.x, lane = t & (kWave - 1), wid = t / kWave;
   const int S = (int)a.S;
   const int blk = blockIdx.x;
@@ -664,7 +674,7 @@ __global__ __launch_bounds__(kST) void fsel_compact_kernel(FastArgs g) {
       }
     }
   }
-  // ---- statistics partials: Σ kept scores, Σ (s - mean)^2, kept per class
+  // ---- statistics: Σ kept scores, Σ (s - mean)^2 and the kept-token counts, added per workgroup
   const double d = (double)s - fs.mean;
   const double ks = wave_sum(kept ? (double)s : 0.0), m2 = wave_sum(valid ? d * d : 0.0);
   if (lane == 0) { s_d[0][wid] = ks; s_d[1][wid] = m2; }
@@ -674,64 +684,27 @@ __global__ __launch_bounds__(kST) void fsel_compact_kernel(FastArgs g) {
 #pragma unroll
     for (int o = kSW / 2; o > 0; o >>= 1) { x += __shfl_xor(x, o, kWave); y += __shfl_xor(y, o, kWave); }
     if (lane == 0) {
-      st_sc1(&g.L.agg[blk].ksum, x);
-      st_sc1(&g.L.agg[blk].m2, y);
-      st_sc1(&g.L.agg[blk].kept3, kept_tot);
+      rtkv_layer_stats* hs = a.stats;
+      rtkv_batch_stats* bs = reinterpret_cast<rtkv_batch_stats*>(hs + 1);
+      unsigned long long n = 0, units = 0, bytes = 0;
+      for (int q = 0; q < 3; ++q) {
+        const unsigned long long nq = fld(kept_tot, q);
+        if (nq) atomicAdd((unsigned long long*)&bs->kept_class[q], nq);
+        n += nq;
+        units += nq * (unsigned long long)a.p.bits[q];
+        bytes += nq * (unsigned long long)rb[q];
+      }
+      if (n) {
+        atomicAdd((unsigned long long*)&bs->kept, n);
+        atomicAdd((unsigned long long*)&bs->cost_units, units);
+        atomicAdd((unsigned long long*)&bs->packed_bytes, bytes);
+        atomicAdd((unsigned long long*)&hs->max_kept, n);
+        atomicAdd((unsigned long long*)&hs->total_packed_bytes, bytes);
+        atomicAdd(&bs->kept_score_sum, x);
+      }
+      atomicAdd(&hs->score_m2, y);
     }
   }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (t == 0) {
-    const uint32_t old = __hip_atomic_fetch_add(&g.L.head->done2, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    s_flag = (old + 1 == gridDim.x);
-  }
-  __syncthreads();
-  if (!s_flag || wid != 0) return;
-  // ---- the last workgroup: row statistics (the fields select.hip's C1/C2 write)
-  const int G = gridDim.x;
-  double ksum = 0.0, m2s = 0.0;
-  uint64_t kt = 0;
-  if (lane < G) {
-    ksum = ld_sc1(&g.L.agg[lane].ksum);
-    m2s = ld_sc1(&g.L.agg[lane].m2);
-    kt = ld_sc1(&g.L.agg[lane].kept3);
-  }
-#pragma unroll
-  for (int o = kWave / 2; o > 0; o >>= 1) {
-    ksum += __shfl_xor(ksum, o, kWave);
-    m2s += __shfl_xor(m2s, o, kWave);
-    kt += __shfl_xor(kt, o, kWave);
-  }
-  if (lane != 0) return;
-  rtkv_layer_stats* hs = a.stats;
-  rtkv_batch_stats* bs = reinterpret_cast<rtkv_batch_stats*>(hs + 1);
-  int64_t kept_n = 0, units = 0, pbytes = 0;
-  for (int q = 0; q < 3; ++q) {
-    const int64_t n = fld(kt, q);
-    bs->class_count[q] = fs.ccount[q];
-    bs->kept_class[q] = n;
-    kept_n += n;
-    units += n * a.p.bits[q];
-    pbytes += n * rb[q];
-  }
-  bs->kept = kept_n;
-  bs->cost_units = units;
-  bs->packed_bytes = pbytes;
-  bs->fallback = fallback ? 1 : 0;
-  bs->reserved = 0;
-  bs->kept_score_sum = ksum;
-  hs->max_kept = kept_n;
-  hs->total_packed_bytes = pbytes;
-  hs->score_sum = fs.ssum;
-  hs->score_m2 = m2s;
-  hs->score_min = key_score(~ld_sc1(&g.L.head->smin_c));
-  hs->score_max = key_score(ld_sc1(&g.L.head->smax));
-  int flags = 0;
-  if (a.kv_dtype == RTKV_F16)
-    for (int q = 0; q < 3; ++q)
-      if (fs.ccount[q] > 0 && a.p.bits[q] >= 16) flags |= RTKV_FLAG_F16_QMAX_OVERFLOW;
-  hs->error_flags = flags;
-  hs->B = 1;
 }
 
 }  // namespace
@@ -810,7 +783,10 @@ int launch_select_fast(const FinalizeArgs& f, void* ws, bool zeroed, hipStream_t
     for (int k = 0; k < 3; ++k) wmax = f.p.bits[k] > wmax ? f.p.bits[k] : wmax;
     g.hist_fb = (f.mode_select == 1 && !(f.p.flags & RTKV_NO_FALLBACK) && !(u8 >= (double)wmax)) ? 1 : 0;
   }
-  if (!zeroed) RTKV_HIP_CHECK(hipMemsetAsync(ws, 0, select_fast_zero_bytes(), st));  // else K1 cleared them
+  if (!zeroed) {  // else K1 cleared them
+    RTKV_HIP_CHECK(hipMemsetAsync(ws, 0, select_fast_zero_bytes(), st));
+    RTKV_HIP_CHECK(hipMemsetAsync(f.stats, 0, rtkv_stats_bytes(f.B), st));
+  }
   const int G = (int)((f.S + kST - 1) / kST);
   int rc;
   if (f.S <= 16 * kST) rc = f.T2 ? launch_f1_dt<16, true>(g, G, st) : launch_f1_dt<16, false>(g, G, st);
