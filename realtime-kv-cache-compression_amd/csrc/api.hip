@@ -171,8 +171,9 @@ int rtkv_select_tokens(const float* scores_dev, const uint8_t* labels_dev, int64
   return launch_select(a, ws.sel, false, (hipStream_t)stream);
 }
 
-int rtkv_quantize_rows(const rtkv_kv_desc* kv, const uint8_t* labels_dev, const int32_t* kept_index_dev,
-                       const rtkv_layer_params* p, const rtkv_layer_out* out, void* stream) {
+static int quantize_rows_impl(const rtkv_kv_desc* kv, const uint8_t* labels_dev, const int32_t* kept_index_dev,
+                              const rtkv_layer_params* p, const rtkv_layer_out* out, void* stream,
+                              const uint8_t* row_label) {
   int rc = check_params(p);
   if (rc) return rc;
   RTKV_REQUIRE(kv && out, "null descriptor");
@@ -181,12 +182,18 @@ int rtkv_quantize_rows(const rtkv_kv_desc* kv, const uint8_t* labels_dev, const 
   q.kv = *kv;
   q.labels = labels_dev;
   q.kept_index = kept_index_dev;
+  q.row_label = row_label;
   q.stats = out->stats_dev;
   for (int g = 0; g < 3; ++g) q.bits[g] = p->bits[g];
   q.out = *out;
   if (!(p->flags & RTKV_EMIT_DEQUANT)) { q.out.k_out_dev = nullptr; q.out.v_out_dev = nullptr; }
   if (!(p->flags & RTKV_EMIT_PACKED)) { q.out.packed_k_dev = nullptr; q.out.packed_v_dev = nullptr; }
   return launch_quant(q, (hipStream_t)stream);
+}
+
+int rtkv_quantize_rows(const rtkv_kv_desc* kv, const uint8_t* labels_dev, const int32_t* kept_index_dev,
+                       const rtkv_layer_params* p, const rtkv_layer_out* out, void* stream) {
+  return quantize_rows_impl(kv, labels_dev, kept_index_dev, p, out, stream, nullptr);
 }
 
 // The fused layer: K1 (W aggregation, or K1' on MFMA when q != null) → K2 → K4.
@@ -259,10 +266,12 @@ static int compress_layer_impl(const rtkv_kv_desc* kv, const rtkv_attn_desc* w, 
   a.mode_scores = 1;
   a.mode_labels = 1;
   a.mode_select = (p->flags & RTKV_NO_SELECTION) ? 2 : 1;
+  const bool row_labels = select_fast_eligible(a);  // the fast path also writes each kept row's class
+  a.row_label = row_labels ? ws.labels : nullptr;
   rc = launch_select(a, ws.sel, true, st);
   if (rc) return rc;
   if ((rc = mark(2))) return rc;
-  rc = rtkv_quantize_rows(kv, out->labels_dev, out->kept_index_dev, p, out, stream);
+  rc = quantize_rows_impl(kv, out->labels_dev, out->kept_index_dev, p, out, stream, row_labels ? ws.labels : nullptr);
   if (rc) return rc;
   return mark(3);
 }

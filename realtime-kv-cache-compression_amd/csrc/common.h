@@ -218,6 +218,7 @@ struct FinalizeArgs {
   rtkv_layer_stats* stats;
   int mode_scores, mode_labels, mode_select;
   int fb_group;            // 1: select the top-10% fallback group alongside (set by launch_select)
+  uint8_t* row_label;      // optional [B][cap] class of each kept row, for K4 (fast path writes it)
 };
 // K2 pipeline (select.hip).  sel_ws: select_workspace_bytes(B, S) bytes; `zeroed` = its first
 // select_zero_bytes(B) bytes and the stats are already zero (K1 clears them in rtkv_compress_layer).
@@ -236,6 +237,7 @@ struct QuantArgs {
   rtkv_kv_desc kv;
   const uint8_t* labels;          // [B,S]
   const int32_t* kept_index;      // [B,cap] or null (all tokens)
+  const uint8_t* row_label;       // [B,cap] class of each kept row, or null (then labels[kept_index])
   const rtkv_layer_stats* stats;  // kept counts / max_kept (null when kept_index is null)
   int32_t bits[3];
   rtkv_layer_out out;

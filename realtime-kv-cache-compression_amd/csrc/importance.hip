@@ -192,7 +192,10 @@ __global__ __launch_bounds__(256) void aggregation_vec_kernel(const typename Dt<
 //   y_m[l]   = x[16m + l] + x[16m + 8 + l]          (chunks 2m, 2m+1: one 16-wide Vectorized<Half>)
 //   part_k   = Σ_j y_{4j+k} (sequential), tail m >= 4·nq into part 0, then part0+part1+part2+part3
 //   A        = Σ_l lanes[l] (l = 0..7, sequential)                       (vectorized_inner_sum, ILP 4)
-template <int DT, int CPR>
+// HB heads per load batch; PF: the next batch's loads are issued before the current batch is
+// summed (two batches in flight, so every wave keeps streaming).  The per-element addition order is
+// the same for every (HB, PF): heads in order, the cascade step after every 16th head.
+template <int DT, int CPR, int HB = 16, bool PF = false>
 __global__ __launch_bounds__(256) void aggregation_shfl_kernel(const typename Dt<DT>::S* __restrict__ W, int H,
                                                                int64_t S, int64_t sb, int64_t sh, int64_t ss,
                                                                int64_t lim, float* __restrict__ A, AggExtras ex) {
@@ -214,28 +217,55 @@ __global__ __launch_bounds__(256) void aggregation_shfl_kernel(const typename Dt
   float a0[8], a1[8], a2[8], a3[8];
 #pragma unroll
   for (int k = 0; k < 8; ++k) a0[k] = a1[k] = a2[k] = a3[k] = 0.f;
-  int h = 0;
-  while (h + 16 <= H) {
-    V v[16];
+  // multi_row_sum's cascade: after every 16th head a1 += a0, every 256th a2 += a1, every 4096th a3 += a2
+  auto cascade = [&](int hh) {
+    if ((hh & 15) == 0) {
 #pragma unroll
-    for (int j = 0; j < 16; ++j) v[j] = load16_nt(base + (int64_t)(h + j) * sh);
+      for (int k = 0; k < 8; ++k) { a1[k] += a0[k]; a0[k] = 0.f; }
+      if ((hh & (15 << 4)) == 0) {
 #pragma unroll
-    for (int j = 0; j < 16; ++j) {
+        for (int k = 0; k < 8; ++k) { a2[k] += a1[k]; a1[k] = 0.f; }
+        if ((hh & (15 << 8)) == 0) {
+#pragma unroll
+          for (int k = 0; k < 8; ++k) { a3[k] += a2[k]; a2[k] = 0.f; }
+        }
+      }
+    }
+  };
+  auto load_batch = [&](V (&v)[HB], int h0) {
+#pragma unroll
+    for (int j = 0; j < HB; ++j) v[j] = load16_nt(base + (int64_t)(h0 + j) * sh);
+  };
+  auto consume = [&](const V (&v)[HB], int h0) {
+#pragma unroll
+    for (int j = 0; j < HB; ++j) {
       float x[8];
       unpack_vec<DT, 8>(v[j], x);
 #pragma unroll
       for (int k = 0; k < 8; ++k) a0[k] += x[k];
+      if (((h0 + j + 1) & 15) == 0) cascade(h0 + j + 1);
     }
-    h += 16;
-#pragma unroll
-    for (int k = 0; k < 8; ++k) { a1[k] += a0[k]; a0[k] = 0.f; }
-    if ((h & (15 << 4)) == 0) {
-#pragma unroll
-      for (int k = 0; k < 8; ++k) { a2[k] += a1[k]; a1[k] = 0.f; }
-      if ((h & (15 << 8)) == 0) {
-#pragma unroll
-        for (int k = 0; k < 8; ++k) { a3[k] += a2[k]; a2[k] = 0.f; }
-      }
+  };
+  int h = 0;
+  if constexpr (!PF) {
+    while (h + HB <= H) {
+      V v[HB];
+      load_batch(v, h);
+      consume(v, h);
+      h += HB;
+    }
+  } else if (H >= HB) {
+    V v0[HB], v1[HB];
+    load_batch(v0, 0);
+    while (true) {
+      if (h + 2 * HB <= H) load_batch(v1, h + HB);
+      consume(v0, h);
+      h += HB;
+      if (h + HB > H) break;
+      if (h + 2 * HB <= H) load_batch(v0, h + HB);
+      consume(v1, h);
+      h += HB;
+      if (h + HB > H) break;
     }
   }
   for (; h < H; ++h) {
@@ -243,6 +273,7 @@ __global__ __launch_bounds__(256) void aggregation_shfl_kernel(const typename Dt
     unpack_vec<DT, 8>(*reinterpret_cast<const V*>(base + (int64_t)h * sh), x);
 #pragma unroll
     for (int k = 0; k < 8; ++k) a0[k] += x[k];
+    if (((h + 1) & 15) == 0) cascade(h + 1);
   }
   const float fH = (float)H;
   float m[8];  // head means of columns ch*8 .. ch*8+7, rounded to the dtype

@@ -14,6 +14,7 @@
 // the dtype after each op (bit-identical to PyTorch CPU).  8 codes of w bits pack into exactly w
 // bytes, so each lane writes its chunk's codes with one store at byte offset c*w.
 #pragma once
+#include <cstdlib>
 #include <type_traits>
 
 #include "common.h"
@@ -261,7 +262,7 @@ __global__ __launch_bounds__(256, 2) void quant_rows_kernel(QuantArgs a) {
     const int b = rr / R, r = rr - b * R;
     const int kept_b = a.kept_index ? (int)bst[b].kept : S;
     int i = (r < kept_b) ? (a.kept_index ? a.kept_index[(int64_t)b * cap + r] : r) : 0;
-    int lab = (r < kept_b) ? (int)a.labels[(int64_t)b * S + i] : 0;
+    int lab = (r < kept_b) ? (a.row_label ? (int)a.row_label[(int64_t)b * cap + r] : (int)a.labels[(int64_t)b * S + i]) : 0;
     i = __builtin_amdgcn_readfirstlane(i);
     lab = __builtin_amdgcn_readfirstlane(lab);
     if (shard) {  // another rank's token, or a padding row this rank does not own
@@ -458,7 +459,11 @@ int launch_quant_dt(const QuantArgs& a, hipStream_t st) {
   const int64_t R = a.kept_index ? (a.out.row_capacity < Sg ? a.out.row_capacity : Sg) : Sg;
   const int64_t tasks = 2 * kv.B * R;
   int64_t blocks = (tasks + 3) / 4;
-  if (blocks > 4096) blocks = 4096;
+  static const int64_t cap_blocks = [] {  // RTKV_K4_BLOCKS: experiment knob; default one wave per task (measured best: 4096 blocks 93 us, 8192 90.5 us at cfg3)
+    const char* e = getenv("RTKV_K4_BLOCKS");
+    return e ? (int64_t)atol(e) : (int64_t)1 << 20;
+  }();
+  if (blocks > cap_blocks) blocks = cap_blocks;
   if (blocks < 1) blocks = 1;
   const int esz = Dt<DT>::kBytes;
   auto al16 = [](const void* p) { return p == nullptr || ((uintptr_t)p % 16) == 0; };

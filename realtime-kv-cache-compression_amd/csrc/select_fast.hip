@@ -669,6 +669,7 @@ __global__ __launch_bounds__(kST) void fsel_compact_kernel(FastArgs g) {
       const int64_t row = (int64_t)fld(rank3, 0) + fld(rank3, 1) + fld(rank3, 2);
       if (row < a.row_capacity) {
         a.kept_index[row] = i;
+        if (a.row_label) a.row_label[row] = (uint8_t)l;
         if (a.row_offset)
           a.row_offset[row] = (int64_t)fld(rank3, 0) * rb[0] + (int64_t)fld(rank3, 1) * rb[1] + (int64_t)fld(rank3, 2) * rb[2];
       }
