@@ -54,6 +54,9 @@ def parse():
                          "(Q + prompt keys + row LSE, K1' on MFMA)")
     ap.add_argument("--sharded", action="store_true",
                     help="use the sequence-sharded driver even at world size 1 (plumbing check)")
+    ap.add_argument("--no-overlap", action="store_true",
+                    help="sharded driver: exchange every layer's packed KV after the last layer instead of "
+                         "overlapping each layer's exchange with the following layers")
     return ap.parse_args()
 
 
@@ -196,7 +199,7 @@ class ShardedJob:
                                           num_hidden_layers=args.layers)
         self.bits = (2, 4, 8)
         self.comp = ShardedPrefillCompressor(self.cfg, emit_packed=not args.no_packed, emit_dequant=True,
-                                             device=device)
+                                             device=device, overlap=not args.no_overlap)
         gen = torch.Generator(device=device)
         gen.manual_seed(1234 + 7919 * rank)
         self.inputs, self.params = [], []
@@ -369,8 +372,11 @@ def main():
         }
         if sharded:
             line["exchange"] = {"received_bytes_per_rank_per_step": job.exchanged_bytes(),
-                                "kind": "grouped RCCL send/recv (one group per layer, enqueued back to back) of packed "
-                                        "K/V codes + scale/zp (exact byte ranges, all peers at once)",
+                                "kind": ("grouped RCCL send/recv per layer of packed K/V codes + scale/zp (exact byte "
+                                         "ranges, all peers at once), " +
+                                         ("all after the last layer" if args.no_overlap else
+                                          "each issued one layer later on its own communicator, overlapping "
+                                          "the following layers' compute")),
                                 "per_layer_collective": "RCCL all-gather of A (4 B/token)"}
         if not sharded:
             per_launch_ms = k_ms[2] / (reps * args.layers)

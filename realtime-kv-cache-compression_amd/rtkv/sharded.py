@@ -15,12 +15,14 @@ tokens (rank j owns tokens [j*S_local, (j+1)*S_local)), and each layer runs as
 
 The selection is global (the reference's min-max normalisation and budget are over the whole
 sequence, token_importance.py:71-83, selective_propagation.py:96), so step 2 is the only exchange
-inside a layer.  After the last layer, ``exchange()`` does the one exchange of the compressed KV:
-a single host read of every layer's rank bounds, then one grouped point-to-point launch per layer
-(all enqueued back to back, waited once) in which each rank sends its byte ranges of the packed K/V
-codes and its scale/zero-point rows to every peer
-(xGMI links are point-to-point, so every rank streams to all 7 peers at once instead of hopping
-round a ring).  Every rank then holds every layer's packed KV byte-identical to the single-GPU
+inside a layer.  The compressed KV of a layer is exchanged by one grouped point-to-point launch in
+which each rank sends its byte ranges of the packed K/V codes and its scale/zero-point rows to every
+peer (xGMI links are point-to-point, so every rank streams to all 7 peers at once instead of
+hopping round a ring).  With ``overlap`` (the default) that launch is issued ``lag`` layers later,
+on a communicator of its own (so it never queues in front of a later layer's all-gather of A), as
+soon as the layer's rank bounds have reached the host through a non-blocking copy: the exchange of
+layer l streams while layers l+1.. compute.  ``exchange()`` issues what is left and waits for all of
+it.  Every rank then holds every layer's packed KV byte-identical to the single-GPU
 ``rtkv_compress_layer`` output.
 
 The device stages are injected (``stages``): ``HipShardStages`` calls librtkv.so; the CPU test
@@ -92,6 +94,8 @@ class ShardBuffers:
         self.k_local = torch.empty(B, S_local, F, dtype=dtype, device=dev) if emit_dequant else None
         self.v_local = torch.empty(B, S_local, F, dtype=dtype, device=dev) if emit_dequant else None
         self.ranges = torch.zeros(B, world + 1, 2, dtype=torch.int64, device=dev)
+        # host copy of the bounds for the overlapped exchange (pinned, reused every step)
+        self.ranges_host = torch.zeros(B, world + 1, 2, dtype=torch.int64, pin_memory=dev.type == "cuda")
 
     def out_struct(self) -> L.LayerOut:
         o = self.g.out_struct()
@@ -127,7 +131,7 @@ class ShardedPrefillCompressor:
     rank's own token chunk (it returns the rank's dequantized rows)."""
 
     def __init__(self, config, group=None, stages=None, emit_packed: bool = True, emit_dequant: bool = True,
-                 device=None):
+                 device=None, overlap: bool = True, lag: int = 2):
         if not dist.is_initialized():
             raise RuntimeError("ShardedPrefillCompressor needs torch.distributed to be initialised")
         self.config = config
@@ -144,6 +148,16 @@ class ShardedPrefillCompressor:
         self._bufs = {}
         self._pending: List[int] = []
         self._A = {}
+        # overlapped exchange: its own communicator (own stream), layers queued with their bounds copy
+        self.overlap = bool(overlap) and self.emit_packed
+        self.lag = max(0, int(lag))
+        self.xgroup = self.group
+        if self.overlap:
+            ranks = dist.get_process_group_ranks(self.group) if self.group is not None else list(range(self.world))
+            self.xgroup = dist.new_group(ranks=ranks)
+        self._queued = []   # (layer_idx, host ranges, event) not yet exchanged
+        self._issued = []   # ShardLayer whose exchange is in flight
+        self._works = []
 
     def _peer_rank(self, j: int) -> int:
         return dist.get_global_rank(self.group, j) if self.group is not None else j
@@ -193,12 +207,73 @@ class ShardedPrefillCompressor:
         self.stages.finalize(A_glob, L.TORCH_DTYPE_CODE[W.dtype], p, bufs)
         self.stages.ranges(bufs, self.world)
         self.stages.quantize(K, V, layout, row0, self.rank, self.world, p, bufs)
-        self._pending.append(layer_idx)
+        if self.overlap:
+            self._queue(layer_idx, bufs)
+            self._issue(keep=self.lag)
+        else:
+            self._pending.append(layer_idx)
         return bufs
 
+    # ------------------------------------------------------------------ overlapped exchange
+    def _queue(self, layer_idx: int, bufs: ShardBuffers):
+        host = bufs.ranges_host
+        if self.device.type == "cuda":
+            host.copy_(bufs.ranges, non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record()
+        else:
+            host.copy_(bufs.ranges)
+            ev = None
+        self._queued.append((layer_idx, host, ev))
+
+    def _issue(self, keep: int):
+        # every rank issues the same layers in the same order (count-based, never completion-based),
+        # as grouped point-to-point launches require
+        while len(self._queued) > keep:
+            layer_idx, host, ev = self._queued.pop(0)
+            if ev is not None:
+                ev.synchronize()  # that layer's bounds are on the host (a layer or more ago)
+            sl = ShardLayer(layer_idx, self._bufs[layer_idx], host.clone())  # a snapshot: the pinned buffer is reused
+            self._works.extend(self._send_recv(sl, self.xgroup))
+            self._issued.append(sl)
+
+    def _send_recv(self, sl: ShardLayer, group):
+        """One grouped launch: this rank's packed K/V byte ranges and scale/zero-point rows of the layer
+        to every peer, the peers' ranges from them."""
+        ops = []
+        me = self.rank
+        g = sl.bufs.g
+        cap = sl.bufs.S_total
+        sz = g.scale_zp.view(-1)
+        for b in range(sl.bufs.B):
+            r = sl.ranges[b]
+            spans = []
+            for j in range(self.world):
+                b0, b1 = int(r[j, 1]), int(r[j + 1, 1])
+                r0, r1 = int(r[j, 0]), int(r[j + 1, 0])
+                spans.append(((b0, b1), ((b * cap + r0) * 4, (b * cap + r1) * 4)))
+            for j in range(self.world):
+                if j == me:
+                    continue
+                peer = self._peer_rank(j)
+                for (lo, hi), buf in ((spans[me][0], g.packed_k), (spans[me][0], g.packed_v), (spans[me][1], sz)):
+                    if hi > lo:
+                        ops.append(dist.P2POp(dist.isend, buf[lo:hi], peer, group))
+                for (lo, hi), buf in ((spans[j][0], g.packed_k), (spans[j][0], g.packed_v), (spans[j][1], sz)):
+                    if hi > lo:
+                        ops.append(dist.P2POp(dist.irecv, buf[lo:hi], peer, group))
+        return dist.batch_isend_irecv(ops) if ops else []
+
     def exchange(self) -> List[ShardLayer]:
-        """One host read of every pending layer's rank bounds, then one grouped P2P launch per layer: each rank's
-        packed K/V byte ranges and scale/zero-point rows go to every peer."""
+        """Finish the exchange of every layer enqueued so far and return their host views.  Overlapped
+        mode: issue the layers still queued, wait for everything in flight.  Otherwise: one host read
+        of every pending layer's rank bounds, then one grouped P2P launch per layer, waited once."""
+        if self.overlap:
+            self._issue(keep=0)
+            for w in self._works:
+                w.wait()
+            out, self._issued, self._works = self._issued, [], []
+            return out
         layers = list(self._pending)
         self._pending = []
         if not layers:
@@ -208,33 +283,8 @@ class ShardedPrefillCompressor:
         if self.world == 1 or not self.emit_packed:
             return out
         works = []
-        me = self.rank
-        for sl in out:
-            ops = []
-            g = sl.bufs.g
-            cap = sl.bufs.S_total
-            sz = g.scale_zp.view(-1)
-            for b in range(sl.bufs.B):
-                r = sl.ranges[b]
-                spans = []
-                for j in range(self.world):
-                    b0, b1 = int(r[j, 1]), int(r[j + 1, 1])
-                    r0, r1 = int(r[j, 0]), int(r[j + 1, 0])
-                    spans.append(((b0, b1), ((b * cap + r0) * 4, (b * cap + r1) * 4)))
-                for j in range(self.world):
-                    if j == me:
-                        continue
-                    peer = self._peer_rank(j)
-                    for (lo, hi), buf in ((spans[me][0], g.packed_k), (spans[me][0], g.packed_v),
-                                          (spans[me][1], sz)):
-                        if hi > lo:
-                            ops.append(dist.P2POp(dist.isend, buf[lo:hi], peer, self.group))
-                    for (lo, hi), buf in ((spans[j][0], g.packed_k), (spans[j][0], g.packed_v),
-                                          (spans[j][1], sz)):
-                        if hi > lo:
-                            ops.append(dist.P2POp(dist.irecv, buf[lo:hi], peer, self.group))
-            if ops:  # one grouped launch per layer: every peer pair of the layer at once
-                works.extend(dist.batch_isend_irecv(ops))
+        for sl in out:  # one grouped launch per layer: every peer pair of the layer at once
+            works.extend(self._send_recv(sl, self.group))
         for w in works:
             w.wait()
         return out

@@ -39,7 +39,7 @@ def _tensor(a, dtype):
     return torch.from_numpy(np.ascontiguousarray(a).view(np.int16)).view(getattr(torch, dtype))
 
 
-def _worker(rank, world, port, S_total, H, D, dtype, layers, q):
+def _worker(rank, world, port, S_total, H, D, dtype, layers, q, overlap=True):
     try:
         for p in (os.path.join(HERE, ".."), os.path.join(HERE, "..", "realtime-kv-cache-compression_amd"),
                   os.path.join(HERE, "..", "oracle"), os.path.join(HERE, "golden"), HERE):
@@ -55,7 +55,7 @@ def _worker(rank, world, port, S_total, H, D, dtype, layers, q):
                                      high_precision_bits=8, medium_precision_bits=4, low_precision_bits=2,
                                      early_layer_ratio=0.8, middle_layer_ratio=0.6, later_layer_ratio=0.4,
                                      num_hidden_layers=layers)
-        comp = ShardedPrefillCompressor(cfg, stages=OracleShardStages(), device="cpu")
+        comp = ShardedPrefillCompressor(cfg, stages=OracleShardStages(), device="cpu", overlap=overlap)
         S_local = S_total // world
         row0 = rank * S_local
         full = {}
@@ -95,13 +95,15 @@ def _worker(rank, world, port, S_total, H, D, dtype, layers, q):
         q.put((rank, "".join(traceback.format_exception(type(e), e, e.__traceback__))))
 
 
-@pytest.mark.parametrize("dtype", ["float16", "float32"])
-def test_sharded_prefill_world2_matches_single_process(dtype):
+@pytest.mark.parametrize("dtype,overlap", [("float16", True), ("float32", True), ("float16", False)])
+def test_sharded_prefill_world2_matches_single_process(dtype, overlap):
+    """overlap: each layer's exchange issued one layer later on its own communicator (default);
+    otherwise all layers exchanged at the end."""
     world, S_total, H, D, layers = 2, 1024, 4, 32, 3
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, S_total, H, D, dtype, layers, q))
+    procs = [ctx.Process(target=_worker, args=(r, world, port, S_total, H, D, dtype, layers, q, overlap))
              for r in range(world)]
     for p in procs:
         p.start()
