@@ -340,6 +340,23 @@ int rtkv_unpack_dequant(const uint8_t* packed_dev, const int64_t* row_offset_dev
                         int64_t H, int64_t D, int dtype, const int32_t bits[3], void* out_dev,
                         int64_t o_stride_b, int64_t o_stride_s, int64_t o_stride_h, void* stream);
 
+/* Decode attention over one layer's PACKED KV: for every batch row b and query head
+ * h, out[b,h,:] = softmax_j(q[b,h]·K'[b,j,h/G]ᵀ·scale)·V'[b,j,h/G] over the kept rows j < rows[b],
+ * where K'/V' are decoded from the packed codes on the fly, element for element the dequantized
+ * rows rtkv_compress_layer writes.  Replaces the reference's attention over the dequantized cache
+ * (modified_llama.py:140-142, 165-166) without materialising K'/V'.  Arguments as
+ * rtkv_unpack_dequant (H = Hkv kv heads of head_dim D, F = Hkv·D a multiple of 512, at most 5120;
+ * packed field widths 2/4/8/16), plus q [B, Hq, D] in the K/V dtype (Hq a multiple of Hkv: GQA),
+ * scale (1/sqrt(D) in the reference, modified_llama.py:89) and out [B, Hq, D] fp32.  Workspace:
+ * rtkv_decode_workspace_size(B, Hq, Hkv, D, row_capacity) bytes. */
+size_t rtkv_decode_workspace_size(int64_t B, int64_t Hq, int64_t Hkv, int64_t D, int64_t row_capacity);
+int rtkv_decode_attention_packed(const uint8_t* packed_k_dev, const uint8_t* packed_v_dev,
+                                 const int64_t* row_offset_dev, const float* scale_zp_dev,
+                                 const int32_t* kept_index_dev, const uint8_t* labels_dev, int64_t B, int64_t S,
+                                 int64_t row_capacity, const int64_t* rows_dev, int64_t Hkv, int64_t D, int dtype,
+                                 const int32_t bits[3], const void* q_dev, int64_t Hq, float scale,
+                                 float* out_dev, void* workspace_dev, size_t workspace_bytes, void* stream);
+
 /* Copy the kept rows of a row-major tensor (row r of batch b = src row kept_index[b*cap + r]), zero
  * rows for r in [kept_b, S'_max), rows of row_bytes bytes, into dst (batch stride dst_stride_b bytes,
  * or S'_max*row_bytes when -1).  The pure gather of apply_token_selection (selective_propagation.py

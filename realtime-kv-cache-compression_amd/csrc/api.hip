@@ -400,6 +400,23 @@ int rtkv_unpack_dequant(const uint8_t* packed_dev, const int64_t* row_offset_dev
                        rows_dev, H, D, dtype, bits, out_dev, o_stride_b, o_stride_s, o_stride_h, (hipStream_t)stream);
 }
 
+size_t rtkv_decode_workspace_size(int64_t B, int64_t Hq, int64_t Hkv, int64_t D, int64_t row_capacity) {
+  if (B < 1 || Hkv < 1 || Hq < Hkv || D < 1 || row_capacity < 1) return 0;
+  return decode_workspace_bytes(B, Hq, Hkv, D, row_capacity);
+}
+
+int rtkv_decode_attention_packed(const uint8_t* packed_k_dev, const uint8_t* packed_v_dev, const int64_t* row_offset_dev,
+                                 const float* scale_zp_dev, const int32_t* kept_index_dev, const uint8_t* labels_dev,
+                                 int64_t B, int64_t S, int64_t row_capacity, const int64_t* rows_dev, int64_t Hkv,
+                                 int64_t D, int dtype, const int32_t bits[3], const void* q_dev, int64_t Hq,
+                                 float scale, float* out_dev, void* workspace_dev, size_t workspace_bytes,
+                                 void* stream) {
+  RTKV_REQUIRE(bits != nullptr, "null bits");
+  return launch_decode(packed_k_dev, packed_v_dev, row_offset_dev, scale_zp_dev, kept_index_dev, labels_dev, B, S,
+                       row_capacity, rows_dev, Hkv, D, dtype, bits, q_dev, Hq, scale, out_dev, workspace_dev,
+                       workspace_bytes, (hipStream_t)stream);
+}
+
 int rtkv_gather_rows(const void* src_dev, int64_t B, int64_t S, int64_t row_bytes, const int32_t* kept_index_dev,
                      int64_t row_capacity, int64_t src_stride_b, void* dst_dev, int64_t dst_stride_b, int64_t src_stride_s,
                      const rtkv_layer_stats* stats_dev, void* stream) {

@@ -61,6 +61,10 @@ class CompressedKVCache:
         p = self.compression_info[layer_idx]
         return unpack_layer(p)
 
+    def attend(self, layer_idx: int, q: torch.Tensor, num_kv_heads: int, scale: Optional[float] = None):
+        """One decode step of attention over the packed layer (no dense K'/V'): fp32 [B, Hq, D]."""
+        return decode_attention(self.compression_info[layer_idx], q, num_kv_heads, scale)
+
 
 def unpack_layer(p: dict):
     """Packed layer dict → dense dequantized (K', V'), bit-identical to the fused output."""
@@ -87,6 +91,45 @@ def unpack_layer(p: dict):
                                                 L.stream_ptr(dev)), "rtkv_unpack_dequant")
         outs.append(out)
     return outs[0], outs[1]
+
+
+def decode_attention(p: dict, q: torch.Tensor, num_kv_heads: int, scale: Optional[float] = None) -> torch.Tensor:
+    """Attention of one new token per batch row over a packed layer, decoded on the fly
+    (rtkv_decode_attention_packed).  q: [B, Hq, D] in the layer's dtype; returns fp32 [B, Hq, D] =
+    softmax(q·K'ᵀ·scale)·V' over the kept rows, with K'/V' exactly the dequantized rows
+    (modified_llama.py:140-142 attends over those dequantized floats).  scale defaults to 1/sqrt(D)
+    (modified_llama.py:89)."""
+    codes_k, codes_v = p["codes_k"], p["codes_v"]
+    L.require_device(codes_k, codes_v, q)
+    dev = codes_k.device
+    if q.dtype != p["dtype"]:
+        raise ValueError(f"q dtype {q.dtype} does not match the packed layer's {p['dtype']}")
+    B, Hq, D = q.shape
+    F = int(p["feature_dim"])
+    if num_kv_heads * D != F:
+        raise ValueError(f"num_kv_heads * head_dim = {num_kv_heads * D} != feature_dim {F}")
+    row_offset = p["row_offset"].contiguous()
+    scale_zp = p["scale_zp"].contiguous()
+    kept_index = p["kept_index"].contiguous()
+    labels = p["labels"].contiguous()
+    Sp = kept_index.shape[1]
+    S = labels.shape[1]
+    out = torch.zeros(B, Hq, D, dtype=torch.float32, device=dev)
+    if Sp == 0:
+        return out
+    rows = p.get("_rows_dev")
+    if rows is None or rows.device != dev:  # kept once per layer: no host→device copy per decode step
+        rows = p["_rows_dev"] = torch.tensor(p["rows"], dtype=torch.int64, device=dev)
+    bits = (ctypes.c_int32 * 3)(*p["bits"])
+    qc = q.contiguous()
+    ws = torch.empty(L.lib().rtkv_decode_workspace_size(B, Hq, num_kv_heads, D, Sp), dtype=torch.uint8, device=dev)
+    sc = float(scale) if scale is not None else 1.0 / float(D) ** 0.5
+    L.check(L.lib().rtkv_decode_attention_packed(codes_k.data_ptr(), codes_v.data_ptr(), row_offset.data_ptr(),
+                                                 scale_zp.data_ptr(), kept_index.data_ptr(), labels.data_ptr(), B, S,
+                                                 Sp, rows.data_ptr(), num_kv_heads, D, L.TORCH_DTYPE_CODE[q.dtype],
+                                                 bits, qc.data_ptr(), Hq, sc, out.data_ptr(), ws.data_ptr(),
+                                                 ws.numel(), L.stream_ptr(dev)), "rtkv_decode_attention_packed")
+    return out
 
 
 class AdaptiveQuantization(nn.Module):

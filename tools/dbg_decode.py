@@ -1,0 +1,40 @@
+"""Diagnostic: per-head error of decode_attention on one case (see tests/test_gpu_decode.py)."""
+import os
+import sys
+
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(HERE, "..", "realtime-kv-cache-compression_amd"))
+sys.path.insert(0, os.path.join(HERE, "..", "tests", "golden"))
+sys.path.insert(0, os.path.join(HERE, "..", "tests"))
+import rtkv  # noqa: E402
+import synth  # noqa: E402
+from test_gpu_decode import dev, reference, COV  # noqa: E402
+
+rtkv.build()
+for (B, S, Hkv, D, Hq, dtype, bits, ratio) in [(1, 700, 40, 128, 40, "float16", (2, 4, 8), 0.9),
+                                               (1, 700, 32, 128, 32, "float16", (2, 4, 8), 0.9),
+                                               (1, 700, 40, 128, 40, "float16", (8, 8, 8), 0.9),
+                                               (1, 2000, 40, 128, 40, "float16", (2, 4, 8), 0.9)]:
+    F = Hkv * D
+    seed = S * 7 + Hkv
+    K, V = synth.kv(seed, B, S, F, dtype)
+    W = synth.attention_slice(seed, B, 8, S, rtkv.prompt_length(S), dtype)
+    cfg = rtkv.CompressionConfig(num_hidden_layers=4, low_precision_bits=bits[0], medium_precision_bits=bits[1],
+                                 high_precision_bits=bits[2], early_layer_ratio=ratio, middle_layer_ratio=ratio,
+                                 later_layer_ratio=ratio, **COV)
+    comp = rtkv.RealTimePrefillCompressor(cfg)
+    ids = torch.zeros(B, S, dtype=torch.long, device="cuda")
+    k2, v2, info = comp.compress_layer_kv_cache(dev(K, dtype), dev(V, dtype), dev(W, dtype), ids, 1)
+    pk = info["packed"]
+    q = dev(synth.cast(synth.normal(seed + 1, (B, Hq, D)), dtype), dtype)
+    ref = reference(k2, v2, pk["rows"], q, Hkv, 1.0 / D ** 0.5)
+    print(B, S, Hkv, bits, "rows", pk["rows"], "codes", pk["codes_k"].numel())
+    for wg in (64, 2048):
+        os.environ["RTKV_DECODE_WGS"] = str(wg)
+        out = rtkv.decode_attention(pk, q, Hkv)
+        err = (out - ref).abs().amax(dim=-1)[0]
+        bad = (err > 1e-3).nonzero().flatten().tolist()
+        print("  wgs", wg, "bad heads", bad, "max err", err.max().item())
+    # zero the last row's codes → which rows matter?
