@@ -6,7 +6,8 @@ class and method names.  All compute runs in librtkv.so (include/rtkv.h); there 
 """
 from . import _lib
 from .base_config import CompressionConfig
-from .compression_layers import AdaptiveQuantization, CompressedKVCache, decode_attention, unpack_layer
+from .compression_layers import (AdaptiveQuantization, CompressedKVCache, decode_attention, load_packed, save_packed,
+                                 unpack_layer)
 from .dynamic_quantization import DynamicPrecisionQuantizer
 from .engine import (LayerBuffers, LayerResult, Workspace, compress_layer, compress_layer_qk, importance_qk_lse,
                      params_from_config, prompt_length)
@@ -18,6 +19,7 @@ __all__ = [
     "CompressionConfig", "RealTimePrefillCompressor", "UnifiedCompressor", "CompressionHook",
     "PromptGuidedImportanceScorer", "LayerWiseImportanceTracker", "DynamicPrecisionQuantizer",
     "SelectiveTokenPropagator", "CompressedKVCache", "AdaptiveQuantization", "unpack_layer", "decode_attention",
+    "save_packed", "load_packed",
     "LayerBuffers", "LayerResult", "Workspace", "compress_layer", "compress_layer_qk", "importance_qk_lse",
     "params_from_config", "prompt_length",
 ]

@@ -65,6 +65,97 @@ class CompressedKVCache:
         """One decode step of attention over the packed layer (no dense K'/V'): fp32 [B, Hq, D]."""
         return decode_attention(self.compression_info[layer_idx], q, num_kv_heads, scale)
 
+    def save(self, path: str):
+        """Write every packed layer to one safetensors file (see save_packed for the format)."""
+        save_packed(self.compression_info, path)
+
+    def load(self, path: str, device="cuda"):
+        """Read the packed layers of a file written by save(); replaces the packed layers held."""
+        self.compression_info = load_packed(path, device)
+
+
+# ---------------------------------------------------------------------- packed (de)serialization
+# File format "rtkv-packed/1": a safetensors file.  Per layer i, tensors "L{i}.codes_k",
+# "L{i}.codes_v" (uint8, the bit-packed rows back to back), "L{i}.row_offset" (int64 [B, S'] byte
+# offset of each kept row), "L{i}.scale_zp" (fp32 [B, S', 4]: K scale, K zero-point, V scale,
+# V zero-point), "L{i}.kept_index" (int32 [B, S'] source token index), "L{i}.labels" (uint8 [B, S]
+# precision class per source token); the metadata entry "L{i}" holds {"rows", "bits", "dtype",
+# "feature_dim"} as JSON.  Loading checks every offset and count against the tensor sizes, so a
+# truncated or inconsistent file raises ValueError instead of reaching a kernel.
+_FORMAT = "rtkv-packed/1"
+_TENSORS = ("codes_k", "codes_v", "row_offset", "scale_zp", "kept_index", "labels")
+_DTYPES = {"float32": torch.float32, "float16": torch.float16, "bfloat16": torch.bfloat16}
+
+
+def save_packed(layers: Dict[int, dict], path: str):
+    import json
+    from safetensors.torch import save_file
+    tensors, meta = {}, {"format": _FORMAT}
+    for i, p in layers.items():
+        for name in _TENSORS:
+            tensors[f"L{i}.{name}"] = p[name].detach().contiguous().cpu()
+        meta[f"L{i}"] = json.dumps({"rows": [int(r) for r in p["rows"]], "bits": [int(b) for b in p["bits"]],
+                                    "dtype": str(p["dtype"]).replace("torch.", ""),
+                                    "feature_dim": int(p["feature_dim"])})
+    save_file(tensors, path, metadata=meta)
+
+
+def _check_packed(i: int, p: dict):
+    def bad(msg):
+        raise ValueError(f"packed layer {i}: {msg}")
+    B, Sp = p["kept_index"].shape
+    if p["row_offset"].shape != (B, Sp) or p["scale_zp"].shape != (B, Sp, 4) or p["labels"].dim() != 2 \
+            or p["labels"].shape[0] != B:
+        bad("inconsistent shapes")
+    if p["codes_k"].numel() != p["codes_v"].numel():
+        bad("codes_k and codes_v differ in size")
+    if len(p["rows"]) != B or any(r < 0 or r > Sp for r in p["rows"]):
+        bad("row counts out of range")
+    F, S = p["feature_dim"], p["labels"].shape[1]
+    widths = [L.lib().rtkv_field_width(L.TORCH_DTYPE_CODE[p["dtype"]], b) for b in p["bits"]]
+    if len(widths) != 3 or min(widths) <= 0:
+        bad("unsupported bits")
+    nbytes = p["codes_k"].numel()
+    for b in range(B):
+        n = p["rows"][b]
+        if n == 0:
+            continue
+        ki = p["kept_index"][b, :n].to(torch.int64)
+        if int(ki.min()) < 0 or int(ki.max()) >= S:
+            bad("kept index out of range")
+        lab = p["labels"][b].to(torch.int64)[ki]
+        if int(lab.max()) > 2:
+            bad("class label out of range")
+        w = torch.tensor(widths, dtype=torch.int64)[lab]
+        off = p["row_offset"][b, :n]
+        if int(off.min()) < 0 or int((off + F * w // 8).max()) > nbytes:
+            bad("row offsets past the end of the codes")
+
+
+def load_packed(path: str, device="cuda") -> Dict[int, dict]:
+    import json
+    from safetensors import safe_open
+    out: Dict[int, dict] = {}
+    with safe_open(path, framework="pt", device="cpu") as f:
+        meta = f.metadata() or {}
+        if meta.get("format") != _FORMAT:
+            raise ValueError(f"{path}: not an {_FORMAT} file")
+        for key, val in meta.items():
+            if not key.startswith("L"):
+                continue
+            i = int(key[1:])
+            m = json.loads(val)
+            p = {name: f.get_tensor(f"L{i}.{name}") for name in _TENSORS}
+            if m["dtype"] not in _DTYPES:
+                raise ValueError(f"packed layer {i}: unknown dtype {m['dtype']}")
+            p.update(rows=list(m["rows"]), bits=tuple(m["bits"]), dtype=_DTYPES[m["dtype"]],
+                     feature_dim=int(m["feature_dim"]))
+            _check_packed(i, p)
+            for name in _TENSORS:
+                p[name] = p[name].to(device)
+            out[i] = p
+    return dict(sorted(out.items()))
+
 
 def unpack_layer(p: dict):
     """Packed layer dict → dense dequantized (K', V'), bit-identical to the fused output."""

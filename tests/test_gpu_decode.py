@@ -110,3 +110,22 @@ def test_decode_rejects_bad_shapes():
         rtkv.decode_attention(info["packed"], q, Hkv)
     with pytest.raises(ValueError):
         rtkv.decode_attention(info["packed"], q.float(), Hkv)
+
+
+def test_packed_file_round_trip_decodes_identically(tmp_path):
+    """compress → save_packed → load_packed → the same K'/V' and the same decode output."""
+    import rtkv
+    B, S, Hkv, D, Hq, dtype = 2, 1500, 8, 128, 32, "float16"
+    K, V = synth.kv(9, B, S, Hkv * D, dtype)
+    W = synth.attention_slice(9, B, 8, S, rtkv.prompt_length(S), dtype)
+    comp = rtkv.RealTimePrefillCompressor(rtkv.CompressionConfig(num_hidden_layers=4, low_precision_bits=2,
+                                                                 medium_precision_bits=4, high_precision_bits=8, **COV))
+    ids = torch.zeros(B, S, dtype=torch.long, device="cuda")
+    k2, v2, info = comp.compress_layer_kv_cache(dev(K, dtype), dev(V, dtype), dev(W, dtype), ids, 2)
+    path = str(tmp_path / "layer.safetensors")
+    rtkv.save_packed({2: info["packed"]}, path)
+    back = rtkv.load_packed(path, device="cuda")[2]
+    dk, dv = rtkv.unpack_layer(back)
+    assert torch.equal(dk, k2) and torch.equal(dv, v2)
+    q = dev(synth.cast(synth.normal(10, (B, Hq, D)), dtype), dtype)
+    assert torch.equal(rtkv.decode_attention(back, q, Hkv), rtkv.decode_attention(info["packed"], q, Hkv))
