@@ -322,6 +322,13 @@ int rtkv_shard_ranges(const int32_t* kept_index_dev, const int64_t* row_offset_d
  * ---------------------------------------------------------------------------------------------- */
 int rtkv_importance_qk_lse(const rtkv_qk_desc* q, int32_t prompt_len, float* A_dev, void* stream);
 
+/* Row log-sum-exp of the prefill attention: lse[b,h,i] = log Σ_j exp(q_i·k_j·scale)
+ * over j ≤ i (causal) or all j < S, without materialising the [B,H,S,S] softmax of
+ * modified_llama.py:88-94 — the producer of the lse that rtkv_importance_qk_lse consumes.  Reads
+ * q_dev / k_dev / strides / causal / scale of the descriptor (lse_dev is ignored; row0 must be 0) and
+ * writes lse_out[b*lse_stride_b + h*lse_stride_h + i] (fp32).  head_dim 64 or 128, fp16/bf16. */
+int rtkv_attention_lse(const rtkv_qk_desc* q, float* lse_out_dev, void* stream);
+
 /* rtkv_compress_layer with the fused importance mode (K1' on MFMA, then K2 and K4 unchanged). */
 int rtkv_compress_layer_qk(const rtkv_kv_desc* kv, const rtkv_qk_desc* q, const rtkv_layer_params* p,
                            const rtkv_layer_out* out, void* workspace_dev, size_t workspace_bytes,
@@ -345,7 +352,7 @@ int rtkv_unpack_dequant(const uint8_t* packed_dev, const int64_t* row_offset_dev
  * where K'/V' are decoded from the packed codes on the fly, element for element the dequantized
  * rows rtkv_compress_layer writes.  Replaces the reference's attention over the dequantized cache
  * (modified_llama.py:140-142, 165-166) without materialising K'/V'.  Arguments as
- * rtkv_unpack_dequant (H = Hkv kv heads of head_dim D, F = Hkv·D a multiple of 512, at most 5120;
+ * rtkv_unpack_dequant (H = Hkv kv heads of head_dim D, F = Hkv·D a multiple of 512;
  * packed field widths 2/4/8/16), plus q [B, Hq, D] in the K/V dtype (Hq a multiple of Hkv: GQA),
  * scale (1/sqrt(D) in the reference, modified_llama.py:89) and out [B, Hq, D] fp32.  Workspace:
  * rtkv_decode_workspace_size(B, Hq, Hkv, D, row_capacity) bytes. */

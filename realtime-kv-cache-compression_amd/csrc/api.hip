@@ -306,6 +306,11 @@ int rtkv_importance_qk_lse(const rtkv_qk_desc* q, int32_t prompt_len, float* A_d
   return launch_qk_importance(*q, prompt_len, A_dev, (hipStream_t)stream, x, nullptr);
 }
 
+int rtkv_attention_lse(const rtkv_qk_desc* q, float* lse_dev, void* stream) {
+  RTKV_REQUIRE(q != nullptr, "null query descriptor");
+  return launch_attention_lse(*q, lse_dev, (hipStream_t)stream);
+}
+
 // ---------------------------------------------------------------------------------- sequence shards
 int rtkv_attention_aggregation_shard(const rtkv_attn_desc* w, int32_t prompt_len, int64_t row0, int64_t S_total,
                                      float* A_dev, void* stream) {

@@ -1,0 +1,215 @@
+// attn_lse.hip — the row log-sum-exp of the prefill attention, the one quantity the fused importance
+// mode (K1', qk_importance.hip) needs besides Q and the prompt keys:
+//
+//   lse[b,h,i] = log Σ_{j ≤ i (causal), j < S} exp(q[b,h,i]·k[b,h/g,j]·scale)
+//
+// i.e. the normaliser of the reference's softmax(Q·Kᵀ/√d + mask) (modified_llama.py:88-94) without
+// materialising the [B,H,S,S] matrix.  fp32 accumulation; parity with a torch fp32 logsumexp is a
+// tolerance (tests/test_gpu_lse.py).
+//
+// Work decomposition (gfx950, wave64): a workgroup owns 64 query rows of one (b, h), one wave per
+// 16 rows; it walks the key tiles of 64 rows up to the causal diagonal, each tile staged in LDS by
+// LDS-DMA (double-buffered, swizzled as in qk_importance.hip) and shared by the 4 waves.  Each wave
+// computes its 16 × 64 logits with v_mfma_f32_16x16x32_{f16,bf16} (4 column tiles × D/32 k-steps);
+// every lane keeps a running (max, sum) per accumulator row over the key columns it holds, in the
+// exp2 domain with a lazily raised max (rescale only when a logit passes it by 8: one wave-uniform
+// branch per tile).  The 16 lanes of a row combine at the end.  Workgroups are issued longest-first
+// (the last query blocks carry the most key tiles).
+#include "common.h"
+
+namespace rtkv {
+
+namespace {
+
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+template <int DT> struct LFrag;
+template <> struct LFrag<RTKV_F16> {
+  using T = f16x8;
+  __device__ __forceinline__ static f32x4 mfma(T a, T b, f32x4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
+  }
+};
+template <> struct LFrag<RTKV_BF16> {
+  using T = bf16x8;
+  __device__ __forceinline__ static f32x4 mfma(T a, T b, f32x4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+  }
+};
+
+constexpr int kLRows = 64;  // query rows per workgroup, and key rows per tile
+constexpr float kLSlack = 8.f;
+
+struct LseArgs {
+  rtkv_qk_desc q;
+  float* lse;
+  int nblk;  // query blocks per (b, h)
+};
+
+__device__ __forceinline__ void lds_dma16(const void* g, void* lds_base) {
+  __builtin_amdgcn_global_load_lds(g, (__attribute__((address_space(3))) void*)lds_base, 16, 0, 0);
+}
+
+template <int DT, int KS>
+__global__ __launch_bounds__(256) void attn_lse_kernel(LseArgs g) {
+  using FT = typename LFrag<DT>::T;
+  using S_ = typename Dt<DT>::S;
+  constexpr int D = 32 * KS;
+  constexpr int RB = 2 * D;                  // bytes per key row
+  constexpr int CH = RB / 16;                // 16-byte chunks per row
+  constexpr int RPI = 1024 / RB;             // rows per DMA wave-instruction
+  constexpr int TILE = kLRows * RB;          // bytes per key tile
+  constexpr int KI = TILE / 1024 / 4;        // DMA instructions per wave per tile
+  extern __shared__ __attribute__((aligned(1024))) uint8_t lds[];  // 2 × TILE
+  const rtkv_qk_desc& q = g.q;
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int c16 = lane & 15, kg = lane >> 4;
+  // longest-first: block x counts down from the last query block
+  const int qb = g.nblk - 1 - (int)blockIdx.x;
+  const int h = blockIdx.y, b = blockIdx.z;
+  const int S = (int)q.S, grp = (int)(q.H / q.Hkv);
+  const int i0 = qb * kLRows;
+  const int wrow0 = i0 + wave * 16;
+  const int crow0 = wrow0 + 4 * kg;          // accumulator rows crow0 + r
+  const float sc = q.scale * 1.4426950408889634f;
+  const S_* Kh = static_cast<const S_*>(q.k_dev) + b * q.k_stride_b + (int64_t)(h / grp) * q.k_stride_h;
+  // key rows this block needs: causal → up to its last query row (global position row0 + i)
+  int64_t kend = q.causal ? q.row0 + i0 + kLRows : S;
+  if (kend > S) kend = S;
+  const int ntiles = (int)((kend + kLRows - 1) / kLRows);
+  const int lrow = lane / CH, lpc = lane % CH;
+  auto issue = [&](int kt) {
+    uint8_t* st = lds + (kt & 1) * TILE;
+#pragma unroll
+    for (int k = 0; k < KI; ++k) {
+      const int r = (wave * KI + k) * RPI + lrow;
+      const int c = lpc ^ (r & (CH - 1));
+      int kr = kt * kLRows + r;
+      kr = kr < S ? kr : S - 1;              // rows past S: any valid row (masked)
+      lds_dma16(Kh + (int64_t)kr * q.k_stride_s + c * 8, st + (wave * KI + k) * 1024);
+    }
+  };
+  // the wave's 16 query rows, A fragments straight from global (once)
+  FT a[KS];
+  {
+    const int qr = wrow0 + c16 < S ? wrow0 + c16 : S - 1;
+    const S_* qrow = static_cast<const S_*>(q.q_dev) + b * q.q_stride_b + (int64_t)h * q.q_stride_h +
+                     (int64_t)qr * q.q_stride_s;
+#pragma unroll
+    for (int s_ = 0; s_ < KS; ++s_) a[s_] = *reinterpret_cast<const FT*>(qrow + (4 * s_ + kg) * 8);
+  }
+  float m[4], l[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    m[r] = -INFINITY;
+    l[r] = 0.f;
+  }
+  issue(0);
+  for (int kt = 0; kt < ntiles; ++kt) {
+    __builtin_amdgcn_s_barrier();  // every wave is done with tile kt-1: its slot is free
+    if (kt + 1 < ntiles) {
+      issue(kt + 1);
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(KI) : "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __builtin_amdgcn_s_barrier();  // ... and every other wave's pieces of tile kt
+    const uint8_t* st = lds + (kt & 1) * TILE;
+    f32x4 acc[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+      const int kr = 16 * t + c16;
+      const uint8_t* krow = st + kr * RB;
+#pragma unroll
+      for (int s_ = 0; s_ < KS; ++s_) {
+        const FT bf = *reinterpret_cast<const FT*>(krow + (((4 * s_ + kg) ^ (kr & (CH - 1))) * 16));
+        acc[t] = LFrag<DT>::mfma(a[s_], bf, acc[t]);
+      }
+    }
+    // logits in the exp2 domain; mask keys past S and (causal) past the query position
+    const bool edge = (int64_t)(kt + 1) * kLRows > (q.causal ? q.row0 + wrow0 : (int64_t)S) || (kt + 1) * kLRows > S;
+    float v[4][4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float x = acc[t][r] * sc;
+        if (edge) {
+          const int j = kt * kLRows + 16 * t + c16;
+          const bool ok = j < S && (!q.causal || (int64_t)j <= q.row0 + crow0 + r);
+          x = ok ? x : -INFINITY;
+        }
+        v[t][r] = x;
+      }
+    bool up = false;
+    float mt[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      mt[r] = fmaxf(fmaxf(v[0][r], v[1][r]), fmaxf(v[2][r], v[3][r]));
+      up |= mt[r] > m[r] + kLSlack;
+    }
+    if (__ballot(up)) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float mn = mt[r] > m[r] + kLSlack ? mt[r] : m[r];
+        l[r] *= (m[r] == -INFINITY) ? 0.f : __builtin_amdgcn_exp2f(m[r] - mn);
+        m[r] = mn;
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+      for (int t = 0; t < 4; ++t) l[r] += (m[r] == -INFINITY) ? 0.f : __builtin_amdgcn_exp2f(v[t][r] - m[r]);
+  }
+  // combine the 16 lanes holding each row: M = max m, L = Σ l·2^(m − M); lse = (M + log2 L)·ln 2
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    float M = m[r];
+#pragma unroll
+    for (int o = 1; o < 16; o <<= 1) M = fmaxf(M, __shfl_xor(M, o, 64));
+    float L = (m[r] == -INFINITY) ? 0.f : l[r] * __builtin_amdgcn_exp2f(m[r] - M);
+#pragma unroll
+    for (int o = 1; o < 16; o <<= 1) L += __shfl_xor(L, o, 64);
+    const int i = crow0 + r;
+    if (c16 == 0 && i < S)
+      g.lse[b * q.lse_stride_b + (int64_t)h * q.lse_stride_h + i] =
+          L > 0.f ? (M + __log2f(L)) * 0.6931471805599453f : -INFINITY;
+  }
+}
+
+template <int DT, int KS>
+int launch_lse_tpl(const LseArgs& a, dim3 grid, hipStream_t st) {
+  constexpr size_t lds = 2 * (size_t)kLRows * (64 * KS);
+  hipLaunchKernelGGL((attn_lse_kernel<DT, KS>), grid, dim3(256), lds, st, a);
+  RTKV_HIP_CHECK(hipGetLastError());
+  return RTKV_OK;
+}
+
+}  // namespace
+
+int launch_attention_lse(const rtkv_qk_desc& q, float* lse, hipStream_t st) {
+  RTKV_REQUIRE(q.q_dev && q.k_dev && lse, "attention_lse: null pointer");
+  RTKV_REQUIRE(q.B >= 1 && q.B <= 65535 && q.H >= 1 && q.H <= 65535 && q.S >= 1 && q.Hkv >= 1,
+               "attention_lse: bad shape");
+  RTKV_REQUIRE(q.H % q.Hkv == 0, "attention_lse: H must be a multiple of Hkv");
+  RTKV_REQUIRE(q.D == 64 || q.D == 128, "attention_lse: head_dim must be 64 or 128");
+  RTKV_REQUIRE(q.dtype == RTKV_F16 || q.dtype == RTKV_BF16, "attention_lse: Q/K must be float16 or bfloat16");
+  RTKV_REQUIRE(q.q_stride_s % 8 == 0 && q.q_stride_h % 8 == 0 && q.q_stride_b % 8 == 0 && q.k_stride_s % 8 == 0 &&
+                   q.k_stride_h % 8 == 0 && q.k_stride_b % 8 == 0 && ((uintptr_t)q.q_dev % 16) == 0 &&
+                   ((uintptr_t)q.k_dev % 16) == 0,
+               "attention_lse: Q/K rows must be 16-byte aligned");
+  RTKV_REQUIRE(q.S < ((int64_t)1 << 31) && q.row0 == 0, "attention_lse: bad row range (row0 must be 0)");
+  LseArgs a;
+  a.q = q;
+  a.lse = lse;
+  a.nblk = (int)((q.S + kLRows - 1) / kLRows);
+  const dim3 grid((unsigned)a.nblk, (unsigned)q.H, (unsigned)q.B);
+  const int ks = (int)(q.D / 32);
+  if (q.dtype == RTKV_F16) return ks == 4 ? launch_lse_tpl<RTKV_F16, 4>(a, grid, st) : launch_lse_tpl<RTKV_F16, 2>(a, grid, st);
+  return ks == 4 ? launch_lse_tpl<RTKV_BF16, 4>(a, grid, st) : launch_lse_tpl<RTKV_BF16, 2>(a, grid, st);
+}
+
+}  // namespace rtkv

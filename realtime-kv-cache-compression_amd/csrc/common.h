@@ -195,6 +195,7 @@ __device__ __forceinline__ void zero_regions(const AggExtras& x) {
 }
 int launch_aggregation(const rtkv_attn_desc& w, int P, float* A, hipStream_t st, const AggExtras& x = AggExtras());
 int launch_qk_importance(const rtkv_qk_desc& q, int P, float* A, hipStream_t st, const AggExtras& x, int* nparts);
+int launch_attention_lse(const rtkv_qk_desc& q, float* lse, hipStream_t st);
 int launch_position_bias(int64_t S, float* pos, hipStream_t st);
 int launch_minmax_normalize(const void* x, int dt, int64_t B, int64_t S, void* out, hipStream_t st);
 

@@ -9,8 +9,8 @@ from .base_config import CompressionConfig
 from .compression_layers import (AdaptiveQuantization, CompressedKVCache, decode_attention, load_packed, save_packed,
                                  unpack_layer)
 from .dynamic_quantization import DynamicPrecisionQuantizer
-from .engine import (LayerBuffers, LayerResult, Workspace, compress_layer, compress_layer_qk, importance_qk_lse,
-                     params_from_config, prompt_length)
+from .engine import (LayerBuffers, LayerResult, Workspace, attention_lse, compress_layer, compress_layer_qk,
+                     importance_qk_lse, params_from_config, prompt_length)
 from .selective_propagation import SelectiveTokenPropagator
 from .token_importance import LayerWiseImportanceTracker, PromptGuidedImportanceScorer
 from .unified_compressor import CompressionHook, RealTimePrefillCompressor, UnifiedCompressor
@@ -20,7 +20,7 @@ __all__ = [
     "PromptGuidedImportanceScorer", "LayerWiseImportanceTracker", "DynamicPrecisionQuantizer",
     "SelectiveTokenPropagator", "CompressedKVCache", "AdaptiveQuantization", "unpack_layer", "decode_attention",
     "save_packed", "load_packed",
-    "LayerBuffers", "LayerResult", "Workspace", "compress_layer", "compress_layer_qk", "importance_qk_lse",
+    "LayerBuffers", "LayerResult", "Workspace", "compress_layer", "compress_layer_qk", "importance_qk_lse", "attention_lse",
     "params_from_config", "prompt_length",
 ]
 

@@ -250,6 +250,17 @@ def importance_qk_lse(Q, K, lse, prompt_len: int, causal: bool = True, scale: Op
     return A
 
 
+def attention_lse(Q, K, causal: bool = True, scale: Optional[float] = None, k_layout: str = "bhsd") -> torch.Tensor:
+    """Row log-sum-exp [B, H, S] (fp32) of softmax(Q·Kᵀ·scale + causal mask) (rtkv_attention_lse):
+    the lse the fused importance mode consumes, without the [B, H, S, S] matrix."""
+    L.require_device(Q, K)
+    B, H, S, _ = Q.shape
+    lse = torch.empty(B, H, S, dtype=torch.float32, device=Q.device)
+    qd = qk_desc(Q, K, lse, scale=scale, causal=causal, k_layout=k_layout)
+    L.check(L.lib().rtkv_attention_lse(ctypes.byref(qd), lse.data_ptr(), L.stream_ptr(Q.device)), "rtkv_attention_lse")
+    return lse
+
+
 def compress_layer(K, V, W, params: L.LayerParams, bufs: LayerBuffers, workspace: Workspace,
                    layout: str = "bsf", stream: Optional[int] = None) -> LayerResult:
     """Enqueue aggregation → scores/labels/selection → quantize+pack+compact for one layer."""

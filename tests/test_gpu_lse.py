@@ -1,0 +1,79 @@
+"""GPU: the attention row log-sum-exp (rtkv_attention_lse, csrc/attn_lse.hip) against a torch fp32
+logsumexp of the masked scores, and the fused importance mode fed by it.
+
+The kernel multiplies fp16/bf16 Q·K on MFMA with fp32 accumulation and sums exp2 in fp32, so the
+tolerance is |Δlse| ≤ 2e-4 + 1e-5·|lse| (summation order and the hardware exp2/log2).  Cases: causal
+and full attention, head_dim 64 and 128, GQA (H / Hkv = 4), S not a multiple of the 64-row tiles,
+tiny S, batch 2, both layouts of K."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module", autouse=True)
+def gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no ROCm device")
+    import rtkv
+    rtkv.build()
+
+
+def ref_lse(Q, K, causal, scale):
+    """Q [B,H,S,D], K [B,Hkv,S,D] → lse [B,H,S] in fp32."""
+    B, H, S, D = Q.shape
+    g = H // K.shape[1]
+    Kf = K.float().repeat_interleave(g, dim=1)
+    s = torch.einsum("bhid,bhjd->bhij", Q.float(), Kf) * scale
+    if causal:
+        s = s.masked_fill(torch.ones(S, S, dtype=torch.bool, device=Q.device).triu(1), float("-inf"))
+    return torch.logsumexp(s, dim=-1)
+
+
+CASES = [
+    # B, H, Hkv, S, D, dtype, causal
+    (1, 4, 4, 1000, 128, torch.float16, True),
+    (2, 8, 2, 333, 64, torch.bfloat16, True),
+    (1, 4, 4, 777, 128, torch.bfloat16, False),
+    (1, 2, 2, 64, 128, torch.float16, True),
+    (1, 2, 1, 5, 64, torch.float16, True),
+    (1, 32, 32, 4096, 128, torch.float16, True),
+]
+
+
+@pytest.mark.parametrize("B,H,Hkv,S,D,dtype,causal", CASES, ids=lambda v: str(v).replace("torch.", ""))
+def test_attention_lse(B, H, Hkv, S, D, dtype, causal):
+    import rtkv
+    g = torch.Generator(device="cuda").manual_seed(S * 31 + H)
+    Q = (torch.randn(B, H, S, D, device="cuda", generator=g) * 1.5).to(dtype)
+    K = (torch.randn(B, Hkv, S, D, device="cuda", generator=g) * 1.5).to(dtype)
+    scale = 1.0 / D ** 0.5
+    lse = rtkv.attention_lse(Q, K, causal=causal)
+    ref = ref_lse(Q, K, causal, scale)
+    assert torch.isfinite(lse).all()
+    torch.testing.assert_close(lse, ref, rtol=1e-5, atol=2e-4)
+    # the [B, S, Hkv*D] layout of the compressor's key input gives the same result
+    Kbsf = K.transpose(1, 2).reshape(B, S, Hkv * D).contiguous()
+    assert torch.equal(rtkv.attention_lse(Q, Kbsf, causal=causal, k_layout="bsf"), lse)
+
+
+def test_fused_importance_from_own_lse():
+    """K1' fed by rtkv_attention_lse == K1' fed by the torch fp32 lse (to the lse tolerance)."""
+    import rtkv
+    B, H, S, D, P = 1, 8, 2048, 128, 128
+    g = torch.Generator(device="cuda").manual_seed(5)
+    Q = torch.randn(B, H, S, D, device="cuda", generator=g).half()
+    K = torch.randn(B, H, S, D, device="cuda", generator=g).half()
+    lse = rtkv.attention_lse(Q, K)
+    ref = ref_lse(Q, K, True, 1.0 / D ** 0.5).contiguous()
+    Kbsf = K.transpose(1, 2).reshape(B, S, H * D).contiguous()
+    A = rtkv.importance_qk_lse(Q, Kbsf, lse, P)
+    A_ref = rtkv.importance_qk_lse(Q, Kbsf, ref, P)
+    torch.testing.assert_close(A, A_ref, rtol=1e-3, atol=1e-6)
+
+
+def test_rejects_unsupported():
+    import rtkv
+    Q = torch.zeros(1, 2, 64, 96, device="cuda", dtype=torch.float16)
+    with pytest.raises(RuntimeError, match="head_dim"):
+        rtkv.attention_lse(Q, Q)
