@@ -11,6 +11,7 @@ from .compression_layers import (AdaptiveQuantization, CompressedKVCache, decode
 from .dynamic_quantization import DynamicPrecisionQuantizer
 from .engine import (LayerBuffers, LayerResult, Workspace, attention_lse, compress_layer, compress_layer_qk,
                      importance_qk_lse, params_from_config, prompt_length)
+from .model_side import CompressedPrefillAttention
 from .selective_propagation import SelectiveTokenPropagator
 from .token_importance import LayerWiseImportanceTracker, PromptGuidedImportanceScorer
 from .unified_compressor import CompressionHook, RealTimePrefillCompressor, UnifiedCompressor
@@ -19,7 +20,7 @@ __all__ = [
     "CompressionConfig", "RealTimePrefillCompressor", "UnifiedCompressor", "CompressionHook",
     "PromptGuidedImportanceScorer", "LayerWiseImportanceTracker", "DynamicPrecisionQuantizer",
     "SelectiveTokenPropagator", "CompressedKVCache", "AdaptiveQuantization", "unpack_layer", "decode_attention",
-    "save_packed", "load_packed",
+    "save_packed", "load_packed", "CompressedPrefillAttention",
     "LayerBuffers", "LayerResult", "Workspace", "compress_layer", "compress_layer_qk", "importance_qk_lse", "attention_lse",
     "params_from_config", "prompt_length",
 ]
