@@ -7,10 +7,11 @@
 // materialising the [B,H,S,S] matrix.  fp32 accumulation; parity with a torch fp32 logsumexp is a
 // tolerance (tests/test_gpu_lse.py).
 //
-// Work decomposition (gfx950, wave64): a workgroup owns 64 query rows of one (b, h), one wave per
-// 16 rows; it walks the key tiles of 64 rows up to the causal diagonal, each tile staged in LDS by
-// LDS-DMA (double-buffered, swizzled as in qk_importance.hip) and shared by the 4 waves.  Each wave
-// computes its 16 × 64 logits with v_mfma_f32_16x16x32_{f16,bf16} (4 column tiles × D/32 k-steps);
+// Work decomposition (gfx950, wave64): a workgroup owns 128 query rows of one (b, h), 32 rows (two
+// groups of 16) per wave; it walks the key tiles of 64 rows up to the causal diagonal, each tile
+// staged in LDS by LDS-DMA (double-buffered, swizzled as in qk_importance.hip) and shared by the 4
+// waves.  Each wave computes its 32 × 64 logits with v_mfma_f32_16x16x32_{f16,bf16} (2 row groups ×
+// 4 column tiles × D/32 k-steps; each key fragment read from LDS feeds both row groups);
 // every lane keeps a running (max, sum) per accumulator row over the key columns it holds, in the
 // exp2 domain with a lazily raised max (rescale only when a logit passes it by 8: one wave-uniform
 // branch per tile).  The 16 lanes of a row combine at the end.  Workgroups are issued longest-first
@@ -39,7 +40,8 @@ template <> struct LFrag<RTKV_BF16> {
   }
 };
 
-constexpr int kLRows = 64;  // query rows per workgroup, and key rows per tile
+constexpr int kLRows = 128;  // query rows per workgroup (4 waves × 2 groups of 16)
+constexpr int kLKeys = 64;   // key rows per tile
 constexpr float kLSlack = 8.f;
 
 struct LseArgs {
@@ -60,7 +62,7 @@ __global__ __launch_bounds__(256) void attn_lse_kernel(LseArgs g) {
   constexpr int RB = 2 * D;                  // bytes per key row
   constexpr int CH = RB / 16;                // 16-byte chunks per row
   constexpr int RPI = 1024 / RB;             // rows per DMA wave-instruction
-  constexpr int TILE = kLRows * RB;          // bytes per key tile
+  constexpr int TILE = kLKeys * RB;          // bytes per key tile
   constexpr int KI = TILE / 1024 / 4;        // DMA instructions per wave per tile
   extern __shared__ __attribute__((aligned(1024))) uint8_t lds[];  // 2 × TILE
   const rtkv_qk_desc& q = g.q;
@@ -71,14 +73,13 @@ __global__ __launch_bounds__(256) void attn_lse_kernel(LseArgs g) {
   const int h = blockIdx.y, b = blockIdx.z;
   const int S = (int)q.S, grp = (int)(q.H / q.Hkv);
   const int i0 = qb * kLRows;
-  const int wrow0 = i0 + wave * 16;
-  const int crow0 = wrow0 + 4 * kg;          // accumulator rows crow0 + r
+  const int wrow0 = i0 + wave * 32;          // the wave's rows: two groups of 16 from here
   const float sc = q.scale * 1.4426950408889634f;
   const S_* Kh = static_cast<const S_*>(q.k_dev) + b * q.k_stride_b + (int64_t)(h / grp) * q.k_stride_h;
   // key rows this block needs: causal → up to its last query row (global position row0 + i)
   int64_t kend = q.causal ? q.row0 + i0 + kLRows : S;
   if (kend > S) kend = S;
-  const int ntiles = (int)((kend + kLRows - 1) / kLRows);
+  const int ntiles = (int)((kend + kLKeys - 1) / kLKeys);
   const int lrow = lane / CH, lpc = lane % CH;
   auto issue = [&](int kt) {
     uint8_t* st = lds + (kt & 1) * TILE;
@@ -86,26 +87,30 @@ __global__ __launch_bounds__(256) void attn_lse_kernel(LseArgs g) {
     for (int k = 0; k < KI; ++k) {
       const int r = (wave * KI + k) * RPI + lrow;
       const int c = lpc ^ (r & (CH - 1));
-      int kr = kt * kLRows + r;
+      int kr = kt * kLKeys + r;
       kr = kr < S ? kr : S - 1;              // rows past S: any valid row (masked)
       lds_dma16(Kh + (int64_t)kr * q.k_stride_s + c * 8, st + (wave * KI + k) * 1024);
     }
   };
-  // the wave's 16 query rows, A fragments straight from global (once)
-  FT a[KS];
-  {
-    const int qr = wrow0 + c16 < S ? wrow0 + c16 : S - 1;
+  // the wave's 32 query rows, A fragments straight from global (once); each key fragment read from
+  // LDS feeds both row groups (half the LDS traffic per flop of one group per wave)
+  FT a[2][KS];
+#pragma unroll
+  for (int rg = 0; rg < 2; ++rg) {
+    const int qr = wrow0 + 16 * rg + c16 < S ? wrow0 + 16 * rg + c16 : S - 1;
     const S_* qrow = static_cast<const S_*>(q.q_dev) + b * q.q_stride_b + (int64_t)h * q.q_stride_h +
                      (int64_t)qr * q.q_stride_s;
 #pragma unroll
-    for (int s_ = 0; s_ < KS; ++s_) a[s_] = *reinterpret_cast<const FT*>(qrow + (4 * s_ + kg) * 8);
+    for (int s_ = 0; s_ < KS; ++s_) a[rg][s_] = *reinterpret_cast<const FT*>(qrow + (4 * s_ + kg) * 8);
   }
-  float m[4], l[4];
+  float m[2][4], l[2][4];
 #pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    m[r] = -INFINITY;
-    l[r] = 0.f;
-  }
+  for (int rg = 0; rg < 2; ++rg)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      m[rg][r] = -INFINITY;
+      l[rg][r] = 0.f;
+    }
   issue(0);
   for (int kt = 0; kt < ntiles; ++kt) {
     __builtin_amdgcn_s_barrier();  // every wave is done with tile kt-1: its slot is free
@@ -117,63 +122,76 @@ __global__ __launch_bounds__(256) void attn_lse_kernel(LseArgs g) {
     }
     __builtin_amdgcn_s_barrier();  // ... and every other wave's pieces of tile kt
     const uint8_t* st = lds + (kt & 1) * TILE;
-    f32x4 acc[4];
+    f32x4 acc[2][4];
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
-      acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+      acc[0][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+      acc[1][t] = f32x4{0.f, 0.f, 0.f, 0.f};
       const int kr = 16 * t + c16;
       const uint8_t* krow = st + kr * RB;
 #pragma unroll
       for (int s_ = 0; s_ < KS; ++s_) {
         const FT bf = *reinterpret_cast<const FT*>(krow + (((4 * s_ + kg) ^ (kr & (CH - 1))) * 16));
-        acc[t] = LFrag<DT>::mfma(a[s_], bf, acc[t]);
+        acc[0][t] = LFrag<DT>::mfma(a[0][s_], bf, acc[0][t]);
+        acc[1][t] = LFrag<DT>::mfma(a[1][s_], bf, acc[1][t]);
       }
     }
-    // logits in the exp2 domain; mask keys past S and (causal) past the query position
-    const bool edge = (int64_t)(kt + 1) * kLRows > (q.causal ? q.row0 + wrow0 : (int64_t)S) || (kt + 1) * kLRows > S;
-    float v[4][4];
+    bool up = false;
+    float v[2][4][4], mt[2][4];
 #pragma unroll
-    for (int t = 0; t < 4; ++t)
+    for (int rg = 0; rg < 2; ++rg) {
+      const int grow0 = wrow0 + 16 * rg;      // first row of the group
+      const int crow0 = grow0 + 4 * kg;       // accumulator rows crow0 + r
+      // logits in the exp2 domain; mask keys past S and (causal) past the query position
+      const bool edge = (int64_t)(kt + 1) * kLKeys > (q.causal ? q.row0 + grow0 : (int64_t)S) || (kt + 1) * kLKeys > S;
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          float x = acc[rg][t][r] * sc;
+          if (edge) {
+            const int j = kt * kLKeys + 16 * t + c16;
+            const bool ok = j < S && (!q.causal || (int64_t)j <= q.row0 + crow0 + r);
+            x = ok ? x : -INFINITY;
+          }
+          v[rg][t][r] = x;
+        }
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        float x = acc[t][r] * sc;
-        if (edge) {
-          const int j = kt * kLRows + 16 * t + c16;
-          const bool ok = j < S && (!q.causal || (int64_t)j <= q.row0 + crow0 + r);
-          x = ok ? x : -INFINITY;
-        }
-        v[t][r] = x;
+        mt[rg][r] = fmaxf(fmaxf(v[rg][0][r], v[rg][1][r]), fmaxf(v[rg][2][r], v[rg][3][r]));
+        up |= mt[rg][r] > m[rg][r] + kLSlack;
       }
-    bool up = false;
-    float mt[4];
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      mt[r] = fmaxf(fmaxf(v[0][r], v[1][r]), fmaxf(v[2][r], v[3][r]));
-      up |= mt[r] > m[r] + kLSlack;
     }
     if (__ballot(up)) {
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const float mn = mt[r] > m[r] + kLSlack ? mt[r] : m[r];
-        l[r] *= (m[r] == -INFINITY) ? 0.f : __builtin_amdgcn_exp2f(m[r] - mn);
-        m[r] = mn;
-      }
+      for (int rg = 0; rg < 2; ++rg)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float mn = mt[rg][r] > m[rg][r] + kLSlack ? mt[rg][r] : m[rg][r];
+          l[rg][r] *= (m[rg][r] == -INFINITY) ? 0.f : __builtin_amdgcn_exp2f(m[rg][r] - mn);
+          m[rg][r] = mn;
+        }
     }
 #pragma unroll
-    for (int r = 0; r < 4; ++r)
+    for (int rg = 0; rg < 2; ++rg)
 #pragma unroll
-      for (int t = 0; t < 4; ++t) l[r] += (m[r] == -INFINITY) ? 0.f : __builtin_amdgcn_exp2f(v[t][r] - m[r]);
+      for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+          l[rg][r] += (m[rg][r] == -INFINITY) ? 0.f : __builtin_amdgcn_exp2f(v[rg][t][r] - m[rg][r]);
   }
   // combine the 16 lanes holding each row: M = max m, L = Σ l·2^(m − M); lse = (M + log2 L)·ln 2
 #pragma unroll
+  for (int rg = 0; rg < 2; ++rg)
+#pragma unroll
   for (int r = 0; r < 4; ++r) {
-    float M = m[r];
+    float M = m[rg][r];
 #pragma unroll
     for (int o = 1; o < 16; o <<= 1) M = fmaxf(M, __shfl_xor(M, o, 64));
-    float L = (m[r] == -INFINITY) ? 0.f : l[r] * __builtin_amdgcn_exp2f(m[r] - M);
+    float L = (m[rg][r] == -INFINITY) ? 0.f : l[rg][r] * __builtin_amdgcn_exp2f(m[rg][r] - M);
 #pragma unroll
     for (int o = 1; o < 16; o <<= 1) L += __shfl_xor(L, o, 64);
-    const int i = crow0 + r;
+    const int i = wrow0 + 16 * rg + 4 * kg + r;
     if (c16 == 0 && i < S)
       g.lse[b * q.lse_stride_b + (int64_t)h * q.lse_stride_h + i] =
           L > 0.f ? (M + __log2f(L)) * 0.6931471805599453f : -INFINITY;
@@ -182,7 +200,7 @@ __global__ __launch_bounds__(256) void attn_lse_kernel(LseArgs g) {
 
 template <int DT, int KS>
 int launch_lse_tpl(const LseArgs& a, dim3 grid, hipStream_t st) {
-  constexpr size_t lds = 2 * (size_t)kLRows * (64 * KS);
+  constexpr size_t lds = 2 * (size_t)kLKeys * (64 * KS);
   hipLaunchKernelGGL((attn_lse_kernel<DT, KS>), grid, dim3(256), lds, st, a);
   RTKV_HIP_CHECK(hipGetLastError());
   return RTKV_OK;
