@@ -355,9 +355,11 @@ int rtkv_unpack_dequant(const uint8_t* packed_dev, const int64_t* row_offset_dev
  * rtkv_unpack_dequant (H = Hkv kv heads of head_dim D, F = Hkv·D a multiple of 512;
  * packed field widths 2/4/8/16), plus q [B, Hq, D] in the K/V dtype (Hq a multiple of Hkv: GQA),
  * scale (1/sqrt(D) in the reference, modified_llama.py:89) and out [B, Hq, D] fp32.  Workspace:
- * rtkv_decode_workspace_size(B, Hq, Hkv, D, row_capacity) bytes. */
+ * rtkv_decode_workspace_size(B, Hq, Hkv, D, row_capacity) bytes.  packed_bytes = size of each code
+ * buffer: a row whose offset + F·w/8 passes it reads as zero codes, rows[b] is clamped to
+ * row_capacity and kept indices to [0, S), so inconsistent metadata cannot read outside the buffers. */
 size_t rtkv_decode_workspace_size(int64_t B, int64_t Hq, int64_t Hkv, int64_t D, int64_t row_capacity);
-int rtkv_decode_attention_packed(const uint8_t* packed_k_dev, const uint8_t* packed_v_dev,
+int rtkv_decode_attention_packed(const uint8_t* packed_k_dev, const uint8_t* packed_v_dev, int64_t packed_bytes,
                                  const int64_t* row_offset_dev, const float* scale_zp_dev,
                                  const int32_t* kept_index_dev, const uint8_t* labels_dev, int64_t B, int64_t S,
                                  int64_t row_capacity, const int64_t* rows_dev, int64_t Hkv, int64_t D, int dtype,

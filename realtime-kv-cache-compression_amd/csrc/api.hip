@@ -410,14 +410,15 @@ size_t rtkv_decode_workspace_size(int64_t B, int64_t Hq, int64_t Hkv, int64_t D,
   return decode_workspace_bytes(B, Hq, Hkv, D, row_capacity);
 }
 
-int rtkv_decode_attention_packed(const uint8_t* packed_k_dev, const uint8_t* packed_v_dev, const int64_t* row_offset_dev,
+int rtkv_decode_attention_packed(const uint8_t* packed_k_dev, const uint8_t* packed_v_dev, int64_t packed_bytes,
+                                 const int64_t* row_offset_dev,
                                  const float* scale_zp_dev, const int32_t* kept_index_dev, const uint8_t* labels_dev,
                                  int64_t B, int64_t S, int64_t row_capacity, const int64_t* rows_dev, int64_t Hkv,
                                  int64_t D, int dtype, const int32_t bits[3], const void* q_dev, int64_t Hq,
                                  float scale, float* out_dev, void* workspace_dev, size_t workspace_bytes,
                                  void* stream) {
   RTKV_REQUIRE(bits != nullptr, "null bits");
-  return launch_decode(packed_k_dev, packed_v_dev, row_offset_dev, scale_zp_dev, kept_index_dev, labels_dev, B, S,
+  return launch_decode(packed_k_dev, packed_v_dev, packed_bytes, row_offset_dev, scale_zp_dev, kept_index_dev, labels_dev, B, S,
                        row_capacity, rows_dev, Hkv, D, dtype, bits, q_dev, Hq, scale, out_dev, workspace_dev,
                        workspace_bytes, (hipStream_t)stream);
 }

@@ -265,7 +265,8 @@ int launch_unpack(const uint8_t* packed, const int64_t* row_offset, const float*
                   int64_t ob, int64_t os, int64_t oh, hipStream_t st);
 
 size_t decode_workspace_bytes(int64_t B, int64_t Hq, int64_t Hkv, int64_t D, int64_t cap);
-int launch_decode(const uint8_t* codes_k, const uint8_t* codes_v, const int64_t* row_offset, const float* scale_zp,
+int launch_decode(const uint8_t* codes_k, const uint8_t* codes_v, int64_t codes_bytes, const int64_t* row_offset,
+                  const float* scale_zp,
                   const int32_t* kept_index, const uint8_t* labels, int64_t B, int64_t S, int64_t cap,
                   const int64_t* rows, int64_t Hkv, int64_t D, int dt, const int32_t bits[3], const void* q,
                   int64_t Hq, float scale, float* out, void* ws, size_t ws_bytes, hipStream_t st);

@@ -36,6 +36,7 @@ constexpr float kSlack = 8.f;  // lazy rescale: running max may trail the row ma
 struct DecodeArgs {
   const uint8_t* codes_k;
   const uint8_t* codes_v;
+  int64_t codes_bytes;        // size of each code buffer
   const int64_t* row_offset;  // [B, cap]
   const float* scale_zp;      // [B, cap, 4]
   const int32_t* kept_index;  // [B, cap]
@@ -167,7 +168,7 @@ __global__ __launch_bounds__(64 * kDW) void decode_split_kernel(DecodeArgs a) {
   const int s = rest % a.splits, t1 = rest / a.splits, hg = t1 % a.HG, b = t1 / a.HG;
   const int F = a.HG * NCH * 512, D = a.D, lph = D / 8;  // lanes per head within one chunk column
   const int c0 = hg * NCH * 64;                            // first chunk of this head group
-  const int64_t nrows = a.rows[b];
+  const int64_t nrows = a.rows[b] < a.cap ? (a.rows[b] > 0 ? a.rows[b] : 0) : a.cap;
   const int64_t per = (nrows + a.splits - 1) / a.splits;
   const int64_t r0 = (int64_t)s * per, r1 = r0 + per < nrows ? r0 + per : nrows;
   const int Hq = a.Hkv * a.G;
@@ -301,7 +302,8 @@ __global__ __launch_bounds__(64 * kDW) void decode_split_kernel(DecodeArgs a) {
     const int64_t jr = jb + (int64_t)kDW * lane;
     const bool ok = jr < r1;
     const int64_t rj = (int64_t)b * a.cap + (ok ? jr : jb);
-    const int ki = a.kept_index[rj];
+    const int ki0 = a.kept_index[rj];
+    const int ki = ki0 < 0 ? 0 : (ki0 >= a.S ? (int)a.S - 1 : ki0);
     const int64_t off = a.row_offset[rj];
     const float4 sz = *reinterpret_cast<const float4*>(a.scale_zp + rj * 4);
     const int lab = a.labels[(int64_t)b * a.S + ki];
@@ -325,7 +327,8 @@ __global__ __launch_bounds__(64 * kDW) void decode_split_kernel(DecodeArgs a) {
       auto issue = [&](int t, ChunkCodes<W> (&xk)[NCH], ChunkCodes<W> (&xv)[NCH]) {
         const int64_t o = (int64_t)(((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)off_hi, t) << 32) |
                                     (uint32_t)__builtin_amdgcn_readlane((int)off_lo, t));
-        const int nb = (F / 8) * W;
+        const int64_t nbr = (int64_t)(F / 8) * W;
+        const int nb = (o >= 0 && o + nbr <= a.codes_bytes) ? (int)nbr : 0;  // out of range: zero codes
         const auto sk = __builtin_amdgcn_make_buffer_rsrc((void*)(a.codes_k + o), (short)0, nb, 0x00020000);
         const auto sv = __builtin_amdgcn_make_buffer_rsrc((void*)(a.codes_v + o), (short)0, nb, 0x00020000);
 #pragma unroll
@@ -494,7 +497,8 @@ size_t decode_workspace_bytes(int64_t B, int64_t Hq, int64_t Hkv, int64_t D, int
   return (size_t)(B * G * s) * (size_t)(2 * Hkv + Hkv * D) * sizeof(float) + 256;
 }
 
-int launch_decode(const uint8_t* codes_k, const uint8_t* codes_v, const int64_t* row_offset, const float* scale_zp,
+int launch_decode(const uint8_t* codes_k, const uint8_t* codes_v, int64_t codes_bytes, const int64_t* row_offset,
+                  const float* scale_zp,
                   const int32_t* kept_index, const uint8_t* labels, int64_t B, int64_t S, int64_t cap,
                   const int64_t* rows, int64_t Hkv, int64_t D, int dt, const int32_t bits[3], const void* q,
                   int64_t Hq, float scale, float* out, void* ws, size_t ws_bytes, hipStream_t st) {
@@ -517,7 +521,8 @@ int launch_decode(const uint8_t* codes_k, const uint8_t* codes_v, const int64_t*
   RTKV_REQUIRE(((uintptr_t)q & 15) == 0 && ((uintptr_t)scale_zp & 15) == 0, "decode: q and scale_zp must be 16-byte aligned");
   const int splits = decode_splits(B, G, F, cap);
   RTKV_REQUIRE(ws && ws_bytes >= decode_workspace_bytes(B, Hq, Hkv, D, cap), "decode: workspace too small");
-  a.codes_k = codes_k; a.codes_v = codes_v; a.row_offset = row_offset; a.scale_zp = scale_zp;
+  RTKV_REQUIRE(codes_bytes >= 0, "decode: negative code buffer size");
+  a.codes_k = codes_k; a.codes_v = codes_v; a.codes_bytes = codes_bytes; a.row_offset = row_offset; a.scale_zp = scale_zp;
   a.kept_index = kept_index; a.labels = labels; a.rows = rows;
   a.S = S; a.cap = cap; a.Hkv = (int)Hkv; a.D = (int)D; a.G = (int)G;
   a.q = q; a.scale = scale * 1.4426950408889634f; a.splits = splits;

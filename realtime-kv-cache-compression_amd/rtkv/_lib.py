@@ -104,7 +104,7 @@ _SIGS = {
     "rtkv_compress_layer_qk_events": ([c_p, c_p, c_p, c_p, c_p, c_sz, c_p, c_p], c_i32),
     "rtkv_gather_rows": ([c_p, c_i64, c_i64, c_i64, c_p, c_i64, c_i64, c_p, c_i64, c_i64, c_p, c_p], c_i32),
     "rtkv_decode_workspace_size": ([c_i64, c_i64, c_i64, c_i64, c_i64], c_sz),
-    "rtkv_decode_attention_packed": ([c_p, c_p, c_p, c_p, c_p, c_p, c_i64, c_i64, c_i64, c_p, c_i64, c_i64, c_i32, c_p,
+    "rtkv_decode_attention_packed": ([c_p, c_p, c_i64, c_p, c_p, c_p, c_p, c_i64, c_i64, c_i64, c_p, c_i64, c_i64, c_i32, c_p,
                                       c_p, c_i64, ctypes.c_float, c_p, c_p, c_sz, c_p], c_i32),
 }
 EXPORTS = tuple(_SIGS)

@@ -215,7 +215,12 @@ def decode_attention(p: dict, q: torch.Tensor, num_kv_heads: int, scale: Optiona
     qc = q.contiguous()
     ws = torch.empty(L.lib().rtkv_decode_workspace_size(B, Hq, num_kv_heads, D, Sp), dtype=torch.uint8, device=dev)
     sc = float(scale) if scale is not None else 1.0 / float(D) ** 0.5
-    L.check(L.lib().rtkv_decode_attention_packed(codes_k.data_ptr(), codes_v.data_ptr(), row_offset.data_ptr(),
+    if codes_k.numel() != codes_v.numel():
+        raise ValueError("codes_k and codes_v differ in size")
+    if any(int(r) < 0 or int(r) > Sp for r in p["rows"]):
+        raise ValueError(f"row counts {p['rows']} outside [0, {Sp}]")
+    L.check(L.lib().rtkv_decode_attention_packed(codes_k.data_ptr(), codes_v.data_ptr(), codes_k.numel(),
+                                                 row_offset.data_ptr(),
                                                  scale_zp.data_ptr(), kept_index.data_ptr(), labels.data_ptr(), B, S,
                                                  Sp, rows.data_ptr(), num_kv_heads, D, L.TORCH_DTYPE_CODE[q.dtype],
                                                  bits, qc.data_ptr(), Hq, sc, out.data_ptr(), ws.data_ptr(),

@@ -129,3 +129,30 @@ def test_packed_file_round_trip_decodes_identically(tmp_path):
     assert torch.equal(dk, k2) and torch.equal(dv, v2)
     q = dev(synth.cast(synth.normal(10, (B, Hq, D)), dtype), dtype)
     assert torch.equal(rtkv.decode_attention(back, q, Hkv), rtkv.decode_attention(info["packed"], q, Hkv))
+
+
+def test_decode_inconsistent_metadata_stays_in_bounds():
+    """Offsets past the code buffer read as zero codes and kept indices are clamped: the kernel
+    never reads outside its buffers (the result is finite, the GPU does not fault)."""
+    import rtkv
+    S, Hkv, D = 800, 4, 128
+    K, V = synth.kv(4, 1, S, Hkv * D, "float16")
+    W = synth.attention_slice(4, 1, 4, S, rtkv.prompt_length(S), "float16")
+    comp = rtkv.RealTimePrefillCompressor(rtkv.CompressionConfig(num_hidden_layers=4, low_precision_bits=2,
+                                                                 medium_precision_bits=4, high_precision_bits=8, **COV))
+    ids = torch.zeros(1, S, dtype=torch.long, device="cuda")
+    _, _, info = comp.compress_layer_kv_cache(dev(K, "float16"), dev(V, "float16"), dev(W, "float16"), ids, 1)
+    pk = dict(info["packed"])
+    pk["row_offset"] = pk["row_offset"].clone()
+    pk["row_offset"][0, :5] = 1 << 40
+    pk["kept_index"] = pk["kept_index"].clone()
+    pk["kept_index"][0, 5:9] = 1 << 30
+    pk.pop("_rows_dev", None)
+    q = torch.randn(1, 8, D, device="cuda").half()
+    out = rtkv.decode_attention(pk, q, Hkv)
+    torch.cuda.synchronize()
+    assert torch.isfinite(out).all()
+    bad = dict(pk, rows=[pk["kept_index"].shape[1] + 1])
+    bad.pop("_rows_dev", None)
+    with pytest.raises(ValueError):
+        rtkv.decode_attention(bad, q, Hkv)
