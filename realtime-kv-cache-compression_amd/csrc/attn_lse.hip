@@ -43,6 +43,7 @@ template <> struct LFrag<RTKV_BF16> {
 constexpr int kLRows = 128;  // query rows per workgroup (4 waves × 2 groups of 16)
 constexpr int kLKeys = 64;   // key rows per tile
 constexpr float kLSlack = 8.f;
+constexpr float kLFloor = -1e30f;  // initial running max
 
 struct LseArgs {
   rtkv_qk_desc q;
@@ -108,9 +109,54 @@ __global__ __launch_bounds__(256) void attn_lse_kernel(LseArgs g) {
   for (int rg = 0; rg < 2; ++rg)
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      m[rg][r] = -INFINITY;
+      m[rg][r] = kLFloor;  // finite: exp2(-inf − m) = 0 and no −inf − (−inf)
       l[rg][r] = 0.f;
     }
+  // running (max, sum) update with the logits of tile kt: mask keys past S and (causal) past the
+  // query position (edge tiles only), then one FMA + exp2 + add per logit in the exp2 domain
+  auto update = [&](f32x4 (&acc)[2][4], int kt) {
+    bool up = false;
+    float mt[2][4];
+#pragma unroll
+    for (int rg = 0; rg < 2; ++rg) {
+      const int grow0 = wrow0 + 16 * rg;      // first row of the group
+      const int crow0 = grow0 + 4 * kg;       // accumulator rows crow0 + r
+      const bool edge = (int64_t)(kt + 1) * kLKeys > (q.causal ? q.row0 + grow0 : (int64_t)S) || (kt + 1) * kLKeys > S;
+      if (edge) {
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int j = kt * kLKeys + 16 * t + c16;
+            const bool ok = j < S && (!q.causal || (int64_t)j <= q.row0 + crow0 + r);
+            acc[rg][t][r] = ok ? acc[rg][t][r] : -INFINITY;
+          }
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        mt[rg][r] = fmaxf(fmaxf(acc[rg][0][r], acc[rg][1][r]), fmaxf(acc[rg][2][r], acc[rg][3][r])) * sc;
+        up |= mt[rg][r] > m[rg][r] + kLSlack;
+      }
+    }
+    if (__ballot(up)) {
+#pragma unroll
+      for (int rg = 0; rg < 2; ++rg)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float mn = mt[rg][r] > m[rg][r] + kLSlack ? mt[rg][r] : m[rg][r];
+          l[rg][r] *= __builtin_amdgcn_exp2f(m[rg][r] - mn);
+          m[rg][r] = mn;
+        }
+    }
+#pragma unroll
+    for (int rg = 0; rg < 2; ++rg)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float nm = -m[rg][r];
+#pragma unroll
+        for (int t = 0; t < 4; ++t) l[rg][r] += __builtin_amdgcn_exp2f(__builtin_fmaf(acc[rg][t][r], sc, nm));
+      }
+  };
   issue(0);
   for (int kt = 0; kt < ntiles; ++kt) {
     __builtin_amdgcn_s_barrier();  // every wave is done with tile kt-1: its slot is free
@@ -136,49 +182,7 @@ __global__ __launch_bounds__(256) void attn_lse_kernel(LseArgs g) {
         acc[1][t] = LFrag<DT>::mfma(a[1][s_], bf, acc[1][t]);
       }
     }
-    bool up = false;
-    float v[2][4][4], mt[2][4];
-#pragma unroll
-    for (int rg = 0; rg < 2; ++rg) {
-      const int grow0 = wrow0 + 16 * rg;      // first row of the group
-      const int crow0 = grow0 + 4 * kg;       // accumulator rows crow0 + r
-      // logits in the exp2 domain; mask keys past S and (causal) past the query position
-      const bool edge = (int64_t)(kt + 1) * kLKeys > (q.causal ? q.row0 + grow0 : (int64_t)S) || (kt + 1) * kLKeys > S;
-#pragma unroll
-      for (int t = 0; t < 4; ++t)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          float x = acc[rg][t][r] * sc;
-          if (edge) {
-            const int j = kt * kLKeys + 16 * t + c16;
-            const bool ok = j < S && (!q.causal || (int64_t)j <= q.row0 + crow0 + r);
-            x = ok ? x : -INFINITY;
-          }
-          v[rg][t][r] = x;
-        }
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        mt[rg][r] = fmaxf(fmaxf(v[rg][0][r], v[rg][1][r]), fmaxf(v[rg][2][r], v[rg][3][r]));
-        up |= mt[rg][r] > m[rg][r] + kLSlack;
-      }
-    }
-    if (__ballot(up)) {
-#pragma unroll
-      for (int rg = 0; rg < 2; ++rg)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const float mn = mt[rg][r] > m[rg][r] + kLSlack ? mt[rg][r] : m[rg][r];
-          l[rg][r] *= (m[rg][r] == -INFINITY) ? 0.f : __builtin_amdgcn_exp2f(m[rg][r] - mn);
-          m[rg][r] = mn;
-        }
-    }
-#pragma unroll
-    for (int rg = 0; rg < 2; ++rg)
-#pragma unroll
-      for (int r = 0; r < 4; ++r)
-#pragma unroll
-        for (int t = 0; t < 4; ++t)
-          l[rg][r] += (m[rg][r] == -INFINITY) ? 0.f : __builtin_amdgcn_exp2f(v[rg][t][r] - m[rg][r]);
+    update(acc, kt);
   }
   // combine the 16 lanes holding each row: M = max m, L = Σ l·2^(m − M); lse = (M + log2 L)·ln 2
 #pragma unroll
@@ -188,7 +192,7 @@ __global__ __launch_bounds__(256) void attn_lse_kernel(LseArgs g) {
     float M = m[rg][r];
 #pragma unroll
     for (int o = 1; o < 16; o <<= 1) M = fmaxf(M, __shfl_xor(M, o, 64));
-    float L = (m[rg][r] == -INFINITY) ? 0.f : l[rg][r] * __builtin_amdgcn_exp2f(m[rg][r] - M);
+    float L = l[rg][r] * __builtin_amdgcn_exp2f(m[rg][r] - M);
 #pragma unroll
     for (int o = 1; o < 16; o <<= 1) L += __shfl_xor(L, o, 64);
     const int i = wrow0 + 16 * rg + 4 * kg + r;
@@ -214,6 +218,7 @@ int launch_attention_lse(const rtkv_qk_desc& q, float* lse, hipStream_t st) {
                "attention_lse: bad shape");
   RTKV_REQUIRE(q.H % q.Hkv == 0, "attention_lse: H must be a multiple of Hkv");
   RTKV_REQUIRE(q.D == 64 || q.D == 128, "attention_lse: head_dim must be 64 or 128");
+  RTKV_REQUIRE(q.scale > 0.f, "attention_lse: scale must be positive");
   RTKV_REQUIRE(q.dtype == RTKV_F16 || q.dtype == RTKV_BF16, "attention_lse: Q/K must be float16 or bfloat16");
   RTKV_REQUIRE(q.q_stride_s % 8 == 0 && q.q_stride_h % 8 == 0 && q.q_stride_b % 8 == 0 && q.k_stride_s % 8 == 0 &&
                    q.k_stride_h % 8 == 0 && q.k_stride_b % 8 == 0 && ((uintptr_t)q.q_dev % 16) == 0 &&
