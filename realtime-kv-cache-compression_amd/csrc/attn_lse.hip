@@ -7,16 +7,19 @@
 // materialising the [B,H,S,S] matrix.  fp32 accumulation; parity with a torch fp32 logsumexp is a
 // tolerance (tests/test_gpu_lse.py).
 //
-// Work decomposition (gfx950, wave64): a workgroup owns 128 query rows of one (b, h), 32 rows (two
-// groups of 16) per wave; it walks the key tiles of 64 rows up to the causal diagonal, each tile
-// staged in LDS by LDS-DMA (double-buffered, swizzled as in qk_importance.hip) and shared by the 4
-// waves.  Each wave computes its 32 × 64 logits with v_mfma_f32_16x16x32_{f16,bf16} (2 row groups ×
-// 4 column tiles × D/32 k-steps; each key fragment read from LDS feeds both row groups);
+// Work decomposition (gfx950, wave64): a workgroup owns 64·RG query rows of one (b, h), RG groups
+// of 16 rows per wave (RG = 1 by default); it walks the key tiles of 64 rows up to the causal
+// diagonal, each tile staged in LDS by LDS-DMA (double-buffered, swizzled as in qk_importance.hip)
+// and shared by the 4 waves.  Each wave computes its 16·RG × 64 logits with
+// v_mfma_f32_16x16x32_{f16,bf16} (RG row groups × 4 column tiles × D/32 k-steps; each key fragment
+// read from LDS feeds every row group);
 // every lane keeps a running (max, sum) per accumulator row over the key columns it holds, in the
 // exp2 domain with a lazily raised max (rescale only when a logit passes it by 8: one wave-uniform
 // branch per tile).  The 16 lanes of a row combine at the end.  Workgroups are issued longest-first
 // (the last query blocks carry the most key tiles).
 #include "common.h"
+
+#include <cstdlib>
 
 namespace rtkv {
 
@@ -40,7 +43,6 @@ template <> struct LFrag<RTKV_BF16> {
   }
 };
 
-constexpr int kLRows = 128;  // query rows per workgroup (4 waves × 2 groups of 16)
 constexpr int kLKeys = 64;   // key rows per tile
 constexpr float kLSlack = 8.f;
 constexpr float kLFloor = -1e30f;  // initial running max
@@ -55,8 +57,9 @@ __device__ __forceinline__ void lds_dma16(const void* g, void* lds_base) {
   __builtin_amdgcn_global_load_lds(g, (__attribute__((address_space(3))) void*)lds_base, 16, 0, 0);
 }
 
-template <int DT, int KS>
+template <int DT, int KS, int RG>
 __global__ __launch_bounds__(256) void attn_lse_kernel(LseArgs g) {
+  constexpr int kLRows = 64 * RG;            // query rows per workgroup (4 waves × RG groups of 16)
   using FT = typename LFrag<DT>::T;
   using S_ = typename Dt<DT>::S;
   constexpr int D = 32 * KS;
@@ -74,7 +77,7 @@ __global__ __launch_bounds__(256) void attn_lse_kernel(LseArgs g) {
   const int h = blockIdx.y, b = blockIdx.z;
   const int S = (int)q.S, grp = (int)(q.H / q.Hkv);
   const int i0 = qb * kLRows;
-  const int wrow0 = i0 + wave * 32;          // the wave's rows: two groups of 16 from here
+  const int wrow0 = i0 + wave * 16 * RG;     // the wave's rows: RG groups of 16 from here
   const float sc = q.scale * 1.4426950408889634f;
   const S_* Kh = static_cast<const S_*>(q.k_dev) + b * q.k_stride_b + (int64_t)(h / grp) * q.k_stride_h;
   // key rows this block needs: causal → up to its last query row (global position row0 + i)
@@ -95,18 +98,18 @@ __global__ __launch_bounds__(256) void attn_lse_kernel(LseArgs g) {
   };
   // the wave's 32 query rows, A fragments straight from global (once); each key fragment read from
   // LDS feeds both row groups (half the LDS traffic per flop of one group per wave)
-  FT a[2][KS];
+  FT a[RG][KS];
 #pragma unroll
-  for (int rg = 0; rg < 2; ++rg) {
+  for (int rg = 0; rg < RG; ++rg) {
     const int qr = wrow0 + 16 * rg + c16 < S ? wrow0 + 16 * rg + c16 : S - 1;
     const S_* qrow = static_cast<const S_*>(q.q_dev) + b * q.q_stride_b + (int64_t)h * q.q_stride_h +
                      (int64_t)qr * q.q_stride_s;
 #pragma unroll
     for (int s_ = 0; s_ < KS; ++s_) a[rg][s_] = *reinterpret_cast<const FT*>(qrow + (4 * s_ + kg) * 8);
   }
-  float m[2][4], l[2][4];
+  float m[RG][4], l[RG][4];
 #pragma unroll
-  for (int rg = 0; rg < 2; ++rg)
+  for (int rg = 0; rg < RG; ++rg)
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       m[rg][r] = kLFloor;  // finite: exp2(-inf − m) = 0 and no −inf − (−inf)
@@ -114,11 +117,11 @@ __global__ __launch_bounds__(256) void attn_lse_kernel(LseArgs g) {
     }
   // running (max, sum) update with the logits of tile kt: mask keys past S and (causal) past the
   // query position (edge tiles only), then one FMA + exp2 + add per logit in the exp2 domain
-  auto update = [&](f32x4 (&acc)[2][4], int kt) {
+  auto update = [&](f32x4 (&acc)[RG][4], int kt) {
     bool up = false;
-    float mt[2][4];
+    float mt[RG][4];
 #pragma unroll
-    for (int rg = 0; rg < 2; ++rg) {
+    for (int rg = 0; rg < RG; ++rg) {
       const int grow0 = wrow0 + 16 * rg;      // first row of the group
       const int crow0 = grow0 + 4 * kg;       // accumulator rows crow0 + r
       const bool edge = (int64_t)(kt + 1) * kLKeys > (q.causal ? q.row0 + grow0 : (int64_t)S) || (kt + 1) * kLKeys > S;
@@ -140,7 +143,7 @@ __global__ __launch_bounds__(256) void attn_lse_kernel(LseArgs g) {
     }
     if (__ballot(up)) {
 #pragma unroll
-      for (int rg = 0; rg < 2; ++rg)
+      for (int rg = 0; rg < RG; ++rg)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const float mn = mt[rg][r] > m[rg][r] + kLSlack ? mt[rg][r] : m[rg][r];
@@ -149,7 +152,7 @@ __global__ __launch_bounds__(256) void attn_lse_kernel(LseArgs g) {
         }
     }
 #pragma unroll
-    for (int rg = 0; rg < 2; ++rg)
+    for (int rg = 0; rg < RG; ++rg)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const float nm = -m[rg][r];
@@ -168,25 +171,25 @@ __global__ __launch_bounds__(256) void attn_lse_kernel(LseArgs g) {
     }
     __builtin_amdgcn_s_barrier();  // ... and every other wave's pieces of tile kt
     const uint8_t* st = lds + (kt & 1) * TILE;
-    f32x4 acc[2][4];
+    f32x4 acc[RG][4];
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
-      acc[0][t] = f32x4{0.f, 0.f, 0.f, 0.f};
-      acc[1][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int rg = 0; rg < RG; ++rg) acc[rg][t] = f32x4{0.f, 0.f, 0.f, 0.f};
       const int kr = 16 * t + c16;
       const uint8_t* krow = st + kr * RB;
 #pragma unroll
       for (int s_ = 0; s_ < KS; ++s_) {
         const FT bf = *reinterpret_cast<const FT*>(krow + (((4 * s_ + kg) ^ (kr & (CH - 1))) * 16));
-        acc[0][t] = LFrag<DT>::mfma(a[0][s_], bf, acc[0][t]);
-        acc[1][t] = LFrag<DT>::mfma(a[1][s_], bf, acc[1][t]);
+#pragma unroll
+        for (int rg = 0; rg < RG; ++rg) acc[rg][t] = LFrag<DT>::mfma(a[rg][s_], bf, acc[rg][t]);
       }
     }
     update(acc, kt);
   }
   // combine the 16 lanes holding each row: M = max m, L = Σ l·2^(m − M); lse = (M + log2 L)·ln 2
 #pragma unroll
-  for (int rg = 0; rg < 2; ++rg)
+  for (int rg = 0; rg < RG; ++rg)
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
     float M = m[rg][r];
@@ -202,12 +205,22 @@ __global__ __launch_bounds__(256) void attn_lse_kernel(LseArgs g) {
   }
 }
 
-template <int DT, int KS>
-int launch_lse_tpl(const LseArgs& a, dim3 grid, hipStream_t st) {
+template <int DT, int KS, int RG>
+int launch_lse_tpl(LseArgs a, const rtkv_qk_desc& q, hipStream_t st) {
   constexpr size_t lds = 2 * (size_t)kLKeys * (64 * KS);
-  hipLaunchKernelGGL((attn_lse_kernel<DT, KS>), grid, dim3(256), lds, st, a);
+  a.nblk = (int)((q.S + 64 * RG - 1) / (64 * RG));
+  const dim3 grid((unsigned)a.nblk, (unsigned)q.H, (unsigned)q.B);
+  hipLaunchKernelGGL((attn_lse_kernel<DT, KS, RG>), grid, dim3(256), lds, st, a);
   RTKV_HIP_CHECK(hipGetLastError());
   return RTKV_OK;
+}
+
+int lse_row_groups() {
+  static const int v = [] {  // tuning knob RTKV_LSE_RG (1 or 2 row groups of 16 per wave)
+    const char* e = std::getenv("RTKV_LSE_RG");
+    return e && std::atoi(e) == 2 ? 2 : 1;
+  }();
+  return v;
 }
 
 }  // namespace
@@ -228,11 +241,13 @@ int launch_attention_lse(const rtkv_qk_desc& q, float* lse, hipStream_t st) {
   LseArgs a;
   a.q = q;
   a.lse = lse;
-  a.nblk = (int)((q.S + kLRows - 1) / kLRows);
-  const dim3 grid((unsigned)a.nblk, (unsigned)q.H, (unsigned)q.B);
-  const int ks = (int)(q.D / 32);
-  if (q.dtype == RTKV_F16) return ks == 4 ? launch_lse_tpl<RTKV_F16, 4>(a, grid, st) : launch_lse_tpl<RTKV_F16, 2>(a, grid, st);
-  return ks == 4 ? launch_lse_tpl<RTKV_BF16, 4>(a, grid, st) : launch_lse_tpl<RTKV_BF16, 2>(a, grid, st);
+  const int ks = (int)(q.D / 32), rg = lse_row_groups();
+#define RTKV_L(DT, K, R) \
+  if (q.dtype == DT && ks == K && rg == R) return launch_lse_tpl<DT, K, R>(a, q, st);
+  RTKV_L(RTKV_F16, 4, 1) RTKV_L(RTKV_F16, 2, 1) RTKV_L(RTKV_BF16, 4, 1) RTKV_L(RTKV_BF16, 2, 1)
+  RTKV_L(RTKV_F16, 4, 2) RTKV_L(RTKV_F16, 2, 2) RTKV_L(RTKV_BF16, 4, 2) RTKV_L(RTKV_BF16, 2, 2)
+#undef RTKV_L
+  RTKV_REQUIRE(false, "attention_lse: unsupported configuration");
 }
 
 }  // namespace rtkv
