@@ -18,7 +18,8 @@
 // stay in flight per wave.  GQ query heads of a kv head (GQA) share every decoded chunk.  The D/8
 // lanes of one head reduce q·k with DPP adds; every lane keeps the online-softmax state (m, l) and
 // 8 value accumulators per (query head, chunk).  fp16 rows are dequantized with packed half2
-// arithmetic (bit-identical: each op of dequant<F16> is one rounded fp16 op).  The 8 waves merge in
+// arithmetic (bit-identical: each op of dequant<F16> is one rounded fp16 op), bf16 rows with
+// v_cvt_pk_bf16_f32 roundings and v_dot2_f32_bf16.  The 8 waves merge in
 // LDS; a second kernel merges the splits.
 #include "common.h"
 #include "quant_impl.h"
@@ -58,6 +59,18 @@ struct DecodeArgs {
 };
 
 using H2 = __attribute__((ext_vector_type(2))) _Float16;
+using B2 = __attribute__((ext_vector_type(2))) __bf16;
+
+// bf16: two fp32 values rounded to bf16 (v_cvt_pk_bf16_f32, round to nearest even: Dt<BF16>::rnd
+// for finite values) and back
+__device__ __forceinline__ B2 rnd_bf2(float a, float b) { return B2{(__bf16)a, (__bf16)b}; }
+__device__ __forceinline__ float bf_lo(B2 v) { return __builtin_bit_cast(float, __builtin_bit_cast(uint32_t, v) << 16); }
+__device__ __forceinline__ float bf_hi(B2 v) { return __builtin_bit_cast(float, __builtin_bit_cast(uint32_t, v) & 0xffff0000u); }
+// dequant<BF16> of a pair of codes: rnd(rnd(c − zp)·scale), each op rounded to bf16
+__device__ __forceinline__ B2 dequant_bf2(float c0, float c1, const RowParams& rp) {
+  const B2 d = rnd_bf2(c0 - rp.zp, c1 - rp.zp);
+  return rnd_bf2(bf_lo(d) * rp.scale, bf_hi(d) * rp.scale);
+}
 
 // Slot order of a chunk's 8 elements in registers.  fp16 works on element pairs (p, p + 4) — the
 // pairing the packed code layouts give with one shift per pair — so slot 2p holds element p and
@@ -158,6 +171,7 @@ template <int DT, int NCH, int GQ, int LPH>
 __global__ __launch_bounds__(64 * kDW) void decode_split_kernel(DecodeArgs a) {
   using S_ = typename Dt<DT>::S;
   constexpr bool kH = DT == RTKV_F16;
+  constexpr bool kB = DT == RTKV_BF16;
   constexpr int kU = GQ * NCH;    // (query head, chunk) units per lane
   extern __shared__ float lds[];  // [kDW][64][kU][10]: m, l, acc[8] per unit
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -174,6 +188,7 @@ __global__ __launch_bounds__(64 * kDW) void decode_split_kernel(DecodeArgs a) {
   const int Hq = a.Hkv * a.G;
   // q (fp16: half2 pairs in slot order; otherwise fp32), accumulators in slot order, m / l
   H2 qh[GQ][NCH][4];
+  B2 qb[GQ][NCH][4];
   float qf[GQ][NCH][8], acc[GQ][NCH][8], m[GQ][NCH], l[GQ][NCH];
 #pragma unroll
   for (int j = 0; j < GQ; ++j) {
@@ -190,6 +205,10 @@ __global__ __launch_bounds__(64 * kDW) void decode_split_kernel(DecodeArgs a) {
           const uint32_t lo = (w4[p >> 1] >> (16 * (p & 1))) & 0xffffu, hi2 = (w4[2 + (p >> 1)] >> (16 * (p & 1))) & 0xffffu;
           qh[j][k][p] = __builtin_bit_cast(H2, lo | (hi2 << 16));
         }
+      } else if constexpr (kB) {
+        const uint32_t w4[4] = {qc.a.x, qc.a.y, qc.a.z, qc.a.w};
+#pragma unroll
+        for (int p = 0; p < 4; ++p) qb[j][k][p] = __builtin_bit_cast(B2, w4[p]);  // elements (2p, 2p+1)
       } else {
         chunk_to_f32<DT>(qc, qf[j][k]);
       }
@@ -219,6 +238,19 @@ __global__ __launch_bounds__(64 * kDW) void decode_split_kernel(DecodeArgs a) {
           float d = 0.f;
 #pragma unroll
           for (int p = 0; p < 4; ++p) d = __builtin_amdgcn_fdot2(qh[j][k][p], kh[p], d, false);
+          sc[k][j] = d;
+        }
+      } else if constexpr (kB) {
+        float kc[8];
+        unpack8<W>(xk[k], kc);
+        B2 kb[4];
+#pragma unroll
+        for (int p = 0; p < 4; ++p) kb[p] = dequant_bf2(kc[2 * p], kc[2 * p + 1], rk);
+#pragma unroll
+        for (int j = 0; j < GQ; ++j) {
+          float d = 0.f;
+#pragma unroll
+          for (int p = 0; p < 4; ++p) d = __builtin_amdgcn_fdot2_f32_bf16(qb[j][k][p], kb[p], d, false);
           sc[k][j] = d;
         }
       } else {
@@ -280,6 +312,19 @@ __global__ __launch_bounds__(64 * kDW) void decode_split_kernel(DecodeArgs a) {
           for (int p = 0; p < 4; ++p) {
             acc[j][k][2 * p] = __builtin_fmaf(pw[j], (float)vh[p].x, acc[j][k][2 * p]);
             acc[j][k][2 * p + 1] = __builtin_fmaf(pw[j], (float)vh[p].y, acc[j][k][2 * p + 1]);
+          }
+        }
+      } else if constexpr (kB) {
+        float vc[8];
+        unpack8<W>(xv[k], vc);
+#pragma unroll
+        for (int p = 0; p < 4; ++p) {
+          const B2 vb = dequant_bf2(vc[2 * p], vc[2 * p + 1], rv);
+          const float v0 = bf_lo(vb), v1 = bf_hi(vb);
+#pragma unroll
+          for (int j = 0; j < GQ; ++j) {
+            acc[j][k][2 * p] = __builtin_fmaf(pw[j], v0, acc[j][k][2 * p]);
+            acc[j][k][2 * p + 1] = __builtin_fmaf(pw[j], v1, acc[j][k][2 * p + 1]);
           }
         }
       } else {

@@ -17,23 +17,26 @@ import rtkv  # noqa: E402
 import synth  # noqa: E402
 
 
+TD = {"float16": torch.float16, "bfloat16": torch.bfloat16}
+
+
 def dev(stored, dtype):
-    return torch.from_numpy(np.ascontiguousarray(stored, np.uint16).view(np.int16)).cuda().view(torch.float16)
+    return torch.from_numpy(np.ascontiguousarray(stored, np.uint16).view(np.int16)).cuda().view(TD[dtype])
 
 
-def run(S, Hkv, Hq, D=128, ratio=0.6, iters=200):
+def run(S, Hkv, Hq, dtype="float16", D=128, ratio=0.6, iters=200):
     F = Hkv * D
-    K, V = synth.kv(11, 1, S, F, "float16")
-    W = synth.attention_slice(11, 1, 8, S, rtkv.prompt_length(S), "float16")
+    K, V = synth.kv(11, 1, S, F, dtype)
+    W = synth.attention_slice(11, 1, 8, S, rtkv.prompt_length(S), dtype)
     cfg = rtkv.CompressionConfig(num_hidden_layers=4, low_precision_bits=2, medium_precision_bits=4,
                                  high_precision_bits=8, early_layer_ratio=ratio, middle_layer_ratio=ratio,
                                  later_layer_ratio=ratio)
     comp = rtkv.RealTimePrefillCompressor(cfg)
     ids = torch.zeros(1, S, dtype=torch.long, device="cuda")
-    k2, v2, info = comp.compress_layer_kv_cache(dev(K, "float16"), dev(V, "float16"), dev(W, "float16"), ids, 1)
+    k2, v2, info = comp.compress_layer_kv_cache(dev(K, dtype), dev(V, dtype), dev(W, dtype), ids, 1)
     pk = info["packed"]
     n = int(pk["rows"][0])
-    q = torch.randn(1, Hq, D, dtype=torch.float16, device="cuda")
+    q = torch.randn(1, Hq, D, device="cuda").to(TD[dtype])
     for _ in range(10):
         rtkv.decode_attention(pk, q, Hkv)
     torch.cuda.synchronize()
@@ -63,14 +66,15 @@ def run(S, Hkv, Hq, D=128, ratio=0.6, iters=200):
     torch.cuda.synchronize()
     us_d = e0.elapsed_time(e1) / iters * 1e3
     dense_by = 2 * n * Hq * D * 2
-    print(f"S={S} Hkv={Hkv} Hq={Hq}: kept {n}, packed {code_bytes/1e6:.2f} MB ({code_bytes*8/(2*n*F):.2f} bits/elem) "
+    print(f"S={S} Hkv={Hkv} Hq={Hq} {dtype}: kept {n}, packed {code_bytes/1e6:.2f} MB ({code_bytes*8/(2*n*F):.2f} bits/elem) "
           f"-> decode {us:.1f} us, {by/us/1e3:.0f} GB/s algorithmic | dense SDPA over K'/V' {us_d:.1f} us "
           f"({dense_by/1e6:.1f} MB, {dense_by/us_d/1e3:.0f} GB/s)", flush=True)
 
 
 if __name__ == "__main__":
     rtkv.build()
-    cases = ((16384, 32, 32), (32768, 32, 32), (16384, 8, 32), (131072, 8, 32), (131072, 8, 8), (32768, 32, 128))
+    cases = ((16384, 32, 32), (32768, 32, 32), (16384, 8, 32), (131072, 8, 32), (131072, 8, 8), (32768, 32, 128),
+             (32768, 32, 32, "bfloat16"), (131072, 8, 32, "bfloat16"))
     only = [int(x) for x in sys.argv[1].split(",")] if len(sys.argv) > 1 else range(len(cases))
     iters = int(sys.argv[2]) if len(sys.argv) > 2 else 200
     for i in only:
