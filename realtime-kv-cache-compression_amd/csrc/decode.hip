@@ -7,9 +7,9 @@
 // dynamic_quantization.py:124) — so a decode step reads F·w/8 bytes per kept row and tensor instead
 // of F·e: 2/4/8-bit rows move 1/8 .. 1/2 of the fp16 bytes.  Attention arithmetic is fp32.
 //
-// Work decomposition (flash-decoding): one workgroup of 8 waves per (split s, head group hg, batch
+// Work decomposition (flash-decoding): one workgroup of 4 waves per (split s, head group hg, batch
 // row b, query-head group gs).  Split s owns a contiguous range of kept rows; wave v takes rows
-// r0 + v + 8t.  The row's F = Hkv·D elements are 8-element chunks; head group hg covers chunks
+// r0 + v + 4t.  The row's F = Hkv·D elements are 8-element chunks; head group hg covers chunks
 // [hg·64·NCH, (hg+1)·64·NCH) (NCH = 1 or 2) and lane l owns chunks c = (hg·NCH + k)·64 + l, i.e. w
 // contiguous code bytes per chunk, so one wave instruction reads 64·w consecutive bytes of the row.
 // Per-row metadata (kept index → class → width, byte offset, scale/zero-points) is loaded for 64
@@ -19,8 +19,8 @@
 // lanes of one head reduce q·k with DPP adds; every lane keeps the online-softmax state (m, l) and
 // 8 value accumulators per (query head, chunk).  fp16 rows are dequantized with packed half2
 // arithmetic (bit-identical: each op of dequant<F16> is one rounded fp16 op), bf16 rows with
-// v_cvt_pk_bf16_f32 roundings and v_dot2_f32_bf16.  The 8 waves merge in
-// LDS; a second kernel merges the splits.
+// v_cvt_pk_bf16_f32 roundings and v_dot2_f32_bf16.  The 4 waves merge in LDS; a second kernel
+// merges the splits.
 #include "common.h"
 #include "quant_impl.h"
 
