@@ -161,14 +161,14 @@ __global__ __launch_bounds__(256) void qk_importance_kernel(QKArgs g) {
       }
     }
     const f32x4 lse = *reinterpret_cast<const f32x4*>(st + KEY_BYTES + Q_BYTES + wave * 64 + kg * 16);
-    float l2[4];
+    float nl2[4];  // −lse·log2(e): one FMA + exp2 + add per logit
 #pragma unroll
-    for (int r = 0; r < 4; ++r) l2[r] = lse[r] * l2e;
+    for (int r = 0; r < 4; ++r) nl2[r] = -lse[r] * l2e;
     if (!masked) {
 #pragma unroll
       for (int t = 0; t < NT; ++t)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) hs[t][r] += __builtin_amdgcn_exp2f(acc[t][r] * sc - l2[r]);
+        for (int r = 0; r < 4; ++r) hs[t][r] += __builtin_amdgcn_exp2f(__builtin_fmaf(acc[t][r], sc, nl2[r]));
     } else {
 #pragma unroll
       for (int t = 0; t < NT; ++t) {
@@ -177,7 +177,7 @@ __global__ __launch_bounds__(256) void qk_importance_kernel(QKArgs g) {
         for (int r = 0; r < 4; ++r) {
           const int i = crow0 + r;
           const bool ok = p < P && i < S && (!q.causal || (int64_t)p <= q.row0 + i);
-          const float w = __builtin_amdgcn_exp2f(acc[t][r] * sc - l2[r]);
+          const float w = __builtin_amdgcn_exp2f(__builtin_fmaf(acc[t][r], sc, nl2[r]));
           hs[t][r] += ok ? w : 0.f;
         }
       }
