@@ -100,9 +100,24 @@ def save_packed(layers: Dict[int, dict], path: str):
     save_file(tensors, path, metadata=meta)
 
 
+_TENSOR_DTYPES = {"codes_k": torch.uint8, "codes_v": torch.uint8, "row_offset": torch.int64,
+                  "scale_zp": torch.float32, "kept_index": torch.int32, "labels": torch.uint8}
+
+
+def _check_dtypes(where, p: dict):
+    """The kernels read these buffers with fixed element types; a wrong dtype would be misread or
+    read past its end."""
+    for name, dt in _TENSOR_DTYPES.items():
+        if p[name].dtype != dt:
+            raise ValueError(f"packed layer {where}: {name} must be {dt}, got {p[name].dtype}")
+
+
 def _check_packed(i: int, p: dict):
     def bad(msg):
         raise ValueError(f"packed layer {i}: {msg}")
+    _check_dtypes(i, p)
+    if p["kept_index"].dim() != 2:
+        bad("kept_index must be [B, S']")
     B, Sp = p["kept_index"].shape
     if p["row_offset"].shape != (B, Sp) or p["scale_zp"].shape != (B, Sp, 4) or p["labels"].dim() != 2 \
             or p["labels"].shape[0] != B:
@@ -203,7 +218,15 @@ def decode_attention(p: dict, q: torch.Tensor, num_kv_heads: int, scale: Optiona
     scale_zp = p["scale_zp"].contiguous()
     kept_index = p["kept_index"].contiguous()
     labels = p["labels"].contiguous()
+    _check_dtypes("decode", p)
+    # the kernel indexes every per-batch array by q's batch row: they must all have B rows
+    if kept_index.dim() != 2 or kept_index.shape[0] != B or len(p["rows"]) != B or labels.shape[0] != B \
+            or row_offset.shape[0] != B or scale_zp.shape[0] != B:
+        raise ValueError(f"q has {B} batch rows but the packed layer has {kept_index.shape[0]} "
+                         f"(rows {len(p['rows'])}, labels {labels.shape[0]})")
     Sp = kept_index.shape[1]
+    if row_offset.shape != (B, Sp) or scale_zp.shape != (B, Sp, 4):
+        raise ValueError("packed layer: row_offset / scale_zp shapes disagree with kept_index")
     S = labels.shape[1]
     out = torch.zeros(B, Hq, D, dtype=torch.float32, device=dev)
     if Sp == 0:
