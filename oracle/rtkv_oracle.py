@@ -172,7 +172,7 @@ def torch_logf(n: int) -> float:
 
 
 def compress_layer(K, V, kvdt, W, wdt, P, alpha, beta, gamma, w_l, theta_h, theta_m, bits, ratio,
-                   no_selection=False, packed=True):
+                   no_selection=False, packed=True, threads=1):
     """Full-layer oracle.  K,V [B,S,F]; W [B,H,S,cols].  Returns a dict of numpy outputs with the
     padded dequant K'/V' trimmed to [B, S'_max, F]."""
     K, V, W = _c(K), _c(V), _c(W)
@@ -200,7 +200,7 @@ def compress_layer(K, V, kvdt, W, wdt, P, alpha, beta, gamma, w_l, theta_h, thet
         f32(w_l), f32(theta_h), f32(theta_m), _ptr(b3), float(ratio), int(bool(no_selection)),
         _ptr(scores), _ptr(labels), _ptr(mask), _ptr(kept_index), _ptr(k_out), _ptr(v_out),
         _ptr(scale_zp), _ptr(pk), _ptr(pv), _ptr(row_offset), _ptr(kept), _ptr(units), _ptr(fb),
-        _ptr(cc), 1)
+        _ptr(cc), int(threads))
     assert smax >= 0, smax
     total = int(row_offset[-1, -1]) if B * S else 0
     if packed and B * S:

@@ -104,7 +104,13 @@ class Writer:
             if not allowed:
                 self.mismatches.append(f"{name}: {what}")
 
-    def finish(self):
+    def finish(self, merge: bool = False):
+        if merge:  # keep every other case, replace the regenerated ones in place
+            with open(os.path.join(OUT, "manifest.json")) as f:
+                old = json.load(f)["cases"]
+            new = {c["name"]: c for c in self.manifest}
+            merged = [new.pop(c["name"], c) for c in old]
+            self.manifest = merged + list(new.values())
         with open(os.path.join(OUT, "manifest.json"), "w") as f:
             json.dump(dict(torch=torch.__version__, capability=torch.backends.cpu.get_cpu_capability(),
                            threads=torch.get_num_threads(), cases=self.manifest), f, indent=1)
@@ -275,6 +281,13 @@ LAYER_CASES = [
     ("cfg2_quant", COVERAGE, 32, 0, 1, 32, 32, 128, 4096, "float16"),
     ("cfg5_13b_l39", COVERAGE, 40, 39, 1, 40, 40, 128, 8192, "bfloat16"),    # Llama-2-13B rows (F = 5120)
     ("cfg5_13b_l20", PUBLISHED, 40, 20, 1, 40, 40, 128, 4096, "float16"),
+    # round 2: BASELINE cfg5 at its real size (Llama-2-13B, F = 5120, global selection over S = 32768)
+    # and cfg3 in the reference model's own dtype (fp32, modified_llama.py:368)
+    ("cfg5_13b_s32768_l39", COVERAGE, 40, 39, 1, 40, 40, 128, 32768, "float16"),
+    ("cfg5_13b_s32768_l0", PUBLISHED, 40, 0, 1, 40, 40, 128, 32768, "bfloat16"),
+    ("cfg5_13b_s32768_l20", COVERAGE, 40, 20, 1, 40, 40, 128, 32768, "float32"),
+    ("cfg3_l0", COVERAGE, 32, 0, 1, 32, 32, 128, 16384, "float32"),
+    ("cfg3_l25", PUBLISHED, 32, 25, 1, 32, 32, 128, 16384, "float32"),
 ]
 
 
@@ -282,6 +295,8 @@ def gen_layers(w: Writer):
     seed = 700
     for (tag, params, L, layer, B, H, Hkv, D, S, dt) in LAYER_CASES:
         seed += 1
+        if not wanted(f"layer_{tag}_{dt}"):
+            continue
         t0 = time.time()
         F = Hkv * D
         P = max(1, min(S // 5, 128))
@@ -339,16 +354,93 @@ def gen_layers(w: Writer):
         print(f"  {name}: {time.time() - t0:.1f}s  S'={scal['max_selected']}  tie={tie}")
 
 
+# ----------------------------------------------------------------------------- multi-layer state
+# A sequence of layers through one compressor, then the aggregate API the reference's experiment
+# scripts and LongBench "TTFT" read: get_overall_compression_stats (unified_compressor.py:174-230),
+# get_cumulative_scores (token_importance.py:202-214) and reset_compression_state (:232-235).
+STATS_CASES = [
+    # name, params, L, processed layers (in call order), B, H, Hkv, D, S, dtype
+    ("stats_seq8", PUBLISHED, 8, list(range(8)), 2, 8, 4, 32, 1024, "float32"),
+    ("stats_sparse", COVERAGE, 12, [5, 0, 9, 2], 1, 4, 4, 64, 640, "float16"),
+]
+TIMING_KEYS = ("total_processing_time", "avg_processing_time_per_layer")
+
+
+def gen_stats(w: Writer):
+    seed = 900
+    for (name, params, L, layers, B, H, Hkv, D, S, dt) in STATS_CASES:
+        seed += 1
+        if not wanted(name):
+            continue
+        cfg = make_config(params, L)
+        comp = RealTimePrefillCompressor(cfg)
+        F = Hkv * D
+        P = max(1, min(S // 5, 128))
+        ids = torch.zeros((B, S), dtype=torch.long)
+        per_layer = []
+        for k, layer in enumerate(layers):
+            K, V = synth.kv(seed * 100 + k, B, S, F, dt)
+            Wt = synth.attention_slice(seed * 100 + k, B, H, S, P, dt)
+            _, _, info = comp.compress_layer_kv_cache(t_of(K, dt), t_of(V, dt), t_of(Wt, dt), ids, layer)
+            per_layer.append(dict(layer=layer, compressed_len=int(info["compressed_shape"][1]),
+                                  compression_ratio=info["compression_ratio"]))
+        overall = comp.get_overall_compression_stats()
+        for key in TIMING_KEYS:  # wall-clock sums: present, but not comparable across machines
+            assert key in overall
+            overall[key] = None
+        arrays = {}
+        queried = sorted(set(list(range(L)) + [L + 3]))
+        cum_none = []
+        for l in queried:
+            try:
+                c = comp.importance_tracker.get_cumulative_scores(l)
+            except KeyError:  # zeros_like(layer_scores[0]) when layer 0 was never processed
+                c = "KeyError"
+            if c is None or isinstance(c, str):
+                cum_none.append([l, c if isinstance(c, str) else None])
+            else:
+                arrays[f"cum_l{l}"] = c.numpy()
+        comp.reset_compression_state()
+        after = dict(overall=comp.get_overall_compression_stats(),
+                     cumulative=comp.importance_tracker.get_cumulative_scores(0),
+                     layer_states=len(comp.layer_states), layer_scores=len(comp.importance_tracker.layer_scores))
+        after["cumulative"] = None if after["cumulative"] is None else "tensor"
+        w.put(name, "stats", dict(seed=seed, params={k: v for k, v in cfg.__dict__.items()
+                                                     if k in ("alpha", "beta", "gamma", "theta_h", "theta_m")},
+                                  L=L, layers=layers, B=B, H=H, Hkv=Hkv, D=D, S=S, P=P, dtype=dt,
+                                  bits=[cfg.low_precision_bits, cfg.medium_precision_bits, cfg.high_precision_bits],
+                                  queried=queried),
+              arrays, dict(overall=overall, per_layer=per_layer, cumulative_special=cum_none, after_reset=after))
+        print(f"  {name}: {len(layers)} layers, overall {overall}")
+
+
+ONLY = None  # fixture-name substrings (--only): regenerate just those and merge into the manifest
+
+
+def wanted(name: str) -> bool:
+    return ONLY is None or any(o in name for o in ONLY)
+
+
 def main():
+    global ONLY
+    import argparse
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--only", nargs="*", help="regenerate only fixtures whose name contains one of these; "
+                                               "other manifest entries are kept")
+    args = ap.parse_args()
+    ONLY = args.only
     print("torch", torch.__version__, torch.backends.cpu.get_cpu_capability(), "threads", torch.get_num_threads())
     assert torch.backends.cpu.get_cpu_capability() == "AVX2", "run with ATEN_CPU_CAPABILITY=avx2"
     orc.build()
     w = Writer()
-    for fn in [gen_position_bias, gen_aggregation, gen_normalize_edge, gen_quant, gen_select, gen_layers]:
+    fns = [gen_position_bias, gen_aggregation, gen_normalize_edge, gen_quant, gen_select, gen_layers, gen_stats]
+    if ONLY is not None:
+        fns = [gen_layers, gen_stats]
+    for fn in fns:
         t0 = time.time()
         fn(w)
         print(f"{fn.__name__}: {time.time() - t0:.1f}s")
-    w.finish()
+    w.finish(merge=ONLY is not None)
     return 1 if w.mismatches else 0
 
 

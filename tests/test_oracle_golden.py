@@ -101,7 +101,8 @@ def test_full_layer(case):
     dt = synth.DTYPES[s["dtype"]]
     pr = s["params"]
     o = orc.compress_layer(K, V, dt, W, dt, s["P"], pr["alpha"], pr["beta"], pr["gamma"], s["layer_weight"],
-                           pr["theta_h"], pr["theta_m"], s["bits"], s["ratio"], no_selection=s["no_selection"])
+                           pr["theta_h"], pr["theta_m"], s["bits"], s["ratio"], no_selection=s["no_selection"],
+                           threads=4)  # OpenMP oracle: same bytes at any thread count
     assert_matches(case, "scores", o["scores"], arrays)
     assert_matches(case, "labels", o["labels"], arrays)
     if s["tie_ambiguous"]:
