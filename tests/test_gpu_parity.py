@@ -409,14 +409,17 @@ def test_native_bhsd_layout_matches_bsf():
 
 
 # ----------------------------------------------------------------------------- full-size properties
-@pytest.mark.parametrize("S,dtype,ratio", [(16384, "float16", 0.6), (65536, "float16", 0.4),
-                                           (32768, "bfloat16", 0.8)])
-def test_full_size_properties(S, dtype, ratio):
+@pytest.mark.parametrize("S,dtype,ratio,H", [(16384, "float16", 0.6, 32), (65536, "float16", 0.4, 32),
+                                             (32768, "bfloat16", 0.8, 32),
+                                             (16384, "float32", 0.6, 32),    # cfg3 at the model's fp32
+                                             (32768, "float16", 0.4, 40),    # cfg5: 13B, F = 5120
+                                             (32768, "float32", 0.6, 40)])
+def test_full_size_properties(S, dtype, ratio, H):
     """BASELINE sizes: closed-form greedy counts, ascending order, budget, pack→unpack == dequant,
     and sampled rows re-quantized by the oracle."""
     import rtkv
     from rtkv import _lib as L
-    H, D = 32, 128
+    D = 128
     F = H * D
     cfg = config(COVERAGE, 32)
     P = rtkv.prompt_length(S)
@@ -454,8 +457,9 @@ def test_full_size_properties(S, dtype, ratio):
                                     scale_zp=bufs.scale_zp[:, :st.max_kept], kept_index=bufs.kept_index[:, :st.max_kept],
                                     labels=bufs.labels, rows=[row["kept"]], bits=(2, 4, 8), dtype=TD[dtype],
                                     feature_dim=F))
-    assert torch.equal(dk.view(torch.int16), k2.view(torch.int16))
-    assert torch.equal(dv.view(torch.int16), v2.view(torch.int16))
+    iv = torch.int32 if dtype == "float32" else torch.int16
+    assert torch.equal(dk.view(iv), k2.view(iv))
+    assert torch.equal(dv.view(iv), v2.view(iv))
     rng = np.random.default_rng(0)
     k2h = host(k2)[0]
     for r in rng.choice(row["kept"], size=16, replace=False):
