@@ -4,9 +4,10 @@
 Metric (BASELINE.json): prefill KV-compress GB/s + TTFT, Llama-2-7B, S = 16k, 1 GPU.
 
 One *step* = the compression of all 32 layers of one prefill (BASELINE config 3: B=1, S=16384,
-32 heads × 128, fp16 K/V, prompt P=128, full importance → quantization → selective propagation)
-through the C ABI's fused driver (rtkv_compress_layer: 3 kernels per layer, no host sync inside
-the step).  Inputs are synthetic (seeded, resident in HBM before timing).
+32 heads × 128, K/V in the reference model's fp32 (modified_llama.py:368), prompt P=128, full
+importance → quantization → selective propagation) through the C ABI's fused driver
+(rtkv_compress_layer: 3 kernels per layer, no host sync inside the step).  Inputs are synthetic
+(seeded, resident in HBM before timing).
 
     python bench.py [--gpus N] [--steps K] [--warmup W]
 
@@ -15,10 +16,15 @@ owns S tokens of an N·S-token prefill; RCCL all-gather of per-token attention m
 selection on every rank, local quantization, RCCL all-gather of the packed KV).
 
 Rank 0 prints ONE JSON line.  ``value`` = algorithmic bytes of the whole job ÷ wall time (GB/s);
-``ttft_ms`` = Σ per-layer compress time (the reference's TTFT, longbench_eval.py:160);
-``roofline`` = the dominant kernel (K4 quantize+pack+compact) timed with HIP events inside this
-run; ``cpu_baseline`` = the C oracle (single-thread restatement of the reference) on a bounded
-sample of the same workload.
+``ttft_ms`` = Σ per-layer compress time of the raw driver;
+``roofline`` = the path's HBM-read roofline as the north star defines it (R = 2·S·H·D·e
++ H·S·P·e bytes per layer over the per-layer time of K1+K2+K4, HIP events on the launch stream);
+``roofline_k4`` = the dominant kernel (K4 quantize+pack+compact) on its own read+write bytes;
+``cpu_baseline`` = the C oracle (OpenMP restatement of the reference) on a bounded sample of the
+same workload.  Extra legs (``--legs``, single GPU, same inputs): ``f16`` (the workload in fp16),
+``packed_only`` (codes + scale/zp, no dequantized K'/V' — what the packed consumers read) and
+``drop_in`` (the reference caller's path, RealTimePrefillCompressor.compress_layer_kv_cache with
+its per-layer host sync; ``ttft_ms`` = Σ processing_time as longbench_eval.py:160 defines TTFT).
 """
 from __future__ import annotations
 
@@ -45,9 +51,17 @@ def parse():
     ap.add_argument("--seq", type=int, default=16384, help="tokens per rank")
     ap.add_argument("--heads", type=int, default=32)
     ap.add_argument("--head-dim", type=int, default=128)
-    ap.add_argument("--dtype", default="float16", choices=["float16", "bfloat16", "float32"])
+    ap.add_argument("--dtype", default="float32", choices=["float16", "bfloat16", "float32"],
+                    help="K/V/attention dtype (default: the reference model's fp32)")
     ap.add_argument("--no-packed", action="store_true", help="skip the packed-code output")
-    ap.add_argument("--cpu-baseline-layers", type=int, default=2, help="layers of the oracle sample (0 = skip)")
+    ap.add_argument("--no-dequant", action="store_true", help="skip the dequantized K'/V' output (packed only)")
+    ap.add_argument("--legs", default="f16,packed_only,drop_in",
+                    help="extra single-GPU legs after the main line: comma list of f16, packed_only, drop_in "
+                         "(or 'none')")
+    ap.add_argument("--leg-steps", type=int, default=5)
+    ap.add_argument("--cpu-baseline-seconds", type=float, default=12.0,
+                    help="CPU work budget of the oracle sample (layers are added until it is spent; 0 = skip)")
+    ap.add_argument("--cpu-baseline-layers", type=int, default=32, help="at most this many layers in the sample")
     ap.add_argument("--quiet", action="store_true")
     ap.add_argument("--importance", default="w", choices=["w", "qk"],
                     help="w: the reference's attention-weights input (prompt slice); qk: fused mode "
@@ -93,13 +107,16 @@ def synth_qk(S: int, H: int, D: int, K, dtype, device, gen, causal=True):
 
 
 class Job:
-    """Per-rank state: inputs and outputs of every layer, resident in HBM."""
+    """Per-rank state: inputs and outputs of every layer, resident in HBM.
 
-    def __init__(self, args, device, rank, world):
+    dtype / emit_dequant / emit_packed override the command line (extra legs); ``inputs`` shares
+    another job's resident inputs instead of generating new ones."""
+
+    def __init__(self, args, device, rank, world, dtype=None, emit_dequant=None, emit_packed=None, inputs=None):
         import rtkv
         from rtkv import _lib as L
         self.args, self.device, self.rank, self.world = args, device, rank, world
-        self.dtype = getattr(torch, args.dtype)
+        self.dtype = getattr(torch, dtype or args.dtype)
         self.S, self.H, self.D = args.seq, args.heads, args.head_dim
         self.F = self.H * self.D
         self.S_total = self.S * world
@@ -109,29 +126,34 @@ class Job:
                                           early_layer_ratio=0.8, middle_layer_ratio=0.6, later_layer_ratio=0.4,
                                           num_hidden_layers=args.layers)
         self.bits = (2, 4, 8)
-        self.emit_packed = not args.no_packed
-        flags = L.EMIT_DEQUANT | (0 if args.no_packed else L.EMIT_PACKED)
+        self.emit_packed = (not args.no_packed) if emit_packed is None else emit_packed
+        self.emit_dequant = (not args.no_dequant) if emit_dequant is None else emit_dequant
+        if not (self.emit_packed or self.emit_dequant):
+            raise SystemExit("--no-packed and --no-dequant together leave nothing to compute")
+        flags = (L.EMIT_DEQUANT if self.emit_dequant else 0) | (L.EMIT_PACKED if self.emit_packed else 0)
         prop = rtkv.SelectiveTokenPropagator(self.cfg)
         gen = torch.Generator(device=device)
         gen.manual_seed(1234 + 7919 * rank)
-        self.inputs, self.bufs, self.params = [], [], []
+        self.inputs = inputs if inputs is not None else []
+        self.bufs, self.params = [], []
         for l in range(args.layers):
-            K, V, W = synth_layer(l, self.S, self.H, self.D, self.P, self.dtype, device, gen)
-            if args.importance == "qk":
-                Q, lse = synth_qk(self.S, self.H, self.D, K, self.dtype, device, gen)
-                self.inputs.append((K, V, Q, lse))
-                del W
-            else:
-                self.inputs.append((K, V, W))
+            if inputs is None:
+                K, V, W = synth_layer(l, self.S, self.H, self.D, self.P, self.dtype, device, gen)
+                if args.importance == "qk":
+                    Q, lse = synth_qk(self.S, self.H, self.D, K, self.dtype, device, gen)
+                    self.inputs.append((K, V, Q, lse))
+                    del W
+                else:
+                    self.inputs.append((K, V, W))
             self.bufs.append(rtkv.LayerBuffers(1, self.S, self.F, self.dtype, device, self.bits,
-                                               emit_dequant=True, emit_packed=self.emit_packed))
+                                               emit_dequant=self.emit_dequant, emit_packed=self.emit_packed))
             self.params.append(rtkv.params_from_config(self.cfg, l, self.P, prop.get_layer_propagation_ratio(l), flags))
         self.ws = rtkv.Workspace(device)
         self.ws.get(1, self.S)
         torch.cuda.synchronize(device)
 
     def step(self, events=None):
-        """Compress every layer (single GPU); events: list of 4-tuples of raw hipEvent_t or None."""
+        """Compress every layer (single GPU); events: list of 4-tuples of torch events or None."""
         import rtkv
         from rtkv import _lib as L
         import ctypes
@@ -158,10 +180,18 @@ class Job:
                        self.ws.buf.data_ptr(), self.ws.buf.numel(), L.stream_ptr(self.device), ev),
                     "compress_layer_events")
 
+    def elem(self):
+        return torch.tensor([], dtype=self.dtype).element_size()
+
+    def read_roofline_bytes(self):
+        """R per layer (north star): every K/V element once + the prompt columns of W."""
+        e = self.elem()
+        return 2 * self.S * self.F * e + self.H * self.S * self.P * e
+
     def layer_bytes(self):
         """Algorithmic HBM bytes per layer: total and the K4 (quantize+pack+compact) part."""
         from rtkv.engine import decode_stats
-        e = torch.tensor([], dtype=self.dtype).element_size()
+        e = self.elem()
         tot, k4 = [], []
         for l in range(self.args.layers):
             st = decode_stats(self.bufs[l].stats.cpu().numpy().tobytes(), 1)
@@ -171,12 +201,66 @@ class Job:
             else:
                 w_read = self.H * self.S * self.P * e               # prompt columns of W
             kv_read = 2 * Sp * self.F * e                        # kept rows of K and V, read once
-            deq = 2 * Sp * self.F * e                            # dequantized K', V'
+            deq = 2 * Sp * self.F * e if self.emit_dequant else 0   # dequantized K', V'
             packed = (2 * pk + Sp * 16) if self.emit_packed else 0   # codes + scale/zp
             meta = self.S * (4 + 4 + 4 + 1 + 1) + Sp * (4 + 8 + 1)   # A, scores, labels, mask / index, offset
             k4.append(kv_read + deq + packed + Sp * (4 + 8 + 1))
             tot.append(w_read + kv_read + deq + packed + meta)
         return tot, k4
+
+    def timed(self, steps, warmup):
+        """(ms per step, per-layer event times [K1, K2, K4] in µs) of this job alone."""
+        for _ in range(warmup):
+            self.step()
+        torch.cuda.synchronize(self.device)
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            self.step()
+        torch.cuda.synchronize(self.device)
+        ms = (time.perf_counter() - t0) / steps * 1e3
+        return ms, self.kernel_times()
+
+    def kernel_times(self, reps=3):
+        """Per-layer mean of K1, K2 and K4 (µs) from HIP events the C ABI records on the launch stream."""
+        events = [[torch.cuda.Event(enable_timing=True) for _ in range(4)] for _ in range(self.args.layers)]
+        for evs in events:
+            for e in evs:
+                e.record()  # materialise the hipEvent_t
+        torch.cuda.synchronize(self.device)
+        k_ms = [0.0, 0.0, 0.0]
+        for _ in range(reps):
+            self.step(events=events)
+            torch.cuda.synchronize(self.device)
+            for evs in events:
+                for k in range(3):
+                    k_ms[k] += evs[k].elapsed_time(evs[k + 1])
+        return [m / (reps * self.args.layers) * 1e3 for m in k_ms]
+
+
+def drop_in_leg(args, job, steps, warmup):
+    """The reference caller's path (modified_llama.py:113-117): RealTimePrefillCompressor.
+    compress_layer_kv_cache per layer, with its host sync for the output shape.  TTFT is the
+    reference's definition, Σ processing_time over the layers (longbench_eval.py:160)."""
+    import rtkv
+    comp = rtkv.RealTimePrefillCompressor(job.cfg, emit_packed=job.emit_packed)
+    ids = torch.zeros(1, job.S, dtype=torch.long, device=job.device)
+    ttft, wall = [], []
+    for it in range(warmup + steps):
+        comp.reset_compression_state()
+        torch.cuda.synchronize(job.device)
+        t0 = time.perf_counter()
+        for l in range(args.layers):
+            K, V, W = job.inputs[l]
+            comp.compress_layer_kv_cache(K, V, W, ids, l)
+        torch.cuda.synchronize(job.device)
+        if it >= warmup:
+            wall.append((time.perf_counter() - t0) * 1e3)
+            ttft.append(comp.get_overall_compression_stats()["total_processing_time"] * 1e3)
+    ms = sum(ttft) / len(ttft)
+    return {"ttft_ms": round(ms, 4), "ms_per_layer": round(ms / args.layers, 4),
+            "wall_ms_per_step": round(sum(wall) / len(wall), 4), "steps": steps,
+            "path": "rtkv.RealTimePrefillCompressor.compress_layer_kv_cache (dequant + packed, one host sync "
+                    "per layer for the output shape)"}
 
 
 class ShardedJob:
@@ -243,37 +327,44 @@ class ShardedJob:
         return n
 
 
-def pmc_traffic(args, kernel="quant_rows_kernel"):
-    """HBM bytes per dispatch of `kernel` from the newest committed PMC summary (profiles/*_pmc.json,
-    written by profiles/summarize.py from separate rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of
-    this script at its default workload), or None for any other workload."""
+def workload_key(args):
+    """Identifies the workload a committed PMC summary was collected on (profiles/*_pmc.json)."""
+    return {"seq": args.seq, "layers": args.layers, "heads": args.heads, "head_dim": args.head_dim,
+            "dtype": args.dtype, "packed": not args.no_packed, "dequant": not args.no_dequant,
+            "importance": args.importance}
+
+
+def pmc_kernels(args):
+    """Per-kernel HBM bytes per dispatch from the newest committed PMC summary of this exact workload
+    (profiles/*_pmc.json, written by profiles/summarize.py from separate rocprofv3 --pmc FETCH_SIZE /
+    WRITE_SIZE passes of `bench.py --legs none`), or (None, None)."""
     import glob
-    default = (args.seq, args.layers, args.heads, args.head_dim, args.dtype, args.no_packed, args.importance) == \
-        (16384, 32, 32, 128, "float16", False, "w")
-    files = sorted(glob.glob(os.path.join(REPO, "profiles", "*_pmc.json")))
-    if not default or not files:
-        return None, None
-    with open(files[-1]) as f:
-        doc = json.load(f)
-    for name, v in doc["kernels"].items():
-        if kernel in name:
-            return v["hbm_bytes"], os.path.relpath(files[-1], REPO)
+    want = workload_key(args)
+    legacy = dict(want, dtype="float16")  # round-1 summaries predate the workload key (f16 default)
+    for path in sorted(glob.glob(os.path.join(REPO, "profiles", "*_pmc.json")), reverse=True):
+        with open(path) as f:
+            doc = json.load(f)
+        if doc.get("workload", legacy if "workload" not in doc else None) == want:
+            return doc["kernels"], os.path.relpath(path, REPO)
     return None, None
 
 
 def cpu_baseline(args, job):
-    """The C oracle (single thread, a literal restatement of the reference) on a bounded sample:
-    the first `cpu_baseline_layers` layers of the same workload, same inputs."""
-    if args.cpu_baseline_layers <= 0 or args.importance != "w":
+    """The C oracle (an OpenMP restatement of the reference: aggregation and per-row quantization
+    over threads, selection serial) on a bounded sample: the first layers of the same workload, same
+    inputs, added until --cpu-baseline-seconds of CPU time are spent."""
+    if args.cpu_baseline_seconds <= 0 or args.importance != "w":
         return None
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     import numpy as np
     import rtkv_oracle as orc
+    threads = os.cpu_count() or 1
+    if os.environ.get("OMP_NUM_THREADS", "").isdigit():   # the host-core share of this job (16 on the GPU box)
+        threads = max(1, min(threads, int(os.environ["OMP_NUM_THREADS"])))
     code = {torch.float32: 0, torch.float16: 1, torch.bfloat16: 2}[job.dtype]
-    n = min(args.cpu_baseline_layers, args.layers)
-    nbytes, secs = 0.0, 0.0
+    nbytes, secs, n = 0.0, 0.0, 0
     tot, _ = job.layer_bytes()
-    for l in range(n):
+    for l in range(min(args.cpu_baseline_layers, args.layers)):
         K, V, W = job.inputs[l]
         as_np = (lambda t: t.cpu().numpy()) if job.dtype == torch.float32 else \
             (lambda t: t.cpu().view(torch.int16).numpy().view(np.uint16))
@@ -281,13 +372,57 @@ def cpu_baseline(args, job):
         p = job.params[l]
         t0 = time.perf_counter()
         orc.compress_layer(Kn, Vn, code, Wn, code, job.P, p.alpha, p.beta, p.gamma, p.layer_weight, p.theta_h,
-                           p.theta_m, job.bits, p.propagation_ratio, packed=job.emit_packed)
+                           p.theta_m, job.bits, p.propagation_ratio, packed=job.emit_packed, threads=threads)
         secs += time.perf_counter() - t0
         nbytes += tot[l]
-    return {"value": round(nbytes / secs / 1e9, 4), "unit": "GB/s", "cores": 1, "kind": "port",
-            "ms_per_layer": round(secs / n * 1e3, 1),
+        n += 1
+        if secs >= args.cpu_baseline_seconds:
+            break
+    return {"value": round(nbytes / secs / 1e9, 4), "unit": "GB/s", "cores": threads, "host_cpus": os.cpu_count(),
+            "kind": "port", "ms_per_layer": round(secs / n * 1e3, 1),
             "sample": f"{n} of {args.layers} layers (S={job.S}, {job.H}x{job.D}, {args.dtype}), C oracle "
-                      f"oracle/rtkv_oracle.c single-threaded on the host"}
+                      f"oracle/rtkv_oracle.c, OpenMP on {threads} host threads (aggregation and per-row "
+                      f"quantization parallel, selection serial)"}
+
+
+def roofline_objects(args, job, kus, k4_bytes):
+    """(path read roofline, K4 roofline) from the per-layer event times kus = [K1, K2, K4] µs."""
+    pmc, src = pmc_kernels(args)
+    layer_us = sum(kus)
+    R = job.read_roofline_bytes()
+    achieved = R / (layer_us / 1e6) / 1e9
+    traffic = None
+    if pmc:
+        traffic = round(sum(v["hbm_bytes"] for v in pmc.values()))
+    path = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_source": src,
+            "scope": "path: K1 + K2 + K4 per layer (HIP events on the launch stream)",
+            "algorithmic_bytes_per_launch": R,
+            "algorithmic_bytes_def": "R = 2*S*H*D*e + H*S*P*e (every K/V element once + W prompt columns; "
+                                     "SURVEY §8d, the north star's HBM-read roofline)",
+            "avg_launch_us": round(layer_us, 2)}
+    k4_us = kus[2]
+    k4_alg = sum(k4_bytes) / args.layers
+    k4_ach = k4_alg / (k4_us / 1e6) / 1e9
+    k4_traffic = None
+    if pmc:
+        k4_traffic = next((round(v["hbm_bytes"]) for k, v in pmc.items() if "quant_rows_kernel" in k), None)
+    k4 = {"bound": "hbm", "achieved": round(k4_ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+          "frac": round(k4_ach / HBM_PEAK_GBS, 4), "traffic": k4_traffic, "traffic_source": src,
+          "algorithmic_bytes_per_launch": round(k4_alg), "kernel": "quant_rows_kernel (K4), read + write bytes",
+          "avg_launch_us": round(k4_us, 2)}
+    return path, k4
+
+
+def leg_summary(args, job, ms, kus):
+    tot, k4 = job.layer_bytes()
+    path, _ = roofline_objects(args, job, kus, k4)
+    return {"value": round(sum(tot) / (ms / 1e3) / 1e9, 2), "unit": "GB/s", "ms_per_step": round(ms, 4),
+            "dtype": {"float16": "f16", "bfloat16": "bf16", "float32": "f32"}[str(job.dtype).split(".")[-1]],
+            "outputs": "+".join(x for x, on in (("dequant", job.emit_dequant), ("packed", job.emit_packed)) if on),
+            "kernel_us_per_layer": {"K1_aggregation": round(kus[0], 2), "K2_finalize": round(kus[1], 2),
+                                    "K4_quant_pack": round(kus[2], 2)},
+            "path_read_roofline_frac": path["frac"], "layer_us": round(sum(kus), 2)}
 
 
 def main():
@@ -330,26 +465,19 @@ def main():
         elapsed = float(t.item())
     ms_per_step = elapsed / args.steps * 1e3
 
-    # per-kernel timing of the fused path (HIP events on the launch stream), outside the timed loop
-    events = [[torch.cuda.Event(enable_timing=True) for _ in range(4)] for _ in range(args.layers)]
-    for evs in events:
-        for e in evs:
-            e.record()  # materialise the hipEvent_t
-    torch.cuda.synchronize(device)
-    reps = 3
-    k_ms = [0.0, 0.0, 0.0]
-    for _ in range(reps):
-        job.step(events=events) if not sharded else job.step()
+    kus = None
+    if sharded:
+        for _ in range(2):
+            job.step()
         torch.cuda.synchronize(device)
-        if not sharded:
-            for evs in events:
-                for k in range(3):
-                    k_ms[k] += evs[k].elapsed_time(evs[k + 1])
+    else:
+        kus = job.kernel_times()  # per-kernel timing (HIP events on the launch stream), outside the timed loop
     tot_bytes, k4_bytes = job.layer_bytes()
     step_bytes = sum(tot_bytes)  # whole-job algorithmic bytes (the sharded job counts all N*S tokens)
     value = step_bytes / (ms_per_step / 1e3) / 1e9
 
     if rank == 0:
+        outs = "+".join(x for x, on in (("dequant", not args.no_dequant), ("packed", not args.no_packed)) if on)
         line = {
             "metric": "prefill KV-compress GB/s + TTFT, Llama-2-7B S=16k, 1 GPU",
             "value": round(value, 2),
@@ -365,8 +493,8 @@ def main():
             "dtype": {"float16": "f16", "bfloat16": "bf16", "float32": "f32"}[args.dtype],
             "data": "synthetic (seeded torch RNG; K,V ~ N(0,1), W = causal u^4-softmax-like prompt slice)",
             "config": {"workload": f"Llama-2-7B prefill KV compression{' (fused Q/LSE importance)' if args.importance == 'qk' else ''}, {args.layers} layers, "
-                                   f"S={job.S * world} ({job.S}/rank), {args.heads}x{args.head_dim}, "
-                                   f"P={job.P}, bits 8/4/2, ratios .8/.6/.4, dequant+packed outputs",
+                                   f"S={job.S * world} ({job.S}/rank), {args.heads}x{args.head_dim}, {args.dtype}, "
+                                   f"P={job.P}, bits 8/4/2, ratios .8/.6/.4, {outs} outputs",
                        "model": "Llama-2-7B (KV shapes only)", "global_batch": 1, "seq_len": job.S * world,
                        "parallelism": f"sequence-shard x{world}" if world > 1 else "single GPU"},
         }
@@ -375,29 +503,40 @@ def main():
                                 "kind": ("grouped RCCL send/recv per layer of packed K/V codes + scale/zp (exact byte "
                                          "ranges, all peers at once), " +
                                          ("all after the last layer" if args.no_overlap else
-                                          "each issued one layer later on its own communicator, overlapping "
+                                          "each issued two layers later on its own communicator, overlapping "
                                           "the following layers' compute")),
                                 "per_layer_collective": "RCCL all-gather of A (4 B/token)"}
-        if not sharded:
-            per_launch_ms = k_ms[2] / (reps * args.layers)
-            achieved = sum(k4_bytes) / args.layers / (per_launch_ms / 1e3) / 1e9
-            traffic, src = pmc_traffic(args)
-            line["roofline"] = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
-                                "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                                "traffic_source": src,
-                                "algorithmic_bytes_per_launch": round(sum(k4_bytes) / args.layers),
-                                "kernel": "quant_rows_kernel (K4)", "avg_launch_us": round(per_launch_ms * 1e3, 2)}
-            line["kernel_us_per_layer"] = {"K1_aggregation": round(k_ms[0] / (reps * args.layers) * 1e3, 2),
-                                           "K2_finalize": round(k_ms[1] / (reps * args.layers) * 1e3, 2),
-                                           "K4_quant_pack": round(per_launch_ms * 1e3, 2)}
-            line["cpu_baseline"] = cpu_baseline(args, job)
-            if args.importance == "qk":  # K1' on MFMA: the Q·K_P^T contraction against the dense f16 peak
-                k1_ms = k_ms[0] / (reps * args.layers)
+        else:
+            path, k4 = roofline_objects(args, job, kus, k4_bytes)
+            line["roofline"] = path
+            line["roofline_k4"] = k4
+            line["kernel_us_per_layer"] = {"K1_aggregation": round(kus[0], 2), "K2_finalize": round(kus[1], 2),
+                                           "K4_quant_pack": round(kus[2], 2)}
+            if args.importance == "qk":  # K1' on MFMA: the Q·K_P^T contraction against the dense peak
                 flops = 2.0 * job.H * job.S * job.P * job.D
-                tf = flops / (k1_ms / 1e3) / 1e12
+                tf = flops / (kus[0] / 1e6) / 1e12
                 line["k1_mfma"] = {"bound": "mfma", "achieved": round(tf, 2), "peak": 2500.0, "unit": "TFLOP/s",
-                                   "frac": round(tf / 2500.0, 4), "avg_launch_us": round(k1_ms * 1e3, 2),
-                                   "hbm_GBs": round((job.H * job.S * job.D * 2 + 4 * job.H * job.S) / (k1_ms / 1e3) / 1e9, 1)}
+                                   "frac": round(tf / 2500.0, 4), "avg_launch_us": round(kus[0], 2),
+                                   "hbm_GBs": round((job.H * job.S * job.D * 2 + 4 * job.H * job.S) / (kus[0] / 1e6) / 1e9, 1)}
+            legs = {}
+            wanted = [x for x in args.legs.split(",") if x and x != "none"] if args.importance == "w" else []
+            for name in wanted:
+                if name == "f16" and args.dtype != "float16":
+                    inputs = None
+                    leg = Job(args, device, rank, world, dtype="float16")
+                    legs["f16"] = leg_summary(args, leg, *leg.timed(args.leg_steps, 2))
+                    del leg
+                elif name == "packed_only":
+                    leg = Job(args, device, rank, world, emit_dequant=False, emit_packed=True, inputs=job.inputs)
+                    legs["packed_only"] = leg_summary(args, leg, *leg.timed(args.leg_steps, 2))
+                    del leg
+                elif name == "drop_in":
+                    legs["drop_in"] = drop_in_leg(args, job, args.leg_steps, 2)
+                    legs["drop_in"]["raw_driver_ms_per_layer"] = round(ms_per_step / args.layers, 4)
+                torch.cuda.empty_cache()
+            if legs:
+                line["legs"] = legs
+            line["cpu_baseline"] = cpu_baseline(args, job)
         print(json.dumps(line), flush=True)
     if dist is not None:
         dist.barrier()

@@ -1,7 +1,10 @@
 #!/usr/bin/env python3
 """Summarise rocprofv3 outputs of bench.py into the small files committed under profiles/.
 
-    python profiles/summarize.py TAG [gpurun_out]
+    python profiles/summarize.py TAG [gpurun_out] [-- BENCH ARGS]
+
+BENCH ARGS are the bench.py arguments of the profiled workload (default: bench.py's defaults); they
+are recorded as the summary's "workload", which bench.py matches before using the traffic.
 
 reads  gpurun_out/prof/run_kernel_stats.csv              (rocprofv3 --kernel-trace --stats)
        gpurun_out/pmc/fetch_counter_collection.csv       (rocprofv3 --pmc FETCH_SIZE, own pass)
@@ -31,9 +34,17 @@ def per_kernel(path, counter):
 
 
 def main():
-    tag = sys.argv[1]
-    src = sys.argv[2] if len(sys.argv) > 2 else "gpurun_out"
+    argv = sys.argv[1:]
+    bench_args = argv[argv.index("--") + 1:] if "--" in argv else []
+    argv = argv[:argv.index("--")] if "--" in argv else argv
+    tag = argv[0]
+    src = argv[1] if len(argv) > 1 else "gpurun_out"
     here = os.path.dirname(os.path.abspath(__file__))
+    sys.path.insert(0, os.path.dirname(here))
+    import bench
+    saved, sys.argv = sys.argv, ["bench.py"] + bench_args
+    workload = bench.workload_key(bench.parse())
+    sys.argv = saved
     shutil.copy(os.path.join(src, "prof", "run_kernel_stats.csv"), os.path.join(here, f"{tag}_kernel_stats.csv"))
     fetch, n = per_kernel(os.path.join(src, "pmc", "fetch_counter_collection.csv"), "FETCH_SIZE")
     write, _ = per_kernel(os.path.join(src, "pmcw", "write_counter_collection.csv"), "WRITE_SIZE")
@@ -46,7 +57,9 @@ def main():
         out[k] = {"dispatches": n[k], "fetch_kib_raw": round(fetch[k], 3), "write_kib_raw": round(write.get(k, 0.0), 3),
                   "hbm_read_bytes": round(fb), "hbm_write_bytes": round(wb), "hbm_bytes": round(fb + wb)}
     doc = {"source": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes) of "
-                     "`python3 bench.py --steps 2 --warmup 1 --cpu-baseline-layers 0`",
+                     "`python3 bench.py --steps 2 --warmup 1 --legs none --cpu-baseline-seconds 0 "
+                     + " ".join(bench_args) + "`",
+           "workload": workload,
            "correction": "bytes = 2 * FETCH_SIZE KiB * 1024 + WRITE_SIZE KiB * 1024 (gfx950, MI355X_MICROARCH.md)",
            "kernels": out}
     with open(os.path.join(here, f"{tag}_pmc.json"), "w") as f:

@@ -153,26 +153,50 @@ class Workspace:
 
 
 class LayerBuffers:
-    """Output buffers of one compressed layer, sized for B batch rows of S tokens (capacity = S)."""
+    """Output buffers of one compressed layer, sized for B batch rows of S tokens (capacity = S).
+
+    Every buffer is a view into ONE device allocation (the drop-in path creates fresh buffers per
+    layer call, as the reference returns fresh tensors; one allocation instead of ten keeps that
+    cheap).  Views are 256-byte aligned."""
 
     def __init__(self, B: int, S: int, F: int, dtype: torch.dtype, device, bits, emit_dequant=True, emit_packed=True):
         self.B, self.S, self.F, self.dtype = B, S, F, dtype
         dev = torch.device(device)
-        self.scores = torch.empty(B, S, dtype=torch.float32, device=dev)
-        self.labels = torch.empty(B, S, dtype=torch.uint8, device=dev)
-        self.mask = torch.empty(B, S, dtype=torch.uint8, device=dev)
-        self.kept_index = torch.empty(B, S, dtype=torch.int32, device=dev)
-        self.stats = torch.empty(L.stats_bytes(B), dtype=torch.uint8, device=dev)
-        self.k_out = torch.empty(B * S * F, dtype=dtype, device=dev) if emit_dequant else None
-        self.v_out = torch.empty(B * S * F, dtype=dtype, device=dev) if emit_dequant else None
+        esz = torch.tensor([], dtype=dtype).element_size()
+        cap = 0
         if emit_packed:
             b3 = (ctypes.c_int32 * 3)(*bits)
             cap = int(L.lib().rtkv_packed_capacity(B, S, F, L.TORCH_DTYPE_CODE[dtype], b3))
-            self.packed_k = torch.empty(max(cap, 1), dtype=torch.uint8, device=dev)
-            self.packed_v = torch.empty(max(cap, 1), dtype=torch.uint8, device=dev)
+        plan = [("scores", B * S * 4), ("labels", B * S), ("mask", B * S), ("kept_index", B * S * 4),
+                ("stats", L.stats_bytes(B))]
+        if emit_dequant:
+            plan += [("k_out", B * S * F * esz), ("v_out", B * S * F * esz)]
+        if emit_packed:
+            plan += [("packed_k", max(cap, 1)), ("packed_v", max(cap, 1)), ("row_offset", B * S * 8),
+                     ("scale_zp", B * S * 16)]
+        offs, total = {}, 0
+        for name, n in plan:
+            offs[name] = (total, n)
+            total += (n + 255) // 256 * 256
+        self.arena = torch.empty(max(total, 1), dtype=torch.uint8, device=dev)
+
+        def view(name, dt, shape):
+            o, n = offs[name]
+            return self.arena[o:o + n].view(dt).view(shape)
+
+        self.scores = view("scores", torch.float32, (B, S))
+        self.labels = view("labels", torch.uint8, (B, S))
+        self.mask = view("mask", torch.uint8, (B, S))
+        self.kept_index = view("kept_index", torch.int32, (B, S))
+        self.stats = view("stats", torch.uint8, (L.stats_bytes(B),))
+        self.k_out = view("k_out", dtype, (B * S * F,)) if emit_dequant else None
+        self.v_out = view("v_out", dtype, (B * S * F,)) if emit_dequant else None
+        if emit_packed:
+            self.packed_k = view("packed_k", torch.uint8, (max(cap, 1),))
+            self.packed_v = view("packed_v", torch.uint8, (max(cap, 1),))
             self.packed_capacity = cap
-            self.row_offset = torch.empty(B, S, dtype=torch.int64, device=dev)
-            self.scale_zp = torch.empty(B, S, 4, dtype=torch.float32, device=dev)
+            self.row_offset = view("row_offset", torch.int64, (B, S))
+            self.scale_zp = view("scale_zp", torch.float32, (B, S, 4))
         else:
             self.packed_k = self.packed_v = self.row_offset = self.scale_zp = None
             self.packed_capacity = 0

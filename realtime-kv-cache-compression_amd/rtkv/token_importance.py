@@ -147,10 +147,12 @@ class LayerWiseImportanceTracker:
         self.record(layer_idx, scores)
         return scores
 
-    def record(self, layer_idx: int, scores: torch.Tensor):
+    def record(self, layer_idx: int, scores: torch.Tensor, copy: bool = True):
+        """Store a layer's scores; copy=False when nobody else holds ``scores`` (the drop-in path's
+        per-call buffers), so the hot path does not launch a copy."""
         if not isinstance(self.layer_scores, _HostScoreDict):  # reset_compression_state assigns {}
             self.layer_scores = _HostScoreDict(self.layer_scores)
-        self.layer_scores[layer_idx] = scores.detach().clone()
+        self.layer_scores[layer_idx] = scores.detach().clone() if copy else scores.detach()
 
     def get_cumulative_scores(self, layer_idx: int):
         """Mean of the stored scores of layers 0..layer_idx (host tensors, as in the reference)."""

@@ -20,6 +20,30 @@ from .selective_propagation import SelectiveTokenPropagator
 from .token_importance import LayerWiseImportanceTracker
 
 
+class _LazyDict(dict):
+    """A dict whose listed keys are computed on first access (then stored)."""
+
+    def __init__(self, base, **lazy):
+        super().__init__(base)
+        self._lazy = lazy
+        for k in lazy:
+            dict.__setitem__(self, k, None)
+
+    def __getitem__(self, key):
+        if key in self._lazy:
+            dict.__setitem__(self, key, self._lazy.pop(key)())
+        return dict.__getitem__(self, key)
+
+    def get(self, key, default=None):
+        return self[key] if key in self else default
+
+    def values(self):
+        return [self[k] for k in self.keys()]
+
+    def items(self):
+        return [(k, self[k]) for k in self.keys()]
+
+
 class RealTimePrefillCompressor:
     """Prompt-guided importance → dynamic precision → selective propagation, per layer."""
 
@@ -91,7 +115,7 @@ class RealTimePrefillCompressor:
         selected_keys, selected_values = res.kv()
         Sp = st.max_kept
         scores = bufs.scores
-        self.importance_tracker.record(layer_idx, scores)
+        self.importance_tracker.record(layer_idx, scores, copy=False)  # bufs are this call's own
 
         # statistics (unified_compressor.py:143-167)
         n = B * S
@@ -103,10 +127,13 @@ class RealTimePrefillCompressor:
         low = n - high - medium
         precision_stats = {"high_count": high, "medium_count": medium, "low_count": low,
                            "high_ratio": high / n, "medium_ratio": medium / n, "low_ratio": low / n}
-        quant_info = {"scales": {}, "zero_points": {}, "bit_assignments": bufs.labels.long().cpu().numpy()}
+        # bit_assignments is the reference's host int64 array (unified_compressor.py:125-129); it is
+        # copied on first access so the layer keeps a single host sync
+        quant_info = _LazyDict({"scales": {}, "zero_points": {}},
+                               bit_assignments=lambda labels=bufs.labels: labels.long().cpu().numpy())
         selection_stats = self.propagator._selection_info(scores, st, ratio, S)
         propagation_info = {"layer_idx": layer_idx, "propagation_ratio": ratio, "original_length": S,
-                            "max_selected_length": Sp, "selection_mask": bufs.mask.bool(),
+                            "max_selected_length": Sp, "selection_mask": bufs.mask.view(torch.bool),
                             "selection_stats": selection_stats}
         std = (st.score_m2 / (n - 1)) ** 0.5 if n > 1 else float("nan")
         processing_time = time.time() - start_time
