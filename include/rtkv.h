@@ -42,7 +42,8 @@ enum rtkv_status {
   RTKV_ERR_INVALID = -1,     /* bad shape / stride / parameter */
   RTKV_ERR_UNSUPPORTED = -2, /* configuration outside the implemented envelope */
   RTKV_ERR_HIP = -3,         /* a HIP runtime call failed */
-  RTKV_ERR_WORKSPACE = -4    /* workspace too small */
+  RTKV_ERR_WORKSPACE = -4,   /* workspace too small */
+  RTKV_ERR_TIMEOUT = -5      /* rtkv_wait_early: the device did not publish in time */
 };
 
 /* rtkv_layer_stats.error_flags bits (device-detected, read after the stream syncs) */
@@ -271,6 +272,35 @@ int rtkv_compress_layer_events(const rtkv_kv_desc* kv, const rtkv_attn_desc* w,
                                void* workspace_dev, size_t workspace_bytes, void* stream,
                                void* const events[4]);
 
+/* Early statistics (no reference counterpart: it serves the drop-in's host sync).  The reference
+ * caller needs the layer's output shape S' before compress_layer_kv_cache returns (the K'/V' views),
+ * so the drop-in waits for the statistics once per layer.  S' and every count are final as soon as
+ * the selection thresholds are (K2's first kernel), so with rtkv_compress_layer_early the device
+ * writes them into `early_host` (host memory from rtkv_host_alloc) and then `seq`; the host spins on
+ * that word (rtkv_wait_early) while the rest of K2 and all of K4 still run, and only score_m2 and
+ * kept_score_sum must be read from stats_dev after the stream syncs.  *published = 1 when this call
+ * will publish (the two-launch K2: B = 1, S <= 32768); 0: read stats_dev after a stream sync.
+ * complete = 0 on publication means the top-10% fallback ran: read stats_dev after a sync too. */
+typedef struct rtkv_early_stats {
+  uint64_t seq;              /* written last (release, system scope) */
+  int32_t complete;
+  int32_t reserved;
+  rtkv_layer_stats stats;    /* score_m2 not set */
+  rtkv_batch_stats batch;    /* B = 1; kept_score_sum not set */
+} rtkv_early_stats;
+
+int rtkv_compress_layer_early(const rtkv_kv_desc* kv, const rtkv_attn_desc* w, const rtkv_layer_params* p,
+                              const rtkv_layer_out* out, void* workspace_dev, size_t workspace_bytes,
+                              void* stream, rtkv_early_stats* early_host, uint64_t seq, int32_t* published);
+int rtkv_compress_layer_qk_early(const rtkv_kv_desc* kv, const rtkv_qk_desc* q, const rtkv_layer_params* p,
+                                 const rtkv_layer_out* out, void* workspace_dev, size_t workspace_bytes,
+                                 void* stream, rtkv_early_stats* early_host, uint64_t seq, int32_t* published);
+/* Spin until early_host->seq == seq (RTKV_OK) or timeout_us passes (RTKV_ERR_TIMEOUT). */
+int rtkv_wait_early(const rtkv_early_stats* early_host, uint64_t seq, int64_t timeout_us);
+/* Pinned, device-coherent host memory for rtkv_early_stats (hipHostMalloc, coherent + mapped). */
+void* rtkv_host_alloc(size_t bytes);
+void rtkv_host_free(void* p);
+
 /* ------------------------------------------------------------------------------------------------
  * Sequence shards (multi-GPU prefill; no reference counterpart — the reference is single-device).
  * Rank j of N owns tokens [row0, row0 + S_local) of an S_total-token prefill.  Per layer:
@@ -394,12 +424,20 @@ int rtkv_tensor_fake_quant(const void* x_dev, int dtype, int64_t n_rows, int64_t
                            const float* scale_zp_dev, void* out_dev, void* stream);
 
 /* Numerics self-check (no reference counterpart; replaces nothing).  The quantizer divides by the
- * row scale with a reciprocal + one FMA correction instead of the IEEE division for 16-bit rows;
- * this enumerates every (dividend, positive divisor) pair of the 16-bit dtype that the fast path
- * admits and counts bitwise differences from the IEEE fp32 quotient.  counts_dev[0] = pairs
- * checked, counts_dev[1] = mismatches (must be 0).  RTKV_ERR_UNSUPPORTED for RTKV_F32 (fp32 rows
- * always use the IEEE division). */
+ * row scale with a reciprocal + one FMA correction instead of the IEEE division where a row-uniform
+ * gate admits it; this enumerates every (dividend, positive divisor) pair of the 16-bit dtype that
+ * the fast path admits and counts bitwise differences from the IEEE fp32 quotient.
+ * counts_dev[0] = pairs checked, counts_dev[1] = mismatches (must be 0).  RTKV_ERR_UNSUPPORTED for
+ * RTKV_F32: see rtkv_selfcheck_division_f32. */
 int rtkv_selfcheck_division(int32_t dtype, unsigned long long* counts_dev, void* stream);
+
+/* The fp32 counterpart, one divisor range per call (adds to counts_dev, which the caller zeroes):
+ * dividends x = ±(1 + xm·2^-23)·2^ex for EVERY mantissa xm, divisors s = (1 + sm·2^-23)·2^es for
+ * sm in [s_lo, s_hi) ⊆ [0, 2^23).  Over ex = es = 0 and the whole range this is every mantissa pair,
+ * which proves the gated fp32 fast quotient (all its steps stay normal, so they commute with
+ * power-of-two scaling); other exponents spot-check that argument. */
+int rtkv_selfcheck_division_f32(int64_t s_lo, int64_t s_hi, int32_t ex, int32_t es, int32_t negative,
+                                unsigned long long* counts_dev, void* stream);
 
 #ifdef __cplusplus
 }

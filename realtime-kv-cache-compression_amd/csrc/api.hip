@@ -4,6 +4,8 @@
 #include <cstring>
 #include <string>
 
+#include <chrono>
+
 #include "common.h"
 
 namespace rtkv {
@@ -199,7 +201,10 @@ int rtkv_quantize_rows(const rtkv_kv_desc* kv, const uint8_t* labels_dev, const 
 // The fused layer: K1 (W aggregation, or K1' on MFMA when q != null) → K2 → K4.
 static int compress_layer_impl(const rtkv_kv_desc* kv, const rtkv_attn_desc* w, const rtkv_qk_desc* qk,
                                const rtkv_layer_params* p, const rtkv_layer_out* out, void* workspace_dev,
-                               size_t workspace_bytes, void* stream, void* const events[4]) {
+                               size_t workspace_bytes, void* stream, void* const events[4],
+                               rtkv_early_stats* early = nullptr, uint64_t early_seq = 0,
+                               int32_t* published = nullptr) {
+  if (published) *published = 0;
   int rc = check_params(p);
   if (rc) return rc;
   RTKV_REQUIRE(kv && (w || qk) && out, "null descriptor");
@@ -268,6 +273,11 @@ static int compress_layer_impl(const rtkv_kv_desc* kv, const rtkv_attn_desc* w, 
   a.mode_select = (p->flags & RTKV_NO_SELECTION) ? 2 : 1;
   const bool row_labels = select_fast_eligible(a);  // the fast path also writes each kept row's class
   a.row_label = row_labels ? ws.labels : nullptr;
+  if (early && row_labels) {  // the fast path's F1 publishes the final counts to the host
+    a.early = early;
+    a.early_seq = early_seq;
+    if (published) *published = 1;
+  }
   rc = launch_select(a, ws.sel, true, st);
   if (rc) return rc;
   if ((rc = mark(2))) return rc;
@@ -286,6 +296,48 @@ int rtkv_compress_layer_events(const rtkv_kv_desc* kv, const rtkv_attn_desc* w, 
 int rtkv_compress_layer(const rtkv_kv_desc* kv, const rtkv_attn_desc* w, const rtkv_layer_params* p,
                         const rtkv_layer_out* out, void* workspace_dev, size_t workspace_bytes, void* stream) {
   return rtkv_compress_layer_events(kv, w, p, out, workspace_dev, workspace_bytes, stream, nullptr);
+}
+
+int rtkv_compress_layer_early(const rtkv_kv_desc* kv, const rtkv_attn_desc* w, const rtkv_layer_params* p,
+                              const rtkv_layer_out* out, void* workspace_dev, size_t workspace_bytes, void* stream,
+                              rtkv_early_stats* early_host, uint64_t seq, int32_t* published) {
+  RTKV_REQUIRE(w != nullptr && early_host != nullptr, "null attention descriptor or early-stats buffer");
+  return compress_layer_impl(kv, w, nullptr, p, out, workspace_dev, workspace_bytes, stream, nullptr, early_host,
+                             seq, published);
+}
+
+int rtkv_compress_layer_qk_early(const rtkv_kv_desc* kv, const rtkv_qk_desc* q, const rtkv_layer_params* p,
+                                 const rtkv_layer_out* out, void* workspace_dev, size_t workspace_bytes, void* stream,
+                                 rtkv_early_stats* early_host, uint64_t seq, int32_t* published) {
+  RTKV_REQUIRE(q != nullptr && early_host != nullptr, "null query descriptor or early-stats buffer");
+  return compress_layer_impl(kv, nullptr, q, p, out, workspace_dev, workspace_bytes, stream, nullptr, early_host,
+                             seq, published);
+}
+
+int rtkv_wait_early(const rtkv_early_stats* early_host, uint64_t seq, int64_t timeout_us) {
+  RTKV_REQUIRE(early_host != nullptr, "null early-stats buffer");
+  const auto t0 = std::chrono::steady_clock::now();
+  for (uint32_t it = 0;; ++it) {
+    if (__atomic_load_n(&early_host->seq, __ATOMIC_ACQUIRE) == seq) return RTKV_OK;
+    if ((it & 255u) == 255u &&
+        std::chrono::duration_cast<std::chrono::microseconds>(std::chrono::steady_clock::now() - t0).count() >
+            timeout_us) {
+      set_error("rtkv: wait_early: the device did not publish the layer statistics in time");
+      return RTKV_ERR_TIMEOUT;
+    }
+    __builtin_ia32_pause();
+  }
+}
+
+void* rtkv_host_alloc(size_t bytes) {
+  void* p = nullptr;
+  if (hipHostMalloc(&p, bytes, hipHostMallocCoherent | hipHostMallocMapped) != hipSuccess) return nullptr;
+  std::memset(p, 0, bytes);
+  return p;
+}
+
+void rtkv_host_free(void* p) {
+  if (p) (void)hipHostFree(p);
 }
 
 int rtkv_compress_layer_qk_events(const rtkv_kv_desc* kv, const rtkv_qk_desc* q, const rtkv_layer_params* p,
@@ -445,6 +497,11 @@ int rtkv_tensor_fake_quant(const void* x_dev, int dtype, int64_t n_rows, int64_t
 
 int rtkv_selfcheck_division(int32_t dtype, unsigned long long* counts_dev, void* stream) {
   return launch_selfcheck_division(dtype, counts_dev, (hipStream_t)stream);
+}
+
+int rtkv_selfcheck_division_f32(int64_t s_lo, int64_t s_hi, int32_t ex, int32_t es, int32_t negative,
+                                unsigned long long* counts_dev, void* stream) {
+  return launch_selfcheck_division_f32(s_lo, s_hi, ex, es, negative, counts_dev, (hipStream_t)stream);
 }
 
 }  // extern "C"

@@ -220,6 +220,8 @@ struct FinalizeArgs {
   int mode_scores, mode_labels, mode_select;
   int fb_group;            // 1: select the top-10% fallback group alongside (set by launch_select)
   uint8_t* row_label;      // optional [B][cap] class of each kept row, for K4 (fast path writes it)
+  rtkv_early_stats* early = nullptr;  // optional host-mapped stats mirror (fast path only)
+  uint64_t early_seq = 0;
 };
 // K2 pipeline (select.hip).  sel_ws: select_workspace_bytes(B, S) bytes; `zeroed` = its first
 // select_zero_bytes(B) bytes and the stats are already zero (K1 clears them in rtkv_compress_layer).
@@ -243,7 +245,8 @@ struct QuantArgs {
   int32_t bits[3];
   rtkv_layer_out out;
   // Sequence shard (rtkv_quantize_rows_shard): kv holds tokens [row0, row0 + kv.S) of an S_glob-token
-  // selection; only kept rows inside that window are processed, padding rows only when pad_owner.
+  // selection; only kept rows inside that window are processed; padding rows get their zero scale/zp on
+  // every rank and their zero dequantized row only from the pad owner.
   // S_glob = 0: unsharded (S_glob = kv.S, every row processed).
   int64_t S_glob;
   int64_t row0;
@@ -276,5 +279,7 @@ int launch_tensor_params(const void* x, int dt, int64_t n_rows, int64_t row_len,
 int launch_tensor_fake_quant(const void* x, int dt, int64_t n_rows, int64_t row_len, const uint8_t* row_labels,
                              int label_value, int bits, const float* scale_zp, void* out, hipStream_t st);
 int launch_selfcheck_division(int dt, unsigned long long* counts, hipStream_t st);
+int launch_selfcheck_division_f32(int64_t s_lo, int64_t s_hi, int ex, int es, int neg, unsigned long long* counts,
+                                  hipStream_t st);
 
 }  // namespace rtkv

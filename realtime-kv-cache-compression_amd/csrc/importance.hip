@@ -336,6 +336,127 @@ __global__ __launch_bounds__(256) void aggregation_shfl_kernel(const typename Dt
   }
 }
 
+// Register path for fp32 with P = 4·CPR (CPR = 32 for P = 128): thread (token, chunk) streams one
+// 16-byte chunk (4 columns) of its token's prompt row for every head, as the 16-bit kernel above,
+// and the inner sum runs across the token's CPR lanes with shuffles in PyTorch's fp32 order
+// (Vectorized<float> = 8 lanes, so chunks 2m and 2m+1 form vector m):
+//   part_k[l] = Σ_j x[8(4j+k) + l]   (j = 0..NV/4-1 sequential from 0, k = 0..3)   row_sum ilp 4
+//   lane[l]   = part_0 + part_1 + part_2 + part_3, A = Σ_l lane[l] (l = 0..7)      vectorized_inner_sum
+// Chunk ch < 8 holds part_{ch/2}[(ch%2)*4 + e] after the first step; chunk 0 folds.
+template <int CPR, int HB = 16>
+__global__ __launch_bounds__(256) void aggregation_shfl32_kernel(const float* __restrict__ W, int H, int64_t S,
+                                                                 int64_t sb, int64_t sh, int64_t ss, int64_t lim,
+                                                                 float* __restrict__ A, AggExtras ex) {
+  constexpr int P = 4 * CPR;
+  constexpr int TT = 256 / CPR;  // tokens per block
+  constexpr int NV = CPR / 2;    // 8-column vectors
+  constexpr int NQ = NV / 4;
+  static_assert(NV % 4 == 0 && CPR <= 64, "aggregation_shfl32: CPR must be a multiple of 8, at most 64");
+  __shared__ float red[2][4];
+  zero_regions(ex);
+  const int b = blockIdx.y;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int tok = threadIdx.x / CPR, ch = threadIdx.x % CPR;
+  const int64_t i = (int64_t)blockIdx.x * TT + tok;
+  const bool valid = i < S;
+  const int64_t ic = valid ? i : S - 1;  // clamped row (its loads are discarded)
+  const float* base = W + b * sb + ic * ss + ch * 4;
+  float a0[4], a1[4], a2[4], a3[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) a0[k] = a1[k] = a2[k] = a3[k] = 0.f;
+  auto cascade = [&](int hh) {  // multi_row_sum: after every 16th head a1 += a0, every 256th a2 += a1, ...
+    if ((hh & 15) == 0) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) { a1[k] += a0[k]; a0[k] = 0.f; }
+      if ((hh & (15 << 4)) == 0) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) { a2[k] += a1[k]; a1[k] = 0.f; }
+        if ((hh & (15 << 8)) == 0) {
+#pragma unroll
+          for (int k = 0; k < 4; ++k) { a3[k] += a2[k]; a2[k] = 0.f; }
+        }
+      }
+    }
+  };
+  int h = 0;
+  while (h + HB <= H) {
+    uint4 v[HB];
+#pragma unroll
+    for (int j = 0; j < HB; ++j) v[j] = load16_nt(base + (int64_t)(h + j) * sh);
+#pragma unroll
+    for (int j = 0; j < HB; ++j) {
+      a0[0] += __uint_as_float(v[j].x);
+      a0[1] += __uint_as_float(v[j].y);
+      a0[2] += __uint_as_float(v[j].z);
+      a0[3] += __uint_as_float(v[j].w);
+      if (((h + j + 1) & 15) == 0) cascade(h + j + 1);
+    }
+    h += HB;
+  }
+  for (; h < H; ++h) {
+    const uint4 v = load16_nt(base + (int64_t)h * sh);
+    a0[0] += __uint_as_float(v.x);
+    a0[1] += __uint_as_float(v.y);
+    a0[2] += __uint_as_float(v.z);
+    a0[3] += __uint_as_float(v.w);
+    if (((h + 1) & 15) == 0) cascade(h + 1);
+  }
+  const float fH = (float)H;
+  float m[4];  // head means of columns ch*4 .. ch*4+3
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    float s = a0[k];
+    s += a1[k];
+    s += a2[k];
+    s += a3[k];
+    const int64_t col = ic * P + ch * 4 + k;
+    if (col >= lim) {  // columns past the 32-aligned block: row_sum (ilp 4) order
+      const float* colp = W + b * sb + ic * ss + ch * 4 + k;
+      s = row_sum_ilp4([&](int hh) { return colp[(int64_t)hh * sh]; }, H);
+    }
+    m[k] = s / fH;
+  }
+  const int tl = lane - ch;  // lane of this token's chunk 0
+  // part_{ch/2}[(ch%2)*4 + e] on chunks ch < 8: vectors m' = 4j + ch/2 live on chunks 8j + ch
+  float part[4];
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    float acc = 0.f;
+#pragma unroll
+    for (int j = 0; j < NQ; ++j) acc += __shfl(m[e], tl + 8 * j + (ch & 7), 64);
+    part[e] = acc;
+  }
+  float fin = 0.f;
+#pragma unroll
+  for (int l = 0; l < 8; ++l) {
+    const int hi = l >> 2, e = l & 3;
+    float p0 = __shfl(part[e], tl + hi, 64);
+    const float p1 = __shfl(part[e], tl + 2 + hi, 64), p2 = __shfl(part[e], tl + 4 + hi, 64),
+                p3 = __shfl(part[e], tl + 6 + hi, 64);
+    p0 += p1;
+    p0 += p2;
+    p0 += p3;
+    fin += p0;
+  }
+  const float Ai = fin;
+  float mn = INFINITY, mx = -INFINITY;
+  if (ch == 0 && valid) {
+    A[(int64_t)b * S + i] = Ai;
+    if (ex.t2 && b == 0) ex.t2[i] = ex.beta * ((S > 1) ? torch_logf((uint32_t)(i + 1)) / ex.logS : 0.f);
+    mn = mx = Ai;
+  }
+  if (ex.part) {  // block (min, max) of A for the score normalisation (token_importance.py:71-83)
+    mn = wave_min(mn);
+    mx = wave_max(mx);
+    if (lane == 0) { red[0][wave] = mn; red[1][wave] = mx; }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      ex.part[((int64_t)b * gridDim.x + blockIdx.x) * 2] = fminf(fminf(red[0][0], red[0][1]), fminf(red[0][2], red[0][3]));
+      ex.part[((int64_t)b * gridDim.x + blockIdx.x) * 2 + 1] = fmaxf(fmaxf(red[1][0], red[1][1]), fmaxf(red[1][2], red[1][3]));
+    }
+  }
+}
+
 // Generic path: any P / strides / alignment (scalar loads; the cfg1 P = 102 case lands here).
 template <int DT>
 __global__ __launch_bounds__(256) void aggregation_scalar_kernel(const typename Dt<DT>::S* __restrict__ W,
@@ -427,6 +548,15 @@ static int launch_agg_dt(const rtkv_attn_desc& w, int P, float* A, hipStream_t s
       dim3 grid((unsigned)((w.S + 15) / 16), (unsigned)w.B);
       if (x.nparts) *x.nparts = (int)grid.x;
       hipLaunchKernelGGL((aggregation_shfl_kernel<DT, 16>), grid, dim3(256), 0, st, W, H, w.S, w.stride_b,
+                         w.stride_h, w.stride_s, lim, A, x);
+      RTKV_HIP_CHECK(hipGetLastError());
+      return RTKV_OK;
+    }
+  } else {
+    if (aligned && P == 128 && !getenv("RTKV_K1_LDS")) {  // register path; RTKV_K1_LDS: cross-check knob
+      dim3 grid((unsigned)((w.S + 7) / 8), (unsigned)w.B);
+      if (x.nparts) *x.nparts = (int)grid.x;
+      hipLaunchKernelGGL((aggregation_shfl32_kernel<32>), grid, dim3(256), 0, st, W, H, w.S, w.stride_b,
                          w.stride_h, w.stride_s, lim, A, x);
       RTKV_HIP_CHECK(hipGetLastError());
       return RTKV_OK;

@@ -308,13 +308,54 @@ __global__ __launch_bounds__(256) void selfcheck_division_kernel(unsigned long l
   }
 }
 
+// fp32: the pairs (x, s) = (X·2^ex, S·2^es) with X = 1 + xm·2^-23 over EVERY mantissa xm, and
+// S = 1 + sm·2^-23 for sm in [s_lo, s_hi) (one workgroup per divisor); ex = es = 0 is the
+// mantissa-exhaustive proof obligation (see fast_div_ok), other exponents check the scaling
+// argument.  neg: negative dividends.  Only pairs the row gate admits are counted.
+__global__ __launch_bounds__(256) void selfcheck_division_f32_kernel(int64_t s_lo, float xscale, float sscale,
+                                                                     int neg, unsigned long long* counts) {
+  const uint32_t sm = (uint32_t)(s_lo + blockIdx.x);
+  const float s = __uint_as_float(0x3f800000u | sm) * sscale;
+  const float r = 1.f / s;
+  const float sg = neg ? -xscale : xscale;
+  unsigned long long checked = 0, bad = 0;
+  for (uint32_t xm = threadIdx.x; xm < (1u << 23); xm += blockDim.x) {
+    const float x = __uint_as_float(0x3f800000u | xm) * sg;
+    const float ax = __builtin_fabsf(x);
+    if (!fast_div_ok<RTKV_F32>(s, ax, ax)) continue;
+    const float q = fast_quotient(x, s, r);
+    const float ref = x / s;
+    ++checked;
+    bad += __builtin_bit_cast(uint32_t, q) != __builtin_bit_cast(uint32_t, ref);
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    checked += __shfl_xor(checked, o);
+    bad += __shfl_xor(bad, o);
+  }
+  if ((threadIdx.x & 63) == 0) {
+    atomicAdd(counts, checked);
+    atomicAdd(counts + 1, bad);
+  }
+}
+
+int launch_selfcheck_division_f32(int64_t s_lo, int64_t s_hi, int ex, int es, int neg, unsigned long long* counts,
+                                  hipStream_t st) {
+  RTKV_REQUIRE(counts, "selfcheck_division_f32: null counts");
+  RTKV_REQUIRE(0 <= s_lo && s_lo < s_hi && s_hi <= ((int64_t)1 << 23), "selfcheck_division_f32: bad divisor range");
+  RTKV_REQUIRE(ex >= -126 && ex <= 127 && es >= -126 && es <= 127, "selfcheck_division_f32: bad exponents");
+  hipLaunchKernelGGL(selfcheck_division_f32_kernel, dim3((unsigned)(s_hi - s_lo)), dim3(256), 0, st, s_lo,
+                     ldexpf(1.f, ex), ldexpf(1.f, es), neg, counts);
+  RTKV_HIP_CHECK(hipGetLastError());
+  return RTKV_OK;
+}
+
 int launch_selfcheck_division(int dt, unsigned long long* counts, hipStream_t st) {
   RTKV_REQUIRE(counts, "selfcheck_division: null counts");
   RTKV_HIP_CHECK(hipMemsetAsync(counts, 0, 2 * sizeof(unsigned long long), st));
   if (dt == RTKV_F16) hipLaunchKernelGGL((selfcheck_division_kernel<RTKV_F16>), dim3(0x7fff), dim3(256), 0, st, counts);
   else if (dt == RTKV_BF16) hipLaunchKernelGGL((selfcheck_division_kernel<RTKV_BF16>), dim3(0x7fff), dim3(256), 0, st, counts);
   else {
-    set_error("rtkv: selfcheck_division: fp32 rows always use the IEEE division");
+    set_error("rtkv: selfcheck_division: fp32 is checked per divisor range (rtkv_selfcheck_division_f32)");
     return RTKV_ERR_UNSUPPORTED;
   }
   RTKV_HIP_CHECK(hipGetLastError());

@@ -130,13 +130,18 @@ struct RowParams {
 //   fp16: every finite x and every positive finite s;
 //   bf16: 2^-62 <= s <= 2^62, |x| <= 2^62, and x == 0 or |x| >= 2^-48·s (tiny quotients below
 //         ~2^-57 are where the correction step can be off; the row gate excludes them).
-// fp32 rows always use the IEEE division (the domain cannot be enumerated).
-// amax = max |x| over the row, amin_nz = min |x| over the nonzero elements (bf16 only).
+//   fp32: 2^-100 <= s <= 2^100, |x| <= 2^100·s, and x == 0 or |x| >= max(2^-60, 2^-100·s).  Then
+//         1/s, x·r, the residual and the quotient are all normal numbers, so every step commutes
+//         with scaling x and s by powers of two, and the pair reduces to its mantissas
+//         (X, S) in [1, 2)^2: all 2^46 of them are enumerated (rtkv_selfcheck_division_f32).
+// amax = max |x| over the row, amin_nz = min |x| over the nonzero elements (bf16 and fp32).
 template <int DT> __device__ __forceinline__ bool fast_div_ok(float s, float amax, float amin_nz) {
   if constexpr (DT == RTKV_F16) return s > 0.f && s < INFINITY;  // false for NaN
   else if constexpr (DT == RTKV_BF16)
     return s >= 0x1p-62f && s <= 0x1p62f && amax <= 0x1p62f && amin_nz >= s * 0x1p-48f;
-  else return false;
+  else
+    return s >= 0x1p-100f && s <= 0x1p100f && amax <= s * 0x1p100f && amin_nz >= 0x1p-60f &&
+           amin_nz >= s * 0x1p-100f;
 }
 __device__ __forceinline__ float fast_quotient(float x, float s, float r) {
   const float q0 = x * r;
@@ -217,11 +222,13 @@ template <int W> __device__ __forceinline__ void pack_store(uint8_t* dst, const 
   }
 }
 
+// Contiguous fp32 rows of exactly 4096 elements fit 128 VGPRs (4 waves/SIMD); the gate bookkeeping would push the
+// compiler to 129 (3 waves) without the bound.  Wider fp32 rows keep the 256-register budget.
 // Row geometry shared by every task of a launch: element f of a row lives at (f / D) * stride_h + f % D.
 // CONTIG (stride_h == D on input and output) makes that plain f.  FULL: the row is exactly NCH*64
 // chunks of 8 (F a multiple of 512), so no lane is idle and packed rows stay 16-byte aligned.
 template <int DT, int NCH, bool CONTIG, bool FULL>
-__global__ __launch_bounds__(256, 2) void quant_rows_kernel(QuantArgs a) {
+__global__ __launch_bounds__(256, (DT == RTKV_F32 && NCH == 8 && FULL && CONTIG) ? 4 : 2) void quant_rows_kernel(QuantArgs a) {
   using S_ = typename Dt<DT>::S;
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -265,16 +272,16 @@ __global__ __launch_bounds__(256, 2) void quant_rows_kernel(QuantArgs a) {
     int lab = (r < kept_b) ? (a.row_label ? (int)a.row_label[(int64_t)b * cap + r] : (int)a.labels[(int64_t)b * S + i]) : 0;
     i = __builtin_amdgcn_readfirstlane(i);
     lab = __builtin_amdgcn_readfirstlane(lab);
-    if (shard) {  // another rank's token, or a padding row this rank does not own
-      if (r < kept_b ? (i < row0 || i >= row1) : !a.pad_owner) continue;
-    }
+    // shard: skip another rank's token; padding rows' zero scale/zp are written by every rank (the
+    // exchange carries kept rows only), their zero dequantized rows by the pad owner alone
+    if (shard && r < kept_b && (i < row0 || i >= row1)) continue;
     const int rloc = a.shard_ranges ? r - (int)a.shard_ranges[((int64_t)b * (a.shard_nranks + 1) + a.shard_rank) * 2] : r;
     S_* orow = emit_deq ? static_cast<S_*>(which ? a.out.v_out_dev : a.out.k_out_dev) + b * osb +
                               (int64_t)rloc * a.out.o_stride_s
                         : nullptr;
     const int64_t sz_idx = ((int64_t)b * cap + r) * 4 + which * 2;
     if (r >= kept_b || lab > 2) {  // zero padding row (selective_propagation.py:214-222)
-      if (emit_deq) {
+      if (emit_deq && (!shard || a.pad_owner)) {
         const Chunk<DT> z = f32_to_chunk<DT>({0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f});
 #pragma unroll
         for (int k = 0; k < NCH; ++k)
@@ -302,13 +309,13 @@ __global__ __launch_bounds__(256, 2) void quant_rows_kernel(QuantArgs a) {
         for (int e = 0; e < 8; ++e) {
           mn = fminf(mn, x[e]);
           mx = fmaxf(mx, x[e]);
-          if constexpr (DT == RTKV_BF16) anz = fminf(anz, x[e] != 0.f ? __builtin_fabsf(x[e]) : INFINITY);
+          if constexpr (DT != RTKV_F16) anz = fminf(anz, x[e] != 0.f ? __builtin_fabsf(x[e]) : INFINITY);
         }
       }
     }
     mn = wave_min(mn);
     mx = wave_max(mx);
-    if constexpr (DT == RTKV_BF16) anz = wave_min(anz);
+    if constexpr (DT != RTKV_F16) anz = wave_min(anz);
     const RowParams rp = row_params<DT>(mn, mx, bits, anz);
     if (a.out.scale_zp_dev && lane < 2) a.out.scale_zp_dev[sz_idx + lane] = lane == 0 ? rp.scale : rp.zp;
     uint8_t* pk = emit_pk ? (which ? a.out.packed_v_dev : a.out.packed_k_dev) + a.out.row_offset_dev[(int64_t)b * cap + r]
@@ -348,12 +355,8 @@ __global__ __launch_bounds__(256, 2) void quant_rows_kernel(QuantArgs a) {
         default: process(std::integral_constant<int, 16>{}, ftag); break;  // launcher guarantees w in {2,4,8,16}
       }
     };
-    if constexpr (DT != RTKV_F32) {
-      if (__builtin_amdgcn_readfirstlane((int)rp.fast)) by_width(std::true_type{});
-      else by_width(std::false_type{});
-    } else {
-      by_width(std::false_type{});
-    }
+    if (__builtin_amdgcn_readfirstlane((int)rp.fast)) by_width(std::true_type{});
+    else by_width(std::false_type{});
   }
 }
 
@@ -381,13 +384,13 @@ __global__ __launch_bounds__(256) void quant_rows_generic_kernel(QuantArgs a) {
     const int64_t kept_b = a.kept_index ? bst[b].kept : S;
     const int64_t i = (r < kept_b) ? (a.kept_index ? a.kept_index[b * cap + r] : r) : 0;
     const int lab = (r < kept_b) ? a.labels[b * S + i] : 0;
-    if (shard && (r < kept_b ? (i < row0 || i >= row1) : !a.pad_owner)) continue;
+    if (shard && r < kept_b && (i < row0 || i >= row1)) continue;  // padding rows: as quant_rows_kernel
     const int64_t rloc = a.shard_ranges ? r - a.shard_ranges[(b * (a.shard_nranks + 1) + a.shard_rank) * 2] : r;
     S_* orow = emit_deq ? static_cast<S_*>(which ? a.out.v_out_dev : a.out.k_out_dev) + b * osb + rloc * a.out.o_stride_s
                         : nullptr;
     auto oaddr = [&](int64_t f) { return (f / D) * a.out.o_stride_h + (f % D); };
     if (r >= kept_b || lab > 2) {
-      if (emit_deq)
+      if (emit_deq && (!shard || a.pad_owner))
         for (int64_t f = lane; f < F; f += 64) orow[oaddr(f)] = Dt<DT>::store(0.f);
       if (a.out.scale_zp_dev && lane < 2) a.out.scale_zp_dev[(b * cap + r) * 4 + which * 2 + lane] = 0.f;
       continue;

@@ -97,6 +97,8 @@ struct FastArgs {
   float bin_lo[kGrp];              // bin(s) = clamp(floor((s - lo) * inv), 0, kNBin - 1): monotone in s
   float bin_inv[kGrp];
   int hist_fb;                     // histogram the fallback group too (fallback possible)
+  rtkv_early_stats* early;         // host-mapped stats mirror (nullable), published by F1's last workgroup
+  uint64_t early_seq;
 };
 
 __device__ __forceinline__ float key_score(uint32_t k) {
@@ -327,6 +329,7 @@ __device__ __forceinline__ void select_thresholds(const FastArgs& g, uint32_t* h
   // ---- quotas: the greedy in closed form (selective_propagation.py:93-131), every thread
   int mode[kGrp];
   int need[kGrp];
+  int64_t quota[3];  // kept tokens per class (final unless the fallback runs)
   {
     const double u8 = 8.0 * ((double)S * a.p.propagation_ratio);
     const int64_t U = (u8 >= 0.0) ? (u8 >= 9.0e18 ? (int64_t)9000000000000000000LL : (int64_t)floor(u8)) : -1;
@@ -345,6 +348,7 @@ __device__ __forceinline__ void select_thresholds(const FastArgs& g, uint32_t* h
       used += n * (bb > 0 ? bb : 0);
       kept += n;
       need[k] = (int)n;
+      quota[k] = n;
       mode[k] = (n == 0) ? M_NONE : (n == N ? M_ALL : M_PART);
     }
     int64_t kf = (int64_t)((double)S * 0.1);
@@ -447,6 +451,48 @@ __device__ __forceinline__ void select_thresholds(const FastArgs& g, uint32_t* h
       if (ccount[q] > 0 && a.p.bits[q] >= 16) flags |= RTKV_FLAG_F16_QMAX_OVERFLOW;
   hs->error_flags = flags;
   hs->B = 1;
+  if (!fallback) {  // the kept counts are the quotas: final here (F2 adds only the score sums)
+    int64_t n = 0, units = 0, bytes = 0;
+    for (int q = 0; q < 3; ++q) {
+      bs->kept_class[q] = quota[q];
+      n += quota[q];
+      units += quota[q] * (int64_t)a.p.bits[q];
+      bytes += quota[q] * row_bytes(a, q);
+    }
+    bs->kept = n;
+    bs->cost_units = units;
+    bs->packed_bytes = bytes;
+    hs->max_kept = n;
+    hs->total_packed_bytes = bytes;
+  }
+  if (g.early) {  // host-mapped mirror for the caller's early return (rtkv_compress_layer_early)
+    rtkv_early_stats* e = g.early;
+    auto put64 = [](void* dst, uint64_t v) {
+      __hip_atomic_store(reinterpret_cast<uint64_t*>(dst), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    };
+    auto put32 = [](void* dst, uint32_t v) {
+      __hip_atomic_store(reinterpret_cast<uint32_t*>(dst), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    };
+    put32(&e->complete, fallback ? 0u : 1u);
+    if (!fallback) {
+      put64(&e->stats.max_kept, (uint64_t)bs->kept);
+      put64(&e->stats.total_packed_bytes, (uint64_t)bs->packed_bytes);
+      put64(&e->stats.score_sum, __builtin_bit_cast(uint64_t, ssum));
+      put32(&e->stats.score_min, __builtin_bit_cast(uint32_t, hs->score_min));
+      put32(&e->stats.score_max, __builtin_bit_cast(uint32_t, hs->score_max));
+      put32(&e->stats.error_flags, (uint32_t)flags);
+      put32(&e->stats.B, 1u);
+      for (int q = 0; q < 3; ++q) {
+        put64(&e->batch.class_count[q], (uint64_t)ccount[q]);
+        put64(&e->batch.kept_class[q], (uint64_t)quota[q]);
+      }
+      put64(&e->batch.kept, (uint64_t)bs->kept);
+      put64(&e->batch.cost_units, (uint64_t)bs->cost_units);
+      put64(&e->batch.packed_bytes, (uint64_t)bs->packed_bytes);
+      put32(&e->batch.fallback, 0u);
+    }
+    __hip_atomic_store(&e->seq, g.early_seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
   FastSel* fs = g.L.sel;
   for (int q = 0; q < kGrp; ++q) {
     fs->mode[q] = mode[q];
@@ -690,17 +736,19 @@ __global__ __launch_bounds__(kST) void fsel_compact_kernel(FastArgs g) {
       unsigned long long n = 0, units = 0, bytes = 0;
       for (int q = 0; q < 3; ++q) {
         const unsigned long long nq = fld(kept_tot, q);
-        if (nq) atomicAdd((unsigned long long*)&bs->kept_class[q], nq);
+        if (nq && fallback) atomicAdd((unsigned long long*)&bs->kept_class[q], nq);
         n += nq;
         units += nq * (unsigned long long)a.p.bits[q];
         bytes += nq * (unsigned long long)rb[q];
       }
       if (n) {
-        atomicAdd((unsigned long long*)&bs->kept, n);
-        atomicAdd((unsigned long long*)&bs->cost_units, units);
-        atomicAdd((unsigned long long*)&bs->packed_bytes, bytes);
-        atomicAdd((unsigned long long*)&hs->max_kept, n);
-        atomicAdd((unsigned long long*)&hs->total_packed_bytes, bytes);
+        if (fallback) {  // otherwise F1 wrote the final counts (the quotas)
+          atomicAdd((unsigned long long*)&bs->kept, n);
+          atomicAdd((unsigned long long*)&bs->cost_units, units);
+          atomicAdd((unsigned long long*)&bs->packed_bytes, bytes);
+          atomicAdd((unsigned long long*)&hs->max_kept, n);
+          atomicAdd((unsigned long long*)&hs->total_packed_bytes, bytes);
+        }
         atomicAdd(&bs->kept_score_sum, x);
       }
       atomicAdd(&hs->score_m2, y);
@@ -751,6 +799,8 @@ int launch_select_fast(const FinalizeArgs& f, void* ws, bool zeroed, hipStream_t
   RTKV_REQUIRE(select_fast_eligible(f), "select_fast: not eligible");
   FastArgs g;
   g.f = f;
+  g.early = f.early;
+  g.early_seq = f.early_seq;
   char* p = static_cast<char*>(ws);
   g.L.head = reinterpret_cast<FastHead*>(p);
   p += sizeof(FastHead);

@@ -19,7 +19,9 @@ LIB_PATH = os.environ.get("RTKV_LIB", os.path.join(ROOT, "librtkv.so"))
 F32, F16, BF16 = 0, 1, 2
 EMIT_DEQUANT, EMIT_PACKED, NO_SELECTION, NO_FALLBACK, SELECT_PIPELINE = 1, 2, 4, 8, 16
 FLAG_F16_QMAX_OVERFLOW = 1
-ERR_NAMES = {-1: "RTKV_ERR_INVALID", -2: "RTKV_ERR_UNSUPPORTED", -3: "RTKV_ERR_HIP", -4: "RTKV_ERR_WORKSPACE"}
+ERR_NAMES = {-1: "RTKV_ERR_INVALID", -2: "RTKV_ERR_UNSUPPORTED", -3: "RTKV_ERR_HIP", -4: "RTKV_ERR_WORKSPACE",
+             -5: "RTKV_ERR_TIMEOUT"}
+ERR_TIMEOUT = -5
 
 TORCH_DTYPE_CODE = {torch.float32: F32, torch.float16: F16, torch.bfloat16: BF16}
 
@@ -69,6 +71,12 @@ class LayerOut(ctypes.Structure):
                 ("packed_capacity", c_i64), ("row_offset_dev", c_p), ("scale_zp_dev", c_p), ("stats_dev", c_p)]
 
 
+class EarlyStats(ctypes.Structure):
+    """rtkv_early_stats: the layer statistics the device publishes to host memory (B = 1)."""
+    _fields_ = [("seq", ctypes.c_uint64), ("complete", c_i32), ("reserved", c_i32), ("stats", LayerStatsHeader),
+                ("batch", BatchStats)]
+
+
 def stats_bytes(B: int) -> int:
     return ctypes.sizeof(LayerStatsHeader) + B * ctypes.sizeof(BatchStats)
 
@@ -94,6 +102,7 @@ _SIGS = {
     "rtkv_tensor_quant_params": ([c_p, c_i32, c_i64, c_i64, c_p, c_i32, c_i32, c_p, c_p, c_sz, c_p], c_i32),
     "rtkv_tensor_fake_quant": ([c_p, c_i32, c_i64, c_i64, c_p, c_i32, c_i32, c_p, c_p, c_p], c_i32),
     "rtkv_selfcheck_division": ([c_i32, c_p, c_p], c_i32),
+    "rtkv_selfcheck_division_f32": ([c_i64, c_i64, c_i32, c_i32, c_i32, c_p, c_p], c_i32),
     "rtkv_attention_aggregation_shard": ([c_p, c_i32, c_i64, c_i64, c_p, c_p], c_i32),
     "rtkv_finalize_select": ([c_p, c_i32, c_i64, c_i64, c_p, c_p, c_i64, c_i32, c_p, c_sz, c_p], c_i32),
     "rtkv_quantize_rows_shard": ([c_p, c_i64, c_i64, c_i32, c_i32, c_p, c_p, c_p, c_p, c_p, c_p], c_i32),
@@ -102,6 +111,11 @@ _SIGS = {
     "rtkv_attention_lse": ([c_p, c_p, c_p], c_i32),
     "rtkv_compress_layer_qk": ([c_p, c_p, c_p, c_p, c_p, c_sz, c_p], c_i32),
     "rtkv_compress_layer_qk_events": ([c_p, c_p, c_p, c_p, c_p, c_sz, c_p, c_p], c_i32),
+    "rtkv_compress_layer_early": ([c_p, c_p, c_p, c_p, c_p, c_sz, c_p, c_p, ctypes.c_uint64, c_p], c_i32),
+    "rtkv_compress_layer_qk_early": ([c_p, c_p, c_p, c_p, c_p, c_sz, c_p, c_p, ctypes.c_uint64, c_p], c_i32),
+    "rtkv_wait_early": ([c_p, ctypes.c_uint64, c_i64], c_i32),
+    "rtkv_host_alloc": ([c_sz], c_p),
+    "rtkv_host_free": ([c_p], None),
     "rtkv_gather_rows": ([c_p, c_i64, c_i64, c_i64, c_p, c_i64, c_i64, c_p, c_i64, c_i64, c_p, c_p], c_i32),
     "rtkv_decode_workspace_size": ([c_i64, c_i64, c_i64, c_i64, c_i64], c_sz),
     "rtkv_decode_attention_packed": ([c_p, c_p, c_i64, c_p, c_p, c_p, c_p, c_i64, c_i64, c_i64, c_p, c_i64, c_i64, c_i32, c_p,

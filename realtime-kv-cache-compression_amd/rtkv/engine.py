@@ -138,6 +138,45 @@ def decode_stats(raw: bytes, B: int) -> LayerStats:
                       h.error_flags, rows)
 
 
+def _early_to_stats(e: L.EarlyStats) -> LayerStats:
+    """Statistics published early by the device (score_m2 / kept_score_sum are not final there)."""
+    h, b = e.stats, e.batch
+    row = dict(class_count=list(b.class_count), kept=b.kept, kept_class=list(b.kept_class), cost_units=b.cost_units,
+               packed_bytes=b.packed_bytes, fallback=bool(b.fallback), kept_score_sum=float("nan"))
+    return LayerStats(h.max_kept, h.total_packed_bytes, h.score_sum, float("nan"), h.score_min, h.score_max,
+                      h.error_flags, [row])
+
+
+class EarlyStatsBuffer:
+    """Host-mapped rtkv_early_stats (rtkv_host_alloc) that the device fills with a layer's final
+    counts as soon as K2 has its thresholds, plus the call sequence counter (one per device)."""
+
+    TIMEOUT_US = 20_000_000
+
+    def __init__(self):
+        self._lib = L.lib()
+        self.ptr = self._lib.rtkv_host_alloc(ctypes.sizeof(L.EarlyStats))
+        if not self.ptr:
+            raise RuntimeError("rtkv: rtkv_host_alloc failed (pinned host memory for the early statistics)")
+        self.seq = 0
+
+    def next_seq(self) -> int:
+        self.seq += 1
+        return self.seq
+
+    def wait(self, seq: int) -> L.EarlyStats:
+        rc = self._lib.rtkv_wait_early(self.ptr, seq, self.TIMEOUT_US)
+        if rc == L.ERR_TIMEOUT:
+            torch.cuda.synchronize()  # surfaces a device fault, if that is what happened
+        L.check(rc, "rtkv_wait_early")
+        return L.EarlyStats.from_buffer_copy(ctypes.string_at(self.ptr, ctypes.sizeof(L.EarlyStats)))
+
+    def __del__(self):
+        if getattr(self, "ptr", None):
+            self._lib.rtkv_host_free(self.ptr)
+            self.ptr = None
+
+
 class Workspace:
     """Caller-owned scratch for the C ABI, grown on demand (one per device)."""
 
@@ -222,18 +261,34 @@ class LayerBuffers:
 
 
 class LayerResult:
-    """Device outputs of one rtkv_compress_layer call; ``stats()`` is the single host sync."""
+    """Device outputs of one rtkv_compress_layer call; ``stats()`` is the single host sync.
 
-    def __init__(self, bufs: LayerBuffers, B: int):
+    With early statistics (``early`` set: the call published them), ``stats()`` waits only for the
+    device's publication — K2's tail and K4 may still be running — and its score_m2 /
+    kept_score_sum are NaN; ``final_stats()`` syncs the stream and reads them all."""
+
+    def __init__(self, bufs: LayerBuffers, B: int, early: Optional[EarlyStatsBuffer] = None, seq: int = 0):
         self.bufs = bufs
         self.B = B
+        self._early, self._seq = early, seq
         self._stats: Optional[LayerStats] = None
+        self._final: Optional[LayerStats] = None
 
     def stats(self) -> LayerStats:
         if self._stats is None:
-            raw = self.bufs.stats.cpu().numpy().tobytes()  # D2H copy on the current stream + sync
-            self._stats = decode_stats(raw, self.B)
+            if self._early is not None:
+                e = self._early.wait(self._seq)
+                if e.complete:
+                    self._stats = _early_to_stats(e)
+                    return self._stats
+            self._stats = self.final_stats()
         return self._stats
+
+    def final_stats(self) -> LayerStats:
+        if self._final is None:
+            raw = self.bufs.stats.cpu().numpy().tobytes()  # D2H copy on the current stream + sync
+            self._final = decode_stats(raw, self.B)
+        return self._final
 
     def kv(self):
         """Dequantized (K', V') as contiguous [B, S'_max, F] views (reference return value)."""
@@ -245,7 +300,7 @@ class LayerResult:
 
 def compress_layer_qk(K, V, Q, lse, params: L.LayerParams, bufs: LayerBuffers, workspace: Workspace,
                       layout: str = "bsf", causal: bool = True, scale: Optional[float] = None,
-                      stream: Optional[int] = None) -> LayerResult:
+                      stream: Optional[int] = None, early: Optional[EarlyStatsBuffer] = None) -> LayerResult:
     """compress_layer in the fused importance mode: K1' computes A from Q, the prompt keys (the first
     P rows of K) and the row LSE on MFMA; K2 and K4 are unchanged."""
     L.require_device(K, V, Q, lse)
@@ -257,6 +312,13 @@ def compress_layer_qk(K, V, Q, lse, params: L.LayerParams, bufs: LayerBuffers, w
     out = bufs.out_struct()
     out.o_stride_h = kd.D
     st = L.stream_ptr(K.device) if stream is None else stream
+    if early is not None:
+        seq, pub = early.next_seq(), ctypes.c_int32(0)
+        rc = L.lib().rtkv_compress_layer_qk_early(ctypes.byref(kd), ctypes.byref(qd), ctypes.byref(params),
+                                                  ctypes.byref(out), ws.data_ptr(), ws.numel(), st, early.ptr, seq,
+                                                  ctypes.byref(pub))
+        L.check(rc, "rtkv_compress_layer_qk_early")
+        return LayerResult(bufs, kd.B, early if pub.value else None, seq)
     rc = L.lib().rtkv_compress_layer_qk(ctypes.byref(kd), ctypes.byref(qd), ctypes.byref(params), ctypes.byref(out),
                                         ws.data_ptr(), ws.numel(), st)
     L.check(rc, "rtkv_compress_layer_qk")
@@ -286,7 +348,8 @@ def attention_lse(Q, K, causal: bool = True, scale: Optional[float] = None, k_la
 
 
 def compress_layer(K, V, W, params: L.LayerParams, bufs: LayerBuffers, workspace: Workspace,
-                   layout: str = "bsf", stream: Optional[int] = None) -> LayerResult:
+                   layout: str = "bsf", stream: Optional[int] = None,
+                   early: Optional[EarlyStatsBuffer] = None) -> LayerResult:
     """Enqueue aggregation → scores/labels/selection → quantize+pack+compact for one layer."""
     L.require_device(K, V, W)
     kd = kv_desc(K, V, layout)
@@ -297,6 +360,13 @@ def compress_layer(K, V, W, params: L.LayerParams, bufs: LayerBuffers, workspace
     out = bufs.out_struct()
     out.o_stride_h = kd.D  # output rows are [H, D] row-major whatever the input layout
     st = L.stream_ptr(K.device) if stream is None else stream
+    if early is not None:
+        seq, pub = early.next_seq(), ctypes.c_int32(0)
+        rc = L.lib().rtkv_compress_layer_early(ctypes.byref(kd), ctypes.byref(wd), ctypes.byref(params),
+                                               ctypes.byref(out), ws.data_ptr(), ws.numel(), st, early.ptr, seq,
+                                               ctypes.byref(pub))
+        L.check(rc, "rtkv_compress_layer_early")
+        return LayerResult(bufs, kd.B, early if pub.value else None, seq)
     rc = L.lib().rtkv_compress_layer(ctypes.byref(kd), ctypes.byref(wd), ctypes.byref(params), ctypes.byref(out),
                                      ws.data_ptr(), ws.numel(), st)
     L.check(rc, "rtkv_compress_layer")

@@ -18,6 +18,11 @@ three steps without that tensor:
    attention, not part of the compression path).
 
 Inputs are the post-RoPE states the reference layer has at :64-75, in its [B, heads, S, D] layout.
+
+Limits at this boundary (checked, ValueError): the states are float16 or bfloat16 with head_dim 64 or
+128 (the MFMA LSE and K1' kernels), and the model's attention_mask, when given, must be the plain
+causal mask — a padded batch (padding columns in the mask, modified_llama.py:90-91) is rejected
+rather than silently scored as unpadded.
 """
 from __future__ import annotations
 
@@ -42,13 +47,25 @@ class CompressedPrefillAttention:
         self.position_mask = position_mask
 
     def __call__(self, query_states: torch.Tensor, key_states: torch.Tensor, value_states: torch.Tensor,
-                 input_ids: Optional[torch.Tensor] = None) -> Tuple[torch.Tensor, Tuple[torch.Tensor, torch.Tensor], Dict]:
+                 input_ids: Optional[torch.Tensor] = None,
+                 attention_mask: Optional[torch.Tensor] = None) -> Tuple[torch.Tensor, Tuple[torch.Tensor, torch.Tensor], Dict]:
         """query [B,H,S,D], key/value [B,Hkv,S,D] (post-RoPE) → (attn_output [B,H,S,D] before o_proj,
-        (K' [B,Hkv,S',D], V' [B,Hkv,S',D]) for the cache, compression_info)."""
+        (K' [B,Hkv,S',D], V' [B,Hkv,S',D]) for the cache, compression_info).  attention_mask: the
+        model's additive [B, 1, S, S] mask (optional; only the causal mask is accepted)."""
         B, H, S, D = query_states.shape
         Hkv = key_states.shape[1]
         if H != self.num_heads or Hkv != self.num_kv_heads or D != self.head_dim:
             raise ValueError("state shapes do not match the layer's head configuration")
+        if query_states.dtype not in (torch.float16, torch.bfloat16) or D not in (64, 128):
+            raise ValueError(f"CompressedPrefillAttention needs float16/bfloat16 states with head_dim 64 or 128 "
+                             f"(got {query_states.dtype}, head_dim {D}); fp32 models use the reference attention "
+                             f"with RealTimePrefillCompressor.compress_layer_kv_cache")
+        if attention_mask is not None:
+            m = attention_mask[..., :S, :S]
+            causal = torch.ones(S, S, dtype=torch.bool, device=m.device).tril()
+            if m.dim() != 4 or not bool(torch.equal((m >= 0).expand(B, 1, S, S), causal.expand(B, 1, S, S))):
+                raise ValueError("attention_mask is not the plain causal mask (padded batches are not supported by "
+                                 "the fused importance mode)")
         Q = query_states.contiguous()
         # [B, S, Hkv·D] keys/values as the reference reshapes them for the compressor (:104-107)
         k_bsf = key_states.transpose(1, 2).reshape(B, S, Hkv * D).contiguous()
@@ -65,11 +82,14 @@ class CompressedPrefillAttention:
             keys, vals = ck, cv
             if self.position_mask:
                 # causal over the kept positions: key j (source token kept_index[b, j]) ≤ query i
+                # (sync-free: each kept token lands at its rank among the row's kept tokens; dropped
+                # tokens all land in a spare column that is cut off)
                 pos = info["propagation_info"]["selection_mask"]
-                kept_pos = torch.full((B, Sp), S, dtype=torch.long, device=Q.device)
-                for b in range(B):
-                    idx = pos[b].nonzero().flatten()
-                    kept_pos[b, : idx.numel()] = idx
+                rank = pos.long().cumsum(-1) - 1
+                tgt = torch.where(pos, rank, torch.full_like(rank, Sp))
+                kp = torch.full((B, Sp + 1), S, dtype=torch.long, device=Q.device)
+                kp.scatter_(1, tgt, torch.arange(S, device=Q.device).expand(B, S))
+                kept_pos = kp[:, :Sp]
                 mask = kept_pos[:, None, None, :] <= torch.arange(S, device=Q.device)[None, None, :, None]
                 # a query before the first kept position sees no key: its output is zero
                 empty = ~mask.any(dim=-1, keepdim=True)

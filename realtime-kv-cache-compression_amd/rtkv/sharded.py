@@ -293,7 +293,11 @@ class ShardedPrefillCompressor:
     def compress_layer_kv_cache(self, key_states, value_states, attention_weights, input_ids, layer_idx):
         """Rank-local twin of RealTimePrefillCompressor.compress_layer_kv_cache: compresses this rank's
         token chunk against the global selection and returns its dequantized kept rows, with the
-        exchanged packed KV of the layer in ``info['shard']``."""
+        exchanged packed KV of the layer in ``info['shard']``.  Layers enqueued with enqueue_layer must
+        be exchanged first (their results would otherwise be returned here)."""
+        if self._queued or self._issued or self._pending:
+            raise RuntimeError("compress_layer_kv_cache: layers enqueued with enqueue_layer are still pending; "
+                               "call exchange() first")
         self.enqueue_layer(key_states, value_states, attention_weights, layer_idx)
         (sl,) = self.exchange()
         k, v = sl.local_kv(self.rank)

@@ -15,24 +15,29 @@ import torch
 
 from . import _lib as L
 from .dynamic_quantization import F16_OVERFLOW_MSG, DynamicPrecisionQuantizer
-from .engine import LayerBuffers, Workspace, compress_layer, compress_layer_qk, params_from_config, prompt_length
+from .engine import (EarlyStatsBuffer, LayerBuffers, Workspace, compress_layer, compress_layer_qk, params_from_config,
+                     prompt_length)
 from .selective_propagation import SelectiveTokenPropagator
 from .token_importance import LayerWiseImportanceTracker
 
 
-class _LazyDict(dict):
-    """A dict whose listed keys are computed on first access (then stored)."""
+class _Lazy:
+    """A value computed on first access (the host copy or sync it needs is deferred until then)."""
+    __slots__ = ("fn",)
 
-    def __init__(self, base, **lazy):
-        super().__init__(base)
-        self._lazy = lazy
-        for k in lazy:
-            dict.__setitem__(self, k, None)
+    def __init__(self, fn):
+        self.fn = fn
+
+
+class _LazyDict(dict):
+    """A dict whose _Lazy values are computed on first access (then stored); key order is kept."""
 
     def __getitem__(self, key):
-        if key in self._lazy:
-            dict.__setitem__(self, key, self._lazy.pop(key)())
-        return dict.__getitem__(self, key)
+        v = dict.__getitem__(self, key)
+        if isinstance(v, _Lazy):
+            v = v.fn()
+            dict.__setitem__(self, key, v)
+        return v
 
     def get(self, key, default=None):
         return self[key] if key in self else default
@@ -42,6 +47,12 @@ class _LazyDict(dict):
 
     def items(self):
         return [(k, self[k]) for k in self.keys()]
+
+    def copy(self):
+        return dict(self.items())
+
+    def __repr__(self):
+        return repr(self.copy())
 
 
 class RealTimePrefillCompressor:
@@ -58,6 +69,7 @@ class RealTimePrefillCompressor:
         # extension: keep the bit-packed codes of every layer (compression_layers.CompressedKVCache)
         self.emit_packed = emit_packed
         self._workspaces: Dict[torch.device, Workspace] = {}
+        self._early: Dict[torch.device, EarlyStatsBuffer] = {}
 
     # ------------------------------------------------------------------ reference API
     def identify_prompt_tokens(self, input_ids: torch.Tensor, special_tokens: Optional[List[int]] = None):
@@ -103,13 +115,20 @@ class RealTimePrefillCompressor:
         flags = L.EMIT_DEQUANT | (L.EMIT_PACKED if emit_packed else 0)
         params = params_from_config(self.config, layer_idx, P, ratio, flags)
         bufs = LayerBuffers(B, S, F, K.dtype, K.device, bits, emit_dequant=True, emit_packed=emit_packed)
-        ws = self._workspaces.setdefault(K.device, Workspace(K.device))
+        ws = self._workspaces.get(K.device)
+        if ws is None:
+            ws = self._workspaces[K.device] = Workspace(K.device)
+        early = self._early.get(K.device)
+        if early is None:
+            early = self._early[K.device] = EarlyStatsBuffer()
         if fused:
             Q = query_states if query_states.stride(-1) == 1 else query_states.contiguous()
-            res = compress_layer_qk(K, V, Q, attention_lse.contiguous(), params, bufs, ws, causal=causal)
+            res = compress_layer_qk(K, V, Q, attention_lse.contiguous(), params, bufs, ws, causal=causal, early=early)
         else:
-            res = compress_layer(K, V, W, params, bufs, ws)
-        st = res.stats()  # the one host sync of the layer
+            res = compress_layer(K, V, W, params, bufs, ws, early=early)
+        # the one host wait of the layer: the device publishes S' and the counts as soon as K2 has its
+        # thresholds, so the views below are built while K2's tail and K4 still run (stream-ordered)
+        st = res.stats()
         if st.error_flags & L.FLAG_F16_QMAX_OVERFLOW:
             raise RuntimeError(F16_OVERFLOW_MSG)
         selected_keys, selected_values = res.kv()
@@ -129,13 +148,17 @@ class RealTimePrefillCompressor:
                            "high_ratio": high / n, "medium_ratio": medium / n, "low_ratio": low / n}
         # bit_assignments is the reference's host int64 array (unified_compressor.py:125-129); it is
         # copied on first access so the layer keeps a single host sync
-        quant_info = _LazyDict({"scales": {}, "zero_points": {}},
-                               bit_assignments=lambda labels=bufs.labels: labels.long().cpu().numpy())
-        selection_stats = self.propagator._selection_info(scores, st, ratio, S)
-        propagation_info = {"layer_idx": layer_idx, "propagation_ratio": ratio, "original_length": S,
-                            "max_selected_length": Sp, "selection_mask": bufs.mask.view(torch.bool),
-                            "selection_stats": selection_stats}
-        std = (st.score_m2 / (n - 1)) ** 0.5 if n > 1 else float("nan")
+        quant_info = _LazyDict({"scales": {}, "zero_points": {},
+                                "bit_assignments": _Lazy(lambda labels=bufs.labels: labels.long().cpu().numpy())})
+        # the score spread and the kept-score sums come from K2's second kernel: read on first access
+        propagation_info = _LazyDict({"layer_idx": layer_idx, "propagation_ratio": ratio, "original_length": S,
+                                      "max_selected_length": Sp, "selection_mask": bufs.mask.view(torch.bool),
+                                      "selection_stats": _Lazy(lambda: self.propagator._selection_info(
+                                          scores, res.final_stats(), ratio, S))})
+
+        def std_score():
+            m2 = res.final_stats().score_m2
+            return (m2 / (n - 1)) ** 0.5 if n > 1 else float("nan")
         processing_time = time.time() - start_time
         compression_info = {
             "layer_idx": layer_idx,
@@ -144,8 +167,8 @@ class RealTimePrefillCompressor:
             "compressed_shape": selected_keys.shape,
             "compression_ratio": compression_ratio,
             "memory_savings": 1.0 - compression_ratio,
-            "importance_stats": {"mean_score": st.score_sum / n, "std_score": std,
-                                 "min_score": st.score_min, "max_score": st.score_max},
+            "importance_stats": _LazyDict({"mean_score": st.score_sum / n, "std_score": _Lazy(std_score),
+                                           "min_score": st.score_min, "max_score": st.score_max}),
             "precision_stats": precision_stats,
             "quantization_info": quant_info,
             "propagation_info": propagation_info,

@@ -53,6 +53,7 @@ class OracleShardStages:
             kept_index[b, :idx.size] = idx
             rb = row_bytes[labels[b, idx]]
             row_offset[b, :idx.size] = base + np.concatenate([[0], np.cumsum(rb)[:-1]]).astype(np.int64)
+            row_offset[b, idx.size:] = base + int(rb.sum())  # padding rows: the row's end offset (as K2)
             bufs.packed_bytes.append(int(rb.sum()))
             base += int(rb.sum())
         bufs.kept = kept.astype(np.int64)
@@ -85,7 +86,9 @@ class OracleShardStages:
         labels, ki, ro = g.labels.numpy(), g.kept_index.numpy(), g.row_offset.numpy()
         rg = bufs.ranges.numpy()
         sz = g.scale_zp.numpy()
+        n = int(bufs.kept.max())
         for b in range(bufs.B):
+            sz[b, int(bufs.kept[b]):n] = 0.0  # padding rows: zero scale/zp on every rank, as the HIP kernel
             r_lo, r_hi = int(rg[b, rank, 0]), int(rg[b, rank + 1, 0])
             for r in range(r_lo, r_hi):
                 i = int(ki[b, r])

@@ -1,0 +1,117 @@
+"""GPU: early statistics (rtkv_compress_layer_early).  The device publishes a layer's final counts to
+host memory as soon as K2 has its thresholds; the drop-in path returns on them while K2's tail and K4
+still run.  Every published field must equal the statistics the stream-synchronised read of the
+device block gives after the layer (score_m2 / kept_score_sum excepted: they are read lazily), the
+fallback and the pipeline path must report themselves as not published/incomplete, and the outputs
+must not change."""
+import numpy as np
+import pytest
+import torch
+
+import synth
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module", autouse=True)
+def gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no ROCm device")
+
+
+def _dev(a, dtype):
+    if dtype == "float32":
+        return torch.from_numpy(np.ascontiguousarray(a)).cuda()
+    return torch.from_numpy(np.ascontiguousarray(a).view(np.int16)).cuda().view(getattr(torch, dtype))
+
+
+CASES = [  # dtype, B, S, H, D, ratio, expect: "complete" | "fallback" | "unpublished"
+    ("float32", 1, 16384, 32, 128, 0.6, "complete"),
+    ("float16", 1, 4096, 8, 64, 0.8, "complete"),
+    ("bfloat16", 1, 777, 4, 64, 0.4, "complete"),
+    ("float16", 1, 2000, 4, 32, 0.0001, "fallback"),    # U = 1 bit: nothing fits, the top-10% fallback
+    ("float16", 2, 1024, 4, 32, 0.6, "unpublished"),    # B > 1: the pipeline K2
+    ("float16", 1, 40000, 4, 32, 0.6, "unpublished"),   # S > 32768: the pipeline K2
+]
+
+
+@pytest.mark.parametrize("dtype,B,S,H,D,ratio,expect", CASES)
+def test_early_stats_equal_the_final_block(dtype, B, S, H, D, ratio, expect):
+    import rtkv
+    from rtkv import _lib as L
+    from rtkv.engine import EarlyStatsBuffer
+    F = H * D
+    P = rtkv.prompt_length(S)
+    K, V = synth.kv(31 + S, B, S, F, dtype)
+    W = synth.attention_slice(31 + S, B, H, S, P, dtype)
+    Kd, Vd, Wd = _dev(K, dtype), _dev(V, dtype), _dev(W, dtype)
+    cfg = rtkv.CompressionConfig(alpha=0.8, beta=0.1, gamma=0.1, theta_h=0.4, theta_m=0.25, num_hidden_layers=1,
+                                 layer_weights=[1.0], high_precision_bits=8, medium_precision_bits=4,
+                                 low_precision_bits=2)
+    params = rtkv.params_from_config(cfg, 0, P, ratio, L.EMIT_DEQUANT | L.EMIT_PACKED)
+    ws = rtkv.Workspace("cuda")
+    early = EarlyStatsBuffer()
+    outs = []
+    for use_early in (True, False):
+        bufs = rtkv.LayerBuffers(B, S, F, Kd.dtype, "cuda", (2, 4, 8))
+        res = rtkv.compress_layer(Kd, Vd, Wd, params, bufs, ws, early=early if use_early else None)
+        st = res.stats()
+        if use_early:
+            published = res._early is not None
+            assert published == (expect != "unpublished")
+            if expect == "complete":
+                assert np.isnan(st.score_m2) and np.isnan(st.batch[0]["kept_score_sum"])
+        fin = res.final_stats()
+        outs.append((st, fin, bufs))
+    (st, fin, bufs_e), (_, ref, bufs_r) = outs
+    for x in (st, fin):
+        assert (x.max_kept, x.total_packed_bytes, x.error_flags) == (ref.max_kept, ref.total_packed_bytes,
+                                                                      ref.error_flags)
+        assert (x.score_sum, x.score_min, x.score_max) == (ref.score_sum, ref.score_min, ref.score_max)
+        for a, b in zip(x.batch, ref.batch):
+            for k in ("class_count", "kept", "kept_class", "cost_units", "packed_bytes", "fallback"):
+                assert a[k] == b[k], k
+    assert ref.batch[0]["fallback"] == (expect == "fallback")
+    assert abs(fin.score_m2 - ref.score_m2) <= 1e-12 * max(1.0, abs(ref.score_m2))
+    for a, b in zip(fin.batch, ref.batch):
+        assert abs(a["kept_score_sum"] - b["kept_score_sum"]) <= 1e-12 * max(1.0, abs(b["kept_score_sum"]))
+    n = ref.max_kept
+    assert torch.equal(bufs_e.kept_index[:, :n], bufs_r.kept_index[:, :n])
+    assert torch.equal(bufs_e.k_out[: B * n * F], bufs_r.k_out[: B * n * F])
+    assert torch.equal(bufs_e.packed_v[: ref.total_packed_bytes], bufs_r.packed_v[: ref.total_packed_bytes])
+
+
+def test_drop_in_returns_before_the_layer_finishes_and_stays_correct():
+    """The drop-in over consecutive layers (one early-stats buffer, rising sequence numbers): every
+    layer's K'/V' and lazily read statistics equal a run that synchronises after each layer."""
+    import rtkv
+    S, H, D, dtype = 8192, 16, 128, "float16"
+    F = H * D
+    cfg = rtkv.CompressionConfig(alpha=0.8, beta=0.1, gamma=0.1, theta_h=0.4, theta_m=0.25, num_hidden_layers=6,
+                                 high_precision_bits=8, medium_precision_bits=4, low_precision_bits=2)
+    P = rtkv.prompt_length(S)
+    ins = []
+    for l in range(6):
+        K, V = synth.kv(70 + l, 1, S, F, dtype)
+        W = synth.attention_slice(70 + l, 1, H, S, P, dtype)
+        ins.append((_dev(K, dtype), _dev(V, dtype), _dev(W, dtype)))
+    ids = torch.zeros(1, S, dtype=torch.long, device="cuda")
+    a, b = rtkv.RealTimePrefillCompressor(cfg), rtkv.RealTimePrefillCompressor(cfg)
+    got = [a.compress_layer_kv_cache(K, V, W, ids, l) for l, (K, V, W) in enumerate(ins)]
+    torch.cuda.synchronize()
+    for l, (K, V, W) in enumerate(ins):
+        k2, v2, info = b.compress_layer_kv_cache(K, V, W, ids, l)
+        torch.cuda.synchronize()
+        gk, gv, gi = got[l]
+        assert gk.shape == k2.shape and torch.equal(gk.view(torch.int16), k2.view(torch.int16))
+        assert torch.equal(gv.view(torch.int16), v2.view(torch.int16))
+        for key in ("mean_score", "min_score", "max_score"):
+            assert gi["importance_stats"][key] == info["importance_stats"][key]
+        assert abs(gi["importance_stats"]["std_score"] - info["importance_stats"]["std_score"]) <= \
+            1e-9 * abs(info["importance_stats"]["std_score"])
+        ga = gi["propagation_info"]["selection_stats"]
+        ra = info["propagation_info"]["selection_stats"]
+        assert ga["selected_counts"] == ra["selected_counts"]
+        assert np.allclose(ga["avg_importance"], ra["avg_importance"], rtol=1e-9, atol=0)
+        assert np.array_equal(gi["quantization_info"]["bit_assignments"], info["quantization_info"]["bit_assignments"])
+    assert a.get_overall_compression_stats()["total_layers_processed"] == 6

@@ -46,6 +46,7 @@ CASES = [
     (1, 8, 8, 512, torch.float16, 0.5, True),
     (2, 32, 8, 384, torch.bfloat16, 0.6, False),
     (1, 8, 8, 256, torch.float16, 1.0, False),
+    (2, 16, 4, 640, torch.bfloat16, 0.5, True),   # ragged kept counts across the batch, GQA
 ]
 
 
@@ -76,7 +77,10 @@ def test_compressed_prefill_attention(B, H, Hkv, S, dtype, ratio, pmask):
         ref = ref_attention(Q, K, cv, causal[None, None])
     elif pmask:
         sel = info["propagation_info"]["selection_mask"]
-        kp = torch.stack([sel[b].nonzero().flatten() for b in range(B)])
+        kp = torch.full((B, Sp), S, dtype=torch.long, device="cuda")  # padding rows: never visible
+        for b in range(B):
+            idx = sel[b].nonzero().flatten()
+            kp[b, : idx.numel()] = idx
         mask = kp[:, None, None, :] <= torch.arange(S, device="cuda")[None, None, :, None]
         ref = ref_attention(Q, ck, cv, mask).nan_to_num(0.0)  # queries with no visible kept key: 0
     else:
@@ -84,3 +88,25 @@ def test_compressed_prefill_attention(B, H, Hkv, S, dtype, ratio, pmask):
         ref = ref_attention(Q, ck, cv, causal[:, :Sp][None, None])
     tol = 3e-3 if dtype == torch.float16 else 1.6e-2  # one rounding of the output to the dtype
     torch.testing.assert_close(out.float(), ref, rtol=tol, atol=tol)
+
+
+def test_attention_mask_and_dtype_limits():
+    """The plain causal mask is accepted (same output as no mask); a padded mask and fp32 states are
+    rejected at the boundary instead of being scored as unpadded / run on the wrong kernels."""
+    from rtkv.model_side import CompressedPrefillAttention
+    B, H, S, D = 2, 8, 256, 64
+    g = torch.Generator(device="cuda").manual_seed(5)
+    Q, K, V = (torch.randn(B, H, S, D, device="cuda", generator=g).half() for _ in range(3))
+    layer = CompressedPrefillAttention(compressor(0.5), H, H, D, layer_idx=1)
+    out0, _, _ = layer(Q, K, V)
+    neg = torch.finfo(torch.float16).min
+    causal = torch.zeros(S, S, device="cuda").masked_fill(~torch.ones(S, S, dtype=torch.bool, device="cuda").tril(), neg)
+    mask = causal[None, None].expand(B, 1, S, S).half()
+    out1, _, _ = layer(Q, K, V, attention_mask=mask)
+    assert torch.equal(out0, out1)
+    padded = mask.clone()
+    padded[1, :, :, :7] = neg  # left padding of batch row 1
+    with pytest.raises(ValueError, match="causal"):
+        layer(Q, K, V, attention_mask=padded)
+    with pytest.raises(ValueError, match="float16/bfloat16"):
+        layer(Q.float(), K.float(), V.float())

@@ -96,6 +96,23 @@ def test_aggregation_scores(case):
         assert_matches(case, f"scores_l{layer}", host(out), arrays)
 
 
+@pytest.mark.parametrize("B,H,S", [(1, 32, 16384), (2, 40, 3001), (1, 7, 100)])
+def test_fp32_register_aggregation_matches_lds_path_and_oracle(B, H, S, monkeypatch):
+    """fp32, P = 128: K1's register/shuffle kernel (aggregation_shfl32_kernel) == the LDS kernel
+    (RTKV_K1_LDS) == the oracle, bit for bit; ragged token blocks and head tails included."""
+    import rtkv
+    P = 128
+    W = synth.attention_slice(900 + S, B, H, S, P, "float32")
+    Wd = dev(W, "float32")
+    sc = rtkv.PromptGuidedImportanceScorer(config(COVERAGE, 4))
+    idx = torch.arange(P, device="cuda")
+    reg = host(sc.compute_attention_aggregation(Wd, idx, 0))
+    monkeypatch.setenv("RTKV_K1_LDS", "1")
+    lds = host(sc.compute_attention_aggregation(Wd, idx, 0))
+    assert np.array_equal(reg, lds)
+    assert np.array_equal(reg, orc.attention_aggregation(W, 0, P))
+
+
 @pytest.mark.parametrize("case", by_kind("normalize"), ids=lambda c: c["name"])
 def test_normalize_edges(case):
     import rtkv
@@ -143,6 +160,34 @@ def test_f16_16bit_raises_like_the_reference():
     labels = torch.tensor(s["labels"], device="cuda")
     with pytest.raises(RuntimeError, match="c10::Half without overflow"):
         q.apply_mixed_precision_quantization(dev(K, "float16"), dev(V, "float16"), labels)
+
+
+def test_fast_division_fp32_every_mantissa_pair():
+    """fp32 rows use the same reciprocal + FMA quotient behind a gate that keeps every step normal
+    (quant_impl.h fast_div_ok), so each step commutes with power-of-two scaling and a pair reduces
+    to its mantissas: all 2^46 (X, S) in [1, 2)^2 are compared bitwise with the IEEE division, then
+    scaled and negative pairs spot-check the scaling argument."""
+    import time
+    import rtkv
+    lib = rtkv._lib.lib()
+    counts = torch.zeros(2, dtype=torch.int64, device="cuda")
+    st = rtkv._lib.stream_ptr(counts.device)
+    step = 1 << 17
+    t0 = time.time()
+    for lo in range(0, 1 << 23, step):
+        rtkv._lib.check(lib.rtkv_selfcheck_division_f32(lo, lo + step, 0, 0, 0, counts.data_ptr(), st),
+                        "rtkv_selfcheck_division_f32")
+        if lo % (1 << 21) == 0:
+            torch.cuda.synchronize()
+            print(f"divisors < {lo + step}: {counts.cpu().tolist()} ({time.time() - t0:.1f} s)", flush=True)
+    checked, bad = counts.cpu().tolist()
+    assert (checked, bad) == (1 << 46, 0)
+    for ex, es, neg in ((-40, 30, 0), (50, -45, 1), (-59, -95, 0), (90, 95, 1), (0, 99, 0), (-20, -99, 1)):
+        counts.zero_()
+        rtkv._lib.check(lib.rtkv_selfcheck_division_f32((ex * 7919) % (1 << 23) // 2, (ex * 7919) % (1 << 23) // 2 + 64,
+                                                        ex, es, neg, counts.data_ptr(), st), "selfcheck")
+        checked, bad = counts.cpu().tolist()
+        assert bad == 0 and checked > 0, (ex, es, neg, checked, bad)
 
 
 @pytest.mark.parametrize("dtype", ["float16", "bfloat16"])
@@ -203,8 +248,19 @@ def _division_edge_rows(dtype: str, F: int) -> np.ndarray:
         rows.append(rng.standard_normal(F) * 1e-25)                   # scale < 2^-62
         rows.append(rng.standard_normal(F) * 2.0 ** -120)             # subnormal-adjacent
     else:
-        rows.append(rng.standard_normal(F) * 1e-38)
-        rows.append(rng.standard_normal(F) * 1e37)
+        rows.append(rng.standard_normal(F) * 1e-38)                   # subnormal-adjacent: IEEE path
+        rows.append(rng.standard_normal(F) * 1e37)                    # scale > 2^100: IEEE path
+        t = 1.0 + rng.standard_normal(F)
+        t[::13] = 2.0 ** -61
+        rows.append(t)                                                # |x| < 2^-60 next to O(1) values
+        t = 1.0 + rng.standard_normal(F)
+        t[::13] = 2.0 ** -59
+        rows.append(t)                                                # just inside the gate
+        rows.append(rng.standard_normal(F) * 2.0 ** -90)              # tiny row (|x| < 2^-60): IEEE path
+        rows.append(rng.standard_normal(F) * 2.0 ** 98)               # scale near 2^100
+        t = rng.standard_normal(F)
+        t[::17] = 1e-37
+        rows.append(t)                                                # |x| < 2^-100 s
     return synth.cast(np.stack(rows)[None], dtype)
 
 

@@ -24,12 +24,12 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _inputs(layer, S_total, H, D, dtype):
+def _inputs(layer, B, S_total, H, D, dtype):
     import rtkv
     import synth
     P = rtkv.prompt_length(S_total)
-    K, V = synth.kv(900 + layer, 1, S_total, H * D, dtype)
-    W = synth.attention_slice(900 + layer, 1, H, S_total, P, dtype)
+    K, V = synth.kv(900 + layer, B, S_total, H * D, dtype)
+    W = synth.attention_slice(900 + layer, B, H, S_total, P, dtype)
     return K, V, W, P
 
 
@@ -39,7 +39,7 @@ def _tensor(a, dtype):
     return torch.from_numpy(np.ascontiguousarray(a).view(np.int16)).view(getattr(torch, dtype))
 
 
-def _worker(rank, world, port, S_total, H, D, dtype, layers, q, overlap=True):
+def _worker(rank, world, port, S_total, H, D, dtype, layers, q, overlap=True, B=1):
     try:
         for p in (os.path.join(HERE, ".."), os.path.join(HERE, "..", "realtime-kv-cache-compression_amd"),
                   os.path.join(HERE, "..", "oracle"), os.path.join(HERE, "golden"), HERE):
@@ -60,7 +60,7 @@ def _worker(rank, world, port, S_total, H, D, dtype, layers, q, overlap=True):
         row0 = rank * S_local
         full = {}
         for l in range(layers):
-            K, V, W, P = _inputs(l, S_total, H, D, dtype)
+            K, V, W, P = _inputs(l, B, S_total, H, D, dtype)
             full[l] = (K, V, W, P)
             sl = slice(row0, row0 + S_local)
             comp.enqueue_layer(_tensor(K[:, sl], dtype), _tensor(V[:, sl], dtype), _tensor(W[:, :, sl], dtype), l)
@@ -75,7 +75,7 @@ def _worker(rank, world, port, S_total, H, D, dtype, layers, q, overlap=True):
                                    p.theta_m, (2, 4, 8), prop.get_layer_propagation_ratio(l))
             g = sl_.bufs.g
             n = o["max_kept"]
-            assert sl_.kept() == n
+            assert max(sl_.kept(b) for b in range(B)) == n
             assert np.array_equal(g.kept_index[:, :n].numpy(), o["kept_index"]), "kept_index"
             assert np.array_equal(g.mask.numpy(), o["mask"]), "mask"
             tot = o["packed_k"].size
@@ -83,11 +83,12 @@ def _worker(rank, world, port, S_total, H, D, dtype, layers, q, overlap=True):
             assert np.array_equal(g.packed_v[:tot].numpy(), o["packed_v"]), "packed V codes"
             assert np.array_equal(g.scale_zp[:, :n].numpy(), o["scale_zp"]), "scale/zero-point"
             assert np.array_equal(g.row_offset[:, :n].numpy(), o["row_offset"]), "row offsets"
-            r0, r1 = int(sl_.ranges[0, rank, 0]), int(sl_.ranges[0, rank + 1, 0])
             k_loc, v_loc = sl_.local_kv(rank)
-            assert np.array_equal(storage(k_loc[:, : r1 - r0]), o["k_out"][:, r0:r1]), "local K' rows"
-            assert np.array_equal(storage(v_loc[:, : r1 - r0]), o["v_out"][:, r0:r1]), "local V' rows"
-            assert (r1 - r0) > 0
+            for b in range(B):
+                r0, r1 = int(sl_.ranges[b, rank, 0]), int(sl_.ranges[b, rank + 1, 0])
+                assert np.array_equal(storage(k_loc[b, : r1 - r0]), o["k_out"][b, r0:r1]), "local K' rows"
+                assert np.array_equal(storage(v_loc[b, : r1 - r0]), o["v_out"][b, r0:r1]), "local V' rows"
+                assert (r1 - r0) > 0
         dist.destroy_process_group()
         q.put((rank, "ok"))
     except BaseException as e:  # report to the parent
@@ -95,15 +96,17 @@ def _worker(rank, world, port, S_total, H, D, dtype, layers, q, overlap=True):
         q.put((rank, "".join(traceback.format_exception(type(e), e, e.__traceback__))))
 
 
-@pytest.mark.parametrize("dtype,overlap", [("float16", True), ("float32", True), ("float16", False)])
-def test_sharded_prefill_world2_matches_single_process(dtype, overlap):
-    """overlap: each layer's exchange issued one layer later on its own communicator (default);
-    otherwise all layers exchanged at the end."""
+@pytest.mark.parametrize("dtype,overlap,B", [("float16", True, 1), ("float32", True, 1), ("float16", False, 1),
+                                             ("bfloat16", True, 2), ("float16", False, 2)])
+def test_sharded_prefill_world2_matches_single_process(dtype, overlap, B):
+    """overlap: each layer's exchange issued `lag` (2) layers later on its own communicator (the
+    default); otherwise all layers exchanged at the end.  B = 2: the A all-gather's token-order
+    permute and the per-batch-row byte / scale spans of the exchange."""
     world, S_total, H, D, layers = 2, 1024, 4, 32, 3
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, S_total, H, D, dtype, layers, q, overlap))
+    procs = [ctx.Process(target=_worker, args=(r, world, port, S_total, H, D, dtype, layers, q, overlap, B))
              for r in range(world)]
     for p in procs:
         p.start()
