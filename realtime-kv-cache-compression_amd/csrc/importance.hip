@@ -547,6 +547,8 @@ static int launch_agg_dt(const rtkv_attn_desc& w, int P, float* A, hipStream_t s
     if (aligned && P == 128) {  // register path (Llama prompts: P = 128)
       dim3 grid((unsigned)((w.S + 15) / 16), (unsigned)w.B);
       if (x.nparts) *x.nparts = (int)grid.x;
+      // 16-head load batches: in the pipeline (after K4's write-back) 29.9 us, against 30.9 us for
+      // 4-head batches with the next one in flight (isolated, tools/k1_grid_probe.hip: 28.7 vs 24.9)
       hipLaunchKernelGGL((aggregation_shfl_kernel<DT, 16>), grid, dim3(256), 0, st, W, H, w.S, w.stride_b,
                          w.stride_h, w.stride_s, lim, A, x);
       RTKV_HIP_CHECK(hipGetLastError());
@@ -556,7 +558,8 @@ static int launch_agg_dt(const rtkv_attn_desc& w, int P, float* A, hipStream_t s
     if (aligned && P == 128 && !getenv("RTKV_K1_LDS")) {  // register path; RTKV_K1_LDS: cross-check knob
       dim3 grid((unsigned)((w.S + 7) / 8), (unsigned)w.B);
       if (x.nparts) *x.nparts = (int)grid.x;
-      hipLaunchKernelGGL((aggregation_shfl32_kernel<32>), grid, dim3(256), 0, st, W, H, w.S, w.stride_b,
+      // 4 heads per load batch (tools/k1_grid_probe.hip: 46.5 us vs 56 us for 16-head batches at cfg3)
+      hipLaunchKernelGGL((aggregation_shfl32_kernel<32, 4>), grid, dim3(256), 0, st, W, H, w.S, w.stride_b,
                          w.stride_h, w.stride_s, lim, A, x);
       RTKV_HIP_CHECK(hipGetLastError());
       return RTKV_OK;
