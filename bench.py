@@ -427,6 +427,9 @@ def leg_summary(args, job, ms, kus):
 
 def main():
     args = parse()
+    if args.importance == "qk" and args.dtype == "float32":
+        raise SystemExit("bench.py: --importance qk runs the MFMA kernels, which take float16 or bfloat16 "
+                         "states: add --dtype float16 (or bfloat16)")
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))

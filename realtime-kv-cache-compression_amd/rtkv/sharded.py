@@ -38,7 +38,7 @@ import torch
 import torch.distributed as dist
 
 from . import _lib as L
-from .engine import LayerBuffers, Workspace, attn_desc, kv_desc, params_from_config, prompt_length
+from .engine import LayerBuffers, Workspace, attn_desc, kv_desc, params_from_config, prompt_length, qk_desc
 from .selective_propagation import SelectiveTokenPropagator
 
 
@@ -69,6 +69,14 @@ class HipShardStages:
         L.check(L.lib().rtkv_shard_ranges(bufs.g.kept_index.data_ptr(), L.ptr(bufs.g.row_offset),
                                           bufs.g.stats.data_ptr(), bufs.B, bufs.S_total, bufs.S_local, world,
                                           bufs.ranges.data_ptr(), self._stream()), "rtkv_shard_ranges")
+
+    def aggregate_qk(self, Q, K_prompt, lse, P: int, row0: int, causal: bool, A_out: torch.Tensor):
+        """Fused importance mode on this rank's rows: A from its queries, the (broadcast) prompt keys
+        [B, P, Hkv*D] and its rows' lse; row0 places the causal mask (rtkv_importance_qk_lse)."""
+        L.require_device(Q, K_prompt, lse, A_out)
+        qd = qk_desc(Q, K_prompt, lse, causal=causal, k_layout="bsf", row0=row0)
+        L.check(L.lib().rtkv_importance_qk_lse(ctypes.byref(qd), int(P), A_out.data_ptr(), self._stream()),
+                "rtkv_importance_qk_lse")
 
     def quantize(self, K, V, layout: str, row0: int, rank: int, world: int, params, bufs: "ShardBuffers"):
         L.require_device(K, V)
@@ -155,6 +163,7 @@ class ShardedPrefillCompressor:
         if self.overlap:
             ranks = dist.get_process_group_ranks(self.group) if self.group is not None else list(range(self.world))
             self.xgroup = dist.new_group(ranks=ranks)
+        self._prompt_keys = {}
         self._queued = []   # (layer_idx, host ranges, event) not yet exchanged
         self._issued = []   # ShardLayer whose exchange is in flight
         self._works = []
@@ -191,20 +200,62 @@ class ShardedPrefillCompressor:
                              f">= P={P}]")
         p = params if params is not None else self.params(layer_idx, S_total)
         bufs = self.buffers(layer_idx, B, S_local, F, K.dtype)
+        A_local = self._A_buffers(B, S_local)[0]
+        self.stages.aggregate(W, P, row0, S_total, A_local)
+        return self._select_and_quantize(K, V, layout, layer_idx, p, bufs, L.TORCH_DTYPE_CODE[W.dtype])
+
+    def enqueue_layer_qk(self, K, V, Q, lse, layer_idx: int, layout: str = "bsf", params=None,
+                         causal: bool = True) -> ShardBuffers:
+        """The fused importance mode on a sequence shard: K, V this rank's
+        [B, S_local, F] (layout 'bsf'); Q [B, H, S_local, D] and lse [B, H, S_local] of this rank's rows.
+        The prompt keys are the first P rows of the GLOBAL keys, which rank 0 holds (S_local >= P):
+        they are broadcast once per layer, then every rank computes A for its own rows on MFMA."""
+        if layout != "bsf":
+            raise ValueError("enqueue_layer_qk takes [B, S_local, F] keys and values")
+        B, S_local, F = K.shape
+        S_total = S_local * self.world
+        row0 = self.rank * S_local
+        P = prompt_length(S_total)
+        if S_local < P:
+            raise ValueError(f"the prompt keys (P={P}) must lie on rank 0: S_local={S_local} < P")
+        if Q.shape[0] != B or Q.shape[2] != S_local or tuple(lse.shape) != (B, Q.shape[1], S_local):
+            raise ValueError(f"queries {tuple(Q.shape)} / lse {tuple(lse.shape)} do not match the shard "
+                             f"[B={B}, S_local={S_local}]")
+        p = params if params is not None else self.params(layer_idx, S_total)
+        bufs = self.buffers(layer_idx, B, S_local, F, K.dtype)
+        A_local = self._A_buffers(B, S_local)[0]
+        kp = self._prompt_keys.get((B, P, F, K.dtype))
+        if kp is None:
+            kp = self._prompt_keys[(B, P, F, K.dtype)] = torch.empty(B, P, F, dtype=K.dtype, device=self.device)
+        if self.rank == 0:
+            kp.copy_(K[:, :P])
+        dist.broadcast(kp, src=self._peer_rank(0), group=self.group)
+        self.stages.aggregate_qk(Q, kp, lse, P, row0, causal, A_local)
+        return self._select_and_quantize(K, V, layout, layer_idx, p, bufs, L.F32)
+
+    def _A_buffers(self, B: int, S_local: int):
         key = (B, S_local)
         if key not in self._A:
+            S_total = S_local * self.world
             self._A[key] = (torch.empty(B, S_local, dtype=torch.float32, device=self.device),
                             torch.empty(self.world, B, S_local, dtype=torch.float32, device=self.device),
                             torch.empty(B, S_total, dtype=torch.float32, device=self.device))
-        A_local, A_parts, A = self._A[key]
-        self.stages.aggregate(W, P, row0, S_total, A_local)
+        return self._A[key]
+
+    def _select_and_quantize(self, K, V, layout: str, layer_idx: int, p, bufs: ShardBuffers, a_dtype: int):
+        """Steps 2-5 of a layer once this rank's A is computed: all-gather, global selection, bounds,
+        local quantization, and the (overlapped) exchange bookkeeping."""
+        B, S_local = bufs.B, bufs.S_local
+        S_total = S_local * self.world
+        row0 = self.rank * S_local
+        A_local, A_parts, A = self._A_buffers(B, S_local)
         dist.all_gather_into_tensor(A_parts.view(-1), A_local.view(-1), group=self.group)
         if B == 1:
             A_glob = A_parts.view(1, S_total)  # rank-major = token order
         else:
             A.copy_(A_parts.permute(1, 0, 2).reshape(B, S_total))
             A_glob = A
-        self.stages.finalize(A_glob, L.TORCH_DTYPE_CODE[W.dtype], p, bufs)
+        self.stages.finalize(A_glob, a_dtype, p, bufs)
         self.stages.ranges(bufs, self.world)
         self.stages.quantize(K, V, layout, row0, self.rank, self.world, p, bufs)
         if self.overlap:

@@ -24,8 +24,8 @@ for s in ${STEPS:-smoke pytest bench}; do
     shard1) step shard1 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29512 bench.py --sharded --steps 3 --warmup 1 --legs none --cpu-baseline-seconds 0 ;;
     gpushard) step gpushard 900 python -m pytest tests/test_gpu_shard.py -q -p no:cacheprovider ;;
     qk) step qk 900 python -m pytest tests/test_gpu_qk.py -q -p no:cacheprovider ;;
-    benchqk) step benchqk 900 python bench.py --importance qk --steps 5 --warmup 2 ;;
-    profqk) step rocprofqk 900 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/profqk -o run -- python3 bench.py --importance qk --steps 3 --warmup 1 ;;
+    benchqk) step benchqk 900 python bench.py --importance qk --dtype float16 --steps 5 --warmup 2 ;;
+    profqk) step rocprofqk 900 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/profqk -o run -- python3 bench.py --importance qk --dtype float16 --steps 3 --warmup 1 ;;
     pmcw)   step pmcw 900 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmcw -o write -- python3 bench.py --steps 2 --warmup 1 --legs none --cpu-baseline-seconds 0 ;;
   esac
 done

@@ -143,3 +143,43 @@ def test_no_selection_single_matches_pipeline():
     for name in a:
         assert torch.equal(a[name].view(torch.uint8) if a[name].dtype != torch.uint8 else a[name],
                            b[name].view(torch.uint8) if b[name].dtype != torch.uint8 else b[name]), name
+
+
+@pytest.mark.parametrize("B,S,ratio,monotone", [(2, 3000, 0.5, False), (1, 12000, 0.3, True),
+                                                (3, 777, 0.0002, False), (1, 40000, 0.3, True)])
+def test_pipeline_with_adversarial_caller_inputs(B, S, ratio, monotone):
+    """Regression for the pipeline's digit search (select.hip find_digit: out-of-range LDS index when a
+    histogram held fewer tokens than the quota, fixed in e2ffcc3): caller scores with ±inf, NaN and
+    ties, caller labels outside {0, 1, 2} (treated as LOW), budgets from zero to above S, B > 1 and
+    S > 32768.  The selection must finish and stay self-consistent: ascending unique in-range kept
+    indices that match the mask and the statistics, and the top-10% fallback when nothing fits."""
+    import rtkv
+    rng = np.random.default_rng(S)
+    scores = rng.standard_normal((B, S)).astype(np.float32)
+    scores[:, ::97] = np.inf
+    scores[:, 5::89] = -np.inf
+    scores[:, 13::7] = 0.5  # a tie block
+    if monotone:  # classes monotone in the score
+        labels = np.where(scores >= 0.4, 2, np.where(scores >= 0.25, 1, 0)).astype(np.int64)
+    else:
+        scores[:, 11::83] = np.nan
+        labels = rng.integers(0, 6, (B, S)).astype(np.int64)
+    prop = rtkv.SelectiveTokenPropagator(rtkv.CompressionConfig(num_hidden_layers=4))
+    sd, ld = torch.from_numpy(scores).cuda(), torch.from_numpy(labels).cuda()
+    if S > 16384:  # caller classes go through the exact general path, limited to S <= 16384 (it says so)
+        with pytest.raises(RuntimeError, match="S <= 16384"):
+            prop.select_tokens_with_budget(sd, ld, ratio, 1)
+        return
+    mask, info = prop.select_tokens_with_budget(sd, ld, ratio, 1)
+    K = torch.zeros(B, S, 8, device="cuda")
+    ks, vs, ss, ls, pinfo = prop.apply_token_selection(K, K, sd, ld, 1)
+    torch.cuda.synchronize()
+    m = mask.cpu().numpy()
+    pm = pinfo["selection_mask"].cpu().numpy()
+    for b in range(B):
+        kept = np.nonzero(pm[b])[0]
+        assert kept.size >= 1  # fallback keeps the top max(1, int(0.1 S)) when nothing fits
+        assert kept.size <= pinfo["max_selected_length"]
+        assert np.all(np.diff(kept) > 0) and kept[-1] < S
+    assert m.shape == (B, S) and m.dtype == bool
+    assert ks.shape[1] == pinfo["max_selected_length"]

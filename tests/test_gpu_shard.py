@@ -98,3 +98,66 @@ def test_shards_union_equals_single_gpu(dtype, S_total, world, H, D, ratio):
     assert torch.equal(pk[:tot], ref.packed_k[:tot])
     assert torch.equal(pv[:tot], ref.packed_v[:tot])
     assert torch.equal(sz[:, :n], ref.scale_zp[:, :n])
+
+
+@pytest.mark.parametrize("dtype,S_total,world,H,Hkv,ratio", [
+    ("float16", 4096, 2, 32, 32, 0.6),
+    ("bfloat16", 3072, 3, 16, 4, 0.5),   # GQA
+])
+def test_fused_mode_shards_union_equals_single_gpu(dtype, S_total, world, H, Hkv, ratio):
+    """Fused importance mode on sequence shards (the prompt keys as rank 0 would broadcast them, each
+    rank's A from its own Q rows and lse with row0): the per-rank A concatenates to the single-GPU
+    rtkv_importance_qk_lse A bit for bit (64-row blocks line up), and the union of the ranks' outputs
+    equals the fused single-GPU rtkv_compress_layer_qk output byte for byte."""
+    import rtkv
+    from rtkv import _lib as L
+    from rtkv.sharded import HipShardStages, ShardBuffers
+    D = 128
+    F = Hkv * D
+    P = rtkv.prompt_length(S_total)
+    td = getattr(torch, dtype)
+    g = torch.Generator(device="cuda").manual_seed(S_total)
+    Kd = torch.randn(1, S_total, F, device="cuda", generator=g).to(td)
+    Vd = torch.randn(1, S_total, F, device="cuda", generator=g).to(td)
+    Q = torch.randn(1, H, S_total, D, device="cuda", generator=g).to(td)
+    lse = rtkv.attention_lse(Q, Kd, k_layout="bsf")
+    cfg = rtkv.CompressionConfig(alpha=0.8, beta=0.1, gamma=0.1, theta_h=0.4, theta_m=0.25, num_hidden_layers=1,
+                                 layer_weights=[1.0], high_precision_bits=8, medium_precision_bits=4,
+                                 low_precision_bits=2)
+    params = rtkv.params_from_config(cfg, 0, P, ratio, L.EMIT_DEQUANT | L.EMIT_PACKED)
+    bits = (2, 4, 8)
+    ref = rtkv.LayerBuffers(1, S_total, F, td, "cuda", bits)
+    res = rtkv.compress_layer_qk(Kd, Vd, Q, lse, params, ref, rtkv.Workspace("cuda"))
+    st = res.stats()
+    k_ref, v_ref = res.kv()
+    A_ref = rtkv.importance_qk_lse(Q, Kd, lse, P)
+    S_local = S_total // world
+    stages = HipShardStages("cuda")
+    kp = Kd[:, :P].contiguous()  # what rank 0 broadcasts
+    A = torch.empty(1, S_total, dtype=torch.float32, device="cuda")
+    for j in range(world):
+        sl = slice(j * S_local, (j + 1) * S_local)
+        A_loc = torch.empty(1, S_local, dtype=torch.float32, device="cuda")
+        stages.aggregate_qk(Q[:, :, sl].contiguous(), kp, lse[:, :, sl].contiguous(), P, j * S_local, True, A_loc)
+        A[:, sl] = A_loc
+    assert torch.equal(A, A_ref)
+    bufs = [ShardBuffers(1, S_local, world, F, td, "cuda", bits) for _ in range(world)]
+    for j in range(world):
+        stages.finalize(A, L.F32, params, bufs[j])
+        stages.ranges(bufs[j], world)
+        sl = slice(j * S_local, (j + 1) * S_local)
+        stages.quantize(Kd[:, sl].contiguous(), Vd[:, sl].contiguous(), "bsf", j * S_local, j, world, params, bufs[j])
+    torch.cuda.synchronize()
+    n, tot = st.max_kept, st.total_packed_bytes
+    rg = bufs[0].ranges.cpu()
+    assert int(rg[0, -1, 0]) == n and int(rg[0, -1, 1]) == tot
+    pk = torch.zeros_like(ref.packed_k)
+    for j in range(world):
+        g_ = bufs[j].g
+        assert torch.equal(g_.kept_index[:, :n], ref.kept_index[:, :n])
+        r0, r1 = int(rg[0, j, 0]), int(rg[0, j + 1, 0])
+        b0, b1 = int(rg[0, j, 1]), int(rg[0, j + 1, 1])
+        pk[b0:b1] = g_.packed_k[b0:b1]
+        assert torch.equal(bufs[j].k_local[:, : r1 - r0], k_ref[:, r0:r1])
+        assert torch.equal(bufs[j].v_local[:, : r1 - r0], v_ref[:, r0:r1])
+    assert torch.equal(pk[:tot], ref.packed_k[:tot])

@@ -33,13 +33,30 @@ def _inputs(layer, B, S_total, H, D, dtype):
     return K, V, W, P
 
 
+def _qk_inputs(layer, B, S_total, H, D, K, dtype):
+    """Fused-mode inputs for the keys K [B,S,H*D]: Q [B,H,S,D] (float32 values of the dtype) and the
+    exact causal row lse of softmax(Q·Kᵀ/√d) over all S keys (float64, rounded to fp32)."""
+    import synth
+    Q = synth.to_f32(synth.cast(synth.normal(500 + layer, (B, H, S_total, D), 4), dtype), dtype)
+    Kf = synth.to_f32(K, dtype).astype(np.float64).reshape(B, S_total, H, D)
+    lse = np.zeros((B, H, S_total), np.float32)
+    causal = np.arange(S_total)[None, :] <= np.arange(S_total)[:, None]
+    for b in range(B):
+        for h in range(H):
+            x = Q[b, h].astype(np.float64) @ Kf[b, :, h].T / np.sqrt(D)
+            x = np.where(causal, x, -np.inf)
+            m = x.max(-1, keepdims=True)
+            lse[b, h] = (m[:, 0] + np.log(np.exp(x - m).sum(-1))).astype(np.float32)
+    return Q, lse
+
+
 def _tensor(a, dtype):
     if dtype == "float32":
         return torch.from_numpy(np.ascontiguousarray(a))
     return torch.from_numpy(np.ascontiguousarray(a).view(np.int16)).view(getattr(torch, dtype))
 
 
-def _worker(rank, world, port, S_total, H, D, dtype, layers, q, overlap=True, B=1):
+def _worker(rank, world, port, S_total, H, D, dtype, layers, q, overlap=True, B=1, mode="w"):
     try:
         for p in (os.path.join(HERE, ".."), os.path.join(HERE, "..", "realtime-kv-cache-compression_amd"),
                   os.path.join(HERE, "..", "oracle"), os.path.join(HERE, "golden"), HERE):
@@ -49,7 +66,8 @@ def _worker(rank, world, port, S_total, H, D, dtype, layers, q, overlap=True, B=
         import rtkv
         import rtkv_oracle as orc
         from rtkv.sharded import ShardedPrefillCompressor
-        from shard_oracle_stages import OracleShardStages, storage
+        import synth
+        from shard_oracle_stages import OracleShardStages, qk_mass, single_process_from_A, storage
 
         cfg = rtkv.CompressionConfig(alpha=0.8, beta=0.1, gamma=0.1, theta_h=0.4, theta_m=0.25,
                                      high_precision_bits=8, medium_precision_bits=4, low_precision_bits=2,
@@ -61,18 +79,30 @@ def _worker(rank, world, port, S_total, H, D, dtype, layers, q, overlap=True, B=
         full = {}
         for l in range(layers):
             K, V, W, P = _inputs(l, B, S_total, H, D, dtype)
-            full[l] = (K, V, W, P)
             sl = slice(row0, row0 + S_local)
-            comp.enqueue_layer(_tensor(K[:, sl], dtype), _tensor(V[:, sl], dtype), _tensor(W[:, :, sl], dtype), l)
+            if mode == "qk":  # fused importance mode: Q and the row lse instead of W
+                Q, lse = _qk_inputs(l, B, S_total, H, D, K, dtype)
+                A = qk_mass(Q, synth.to_f32(K, dtype), lse, P, 0)
+                W = None
+                comp.enqueue_layer_qk(_tensor(K[:, sl], dtype), _tensor(V[:, sl], dtype),
+                                      torch.from_numpy(Q[:, :, sl].copy()).to(getattr(torch, dtype)),
+                                      torch.from_numpy(lse[:, :, sl].copy()), l)
+            else:
+                A = None
+                comp.enqueue_layer(_tensor(K[:, sl], dtype), _tensor(V[:, sl], dtype), _tensor(W[:, :, sl], dtype), l)
+            full[l] = (K, V, W, P, A)
         out = comp.exchange()
         code = {"float32": 0, "float16": 1, "bfloat16": 2}[dtype]
         prop = rtkv.SelectiveTokenPropagator(cfg)
         for sl_ in out:
             l = sl_.layer_idx
-            K, V, W, P = full[l]
+            K, V, W, P, A = full[l]
             p = comp.params(l, S_total)
-            o = orc.compress_layer(K, V, code, W, code, P, p.alpha, p.beta, p.gamma, p.layer_weight, p.theta_h,
-                                   p.theta_m, (2, 4, 8), prop.get_layer_propagation_ratio(l))
+            if mode == "qk":
+                o = single_process_from_A(K, V, code, A, p, (2, 4, 8), prop.get_layer_propagation_ratio(l))
+            else:
+                o = orc.compress_layer(K, V, code, W, code, P, p.alpha, p.beta, p.gamma, p.layer_weight, p.theta_h,
+                                       p.theta_m, (2, 4, 8), prop.get_layer_propagation_ratio(l))
             g = sl_.bufs.g
             n = o["max_kept"]
             assert max(sl_.kept(b) for b in range(B)) == n
@@ -96,17 +126,20 @@ def _worker(rank, world, port, S_total, H, D, dtype, layers, q, overlap=True, B=
         q.put((rank, "".join(traceback.format_exception(type(e), e, e.__traceback__))))
 
 
-@pytest.mark.parametrize("dtype,overlap,B", [("float16", True, 1), ("float32", True, 1), ("float16", False, 1),
-                                             ("bfloat16", True, 2), ("float16", False, 2)])
-def test_sharded_prefill_world2_matches_single_process(dtype, overlap, B):
+@pytest.mark.parametrize("dtype,overlap,B,mode", [("float16", True, 1, "w"), ("float32", True, 1, "w"),
+                                                  ("float16", False, 1, "w"), ("bfloat16", True, 2, "w"),
+                                                  ("float16", False, 2, "w"), ("float16", True, 1, "qk"),
+                                                  ("bfloat16", False, 2, "qk")])
+def test_sharded_prefill_world2_matches_single_process(dtype, overlap, B, mode):
     """overlap: each layer's exchange issued `lag` (2) layers later on its own communicator (the
     default); otherwise all layers exchanged at the end.  B = 2: the A all-gather's token-order
-    permute and the per-batch-row byte / scale spans of the exchange."""
+    permute and the per-batch-row byte / scale spans of the exchange.  mode 'qk': the fused importance
+    mode (enqueue_layer_qk: prompt keys broadcast from rank 0, A from each rank's Q rows and lse)."""
     world, S_total, H, D, layers = 2, 1024, 4, 32, 3
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, S_total, H, D, dtype, layers, q, overlap, B))
+    procs = [ctx.Process(target=_worker, args=(r, world, port, S_total, H, D, dtype, layers, q, overlap, B, mode))
              for r in range(world)]
     for p in procs:
         p.start()

@@ -116,6 +116,12 @@ int main() {
   run("rows 16KB, packed only, 16-B code stores", (double)rows * ROW_U4 * 16 * (1.0 + 1.0 / 8), [&](int i) {
     hipLaunchKernelGGL((mix<ROW_U4, 4, true, false, 16>), dim3((rows * 4 + 3) / 4), dim3(256), 0, 0, Sx[i], idx, D[i], P[i], rows);
   });
+  run("rows 16KB, packed only, plain 8-B code stores", (double)rows * ROW_U4 * 16 * (1.0 + 1.0 / 8), [&](int i) {
+    hipLaunchKernelGGL((mix<ROW_U4, 4, false, false, 8>), dim3((rows * 4 + 3) / 4), dim3(256), 0, 0, Sx[i], idx, D[i], P[i], rows);
+  });
+  run("rows 16KB, packed only, 1 wave/row", (double)rows * ROW_U4 * 16 * (1.0 + 1.0 / 8), [&](int i) {
+    hipLaunchKernelGGL((mix<ROW_U4, 1, true, false, 8>), dim3((rows + 3) / 4), dim3(256), 0, 0, Sx[i], idx, D[i], P[i], rows);
+  });
   run("rows 16KB gathered, read only, 4 waves/row", (double)rows * ROW_U4 * 16, [&](int i) {
     hipLaunchKernelGGL((mix<ROW_U4, 4, true, false, 1>), dim3((rows * 4 + 3) / 4), dim3(256), 0, 0, Sx[i], idx, D[i], P[i], rows);
   });
