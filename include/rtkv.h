@@ -351,6 +351,15 @@ int rtkv_shard_ranges(const int32_t* kept_index_dev, const int64_t* row_offset_d
  * (token_importance.py:21-47) fed by the materialised softmax of modified_llama.py:88-94.
  * ---------------------------------------------------------------------------------------------- */
 int rtkv_importance_qk_lse(const rtkv_qk_desc* q, int32_t prompt_len, float* A_dev, void* stream);
+/* The same with a [B][H][S] fp32 scratch (rtkv_qk_scratch_size bytes): the head-major kernel (the
+ * prompt keys of one head staged once per workgroup, per-head row sums reduced in head order) when
+ * S % 4 == 0, D = 128 and P > 64 — the kernel rtkv_compress_layer_qk uses when its workspace has
+ * rtkv_workspace_size_qk(B, H, S) bytes.  Same tolerance as above; the two kernels differ in the
+ * summation order only. */
+size_t rtkv_qk_scratch_size(int64_t B, int64_t H, int64_t S);
+size_t rtkv_workspace_size_qk(int64_t B, int64_t H, int64_t S);
+int rtkv_importance_qk_lse_ws(const rtkv_qk_desc* q, int32_t prompt_len, float* A_dev, void* scratch_dev,
+                              size_t scratch_bytes, void* stream);
 
 /* Row log-sum-exp of the prefill attention: lse[b,h,i] = log Σ_j exp(q_i·k_j·scale)
  * over j ≤ i (causal) or all j < S, without materialising the [B,H,S,S] softmax of

@@ -250,7 +250,11 @@ static int compress_layer_impl(const rtkv_kv_desc* kv, const rtkv_attn_desc* w, 
   } else {
     x.S_total = kv->S;
     x.row0 = 0;
-    rc = launch_qk_importance(*qk, p->prompt_len, ws.A, st, x, &nparts);
+    // the head-major K1' uses the workspace past the base layout when the caller sized it with
+    // rtkv_workspace_size_qk
+    const size_t base = ws_bytes(kv->B, kv->S);
+    float* scratch = workspace_bytes > base ? reinterpret_cast<float*>(static_cast<char*>(workspace_dev) + base) : nullptr;
+    rc = launch_qk_importance(*qk, p->prompt_len, ws.A, st, x, &nparts, scratch, scratch ? workspace_bytes - base : 0);
   }
   if (rc) return rc;
   if ((rc = mark(1))) return rc;
@@ -356,6 +360,22 @@ int rtkv_importance_qk_lse(const rtkv_qk_desc* q, int32_t prompt_len, float* A_d
   RTKV_REQUIRE(q != nullptr, "null query descriptor");
   AggExtras x;
   return launch_qk_importance(*q, prompt_len, A_dev, (hipStream_t)stream, x, nullptr);
+}
+
+size_t rtkv_qk_scratch_size(int64_t B, int64_t H, int64_t S) { return qk_scratch_bytes(B, H, S); }
+
+size_t rtkv_workspace_size_qk(int64_t B, int64_t H, int64_t S) {
+  return ws_bytes(B, S) + align_up(qk_scratch_bytes(B, H, S), 256);
+}
+
+int rtkv_importance_qk_lse_ws(const rtkv_qk_desc* q, int32_t prompt_len, float* A_dev, void* scratch_dev,
+                              size_t scratch_bytes, void* stream) {
+  RTKV_REQUIRE(q != nullptr, "null query descriptor");
+  AggExtras x;
+  x.S_total = q->row0 + q->S;  // only the β·pos epilogue would read it (t2 is null here)
+  x.row0 = q->row0;
+  return launch_qk_importance(*q, prompt_len, A_dev, (hipStream_t)stream, x, nullptr,
+                              static_cast<float*>(scratch_dev), scratch_bytes);
 }
 
 int rtkv_attention_lse(const rtkv_qk_desc* q, float* lse_dev, void* stream) {

@@ -194,7 +194,10 @@ __device__ __forceinline__ void zero_regions(const AggExtras& x) {
   }
 }
 int launch_aggregation(const rtkv_attn_desc& w, int P, float* A, hipStream_t st, const AggExtras& x = AggExtras());
-int launch_qk_importance(const rtkv_qk_desc& q, int P, float* A, hipStream_t st, const AggExtras& x, int* nparts);
+// scratch: [B][H][S] fp32 (qk_scratch_bytes) for the head-major kernel, or null (head-walking kernel)
+size_t qk_scratch_bytes(int64_t B, int64_t H, int64_t S);
+int launch_qk_importance(const rtkv_qk_desc& q, int P, float* A, hipStream_t st, const AggExtras& x, int* nparts,
+                         float* scratch = nullptr, size_t scratch_bytes = 0);
 int launch_attention_lse(const rtkv_qk_desc& q, float* lse, hipStream_t st);
 int launch_position_bias(int64_t S, float* pos, hipStream_t st);
 int launch_minmax_normalize(const void* x, int dt, int64_t B, int64_t S, void* out, hipStream_t st);

@@ -18,6 +18,8 @@
 // (cdna_hip_programming.md §3): lane l holds A[row l&15][k 8(l>>4)..+7] and
 // B[k 8(l>>4)..+7][col l&15]; the accumulator holds col l&15, rows 4(l>>4) + reg.
 // Waves own disjoint rows, so the only reduction is over the 16 columns held across lanes.
+#include <cstdlib>
+
 #include "common.h"
 
 namespace rtkv {
@@ -219,6 +221,177 @@ __global__ __launch_bounds__(256) void qk_importance_kernel(QKArgs g) {
   }
 }
 
+// Head-major variant (S % 4 == 0, with a [B][H][S] fp32 scratch): a workgroup owns ONE head and a
+// block of 4·RPW query rows.  The head's P×D prompt keys are staged in LDS once (32 KiB) and stay
+// there; each wave then streams its RPW rows in 16-row tiles, the query fragments and LSE going
+// straight to registers in the MFMA A-fragment layout (the next tile in flight while one computes),
+// no barrier after the key tile, and writes the 16 rows' per-head sums to the scratch.  qk_head_reduce_kernel sums
+// the H heads of each row in head order (deterministic) and does K1's epilogue (β·pos, per-block
+// min/max, zeroing).  Against the head-walking kernel above: the keys are staged once per
+// workgroup instead of once per head, and 8-16 waves per CU keep queries in flight.
+template <int DT, int NT, int KS>
+__global__ __launch_bounds__(256) void qk_head_kernel(QKArgs g, float* __restrict__ part, int rpw) {
+  using FT = typename Frag<DT>::T;
+  using S_ = typename Dt<DT>::S;
+  constexpr int D = 32 * KS;
+  constexpr int PT = 16 * NT;
+  constexpr int RB = 2 * D;
+  constexpr int CH = RB / 16;
+  constexpr int RPI = 1024 / RB;
+  constexpr int KEY_BYTES = PT * RB;
+  constexpr int KI = KEY_BYTES / 1024 / 4;
+  extern __shared__ __attribute__((aligned(1024))) uint8_t lds[];  // KEY_BYTES
+  const rtkv_qk_desc& q = g.q;
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int c16 = lane & 15, kg = lane >> 4;
+  const int h = blockIdx.y, b = blockIdx.z;
+  const int S = (int)q.S, grp = (int)(q.H / q.Hkv), P = g.P;
+  const int wrow = (blockIdx.x * 4 + wave) * rpw;  // this wave's first row
+  const float l2e = 1.4426950408889634f;
+  const float sc = q.scale * l2e;
+  const S_* Qh = static_cast<const S_*>(q.q_dev) + b * q.q_stride_b + (int64_t)h * q.q_stride_h;
+  const float* Lh = q.lse_dev + b * q.lse_stride_b + (int64_t)h * q.lse_stride_h;
+  float* Ph = part + ((int64_t)b * q.H + h) * S;
+  {  // the head's prompt keys into LDS, swizzled as in qk_importance_kernel
+    const S_* kh = static_cast<const S_*>(q.k_dev) + b * q.k_stride_b + (int64_t)(h / grp) * q.k_stride_h;
+    const int lrow = lane / CH, lpc = lane % CH;
+#pragma unroll
+    for (int k = 0; k < KI; ++k) {
+      const int r = (wave * KI + k) * RPI + lrow;
+      const int c = lpc ^ (r & (CH - 1));
+      const int pr = r < P ? r : P - 1;
+      glds16(kh + (int64_t)pr * q.k_stride_s + c * 8, lds + (wave * KI + k) * 1024);
+    }
+  }
+  const int ntile = rpw / 16;
+  auto load_tile = [&](int k, FT (&a)[KS], f32x4& l) {  // tile k of this wave (clamped rows)
+    const int r0 = wrow + 16 * (k < ntile ? k : ntile - 1);
+    const int qr = r0 + c16 < S ? r0 + c16 : S - 1;
+    const S_* qp = Qh + (int64_t)qr * q.q_stride_s;
+#pragma unroll
+    for (int s_ = 0; s_ < KS; ++s_) a[s_] = *reinterpret_cast<const FT*>(qp + (4 * s_ + kg) * 8);
+    const int lr = r0 + 4 * kg < S ? r0 + 4 * kg : S - 4;
+    l = *reinterpret_cast<const f32x4*>(Lh + lr);
+  };
+  FT qa[KS], qn[KS];
+  f32x4 ql, qln;
+  load_tile(0, qa, ql);
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(KS + 1) : "memory");  // this wave's key pieces landed
+  __syncthreads();                                               // ... and every wave's
+  for (int k = 0; k < ntile; ++k) {
+    load_tile(k + 1, qn, qln);  // the next tile in flight while this one computes (clamped at the end)
+    const int r0 = wrow + 16 * k;
+    const int crow0 = r0 + 4 * kg;
+    // the key fragments are re-read from LDS for every tile: kept in registers (the compiler would
+    // hoist them) they cost 128 VGPRs, and occupancy is what hides the query loads here
+    uint32_t kofs = 0;  // opaque zero offset: the LDS reads stay in the loop (and ds_read, not flat)
+    asm volatile("" : "+v"(kofs));
+    const uint8_t* kt = lds + kofs;
+    f32x4 acc[NT];
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+      const int kr = 16 * t + c16;
+      const uint8_t* krow = kt + kr * RB;
+#pragma unroll
+      for (int s_ = 0; s_ < KS; ++s_) {
+        const FT bf = *reinterpret_cast<const FT*>(krow + (((4 * s_ + kg) ^ (kr & (CH - 1))) * 16));
+        acc[t] = Frag<DT>::mfma(qa[s_], bf, acc[t]);
+      }
+    }
+    const int lr = crow0 < S ? crow0 : S - 4;
+    float nl2[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int e = crow0 + r - lr;  // 0..3 except in the clamped tail
+      const float lv = e == 0 ? ql[0] : (e == 1 ? ql[1] : (e == 2 ? ql[2] : ql[3]));
+      nl2[r] = -lv * l2e;
+    }
+    const bool masked = (q.causal && q.row0 + r0 < PT - 1) || r0 + 16 > S || P < PT;
+    float v[4] = {0.f, 0.f, 0.f, 0.f};
+    if (!masked) {
+#pragma unroll
+      for (int t = 0; t < NT; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] += __builtin_amdgcn_exp2f(__builtin_fmaf(acc[t][r], sc, nl2[r]));
+    } else {
+#pragma unroll
+      for (int t = 0; t < NT; ++t) {
+        const int p = 16 * t + c16;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int i = crow0 + r;
+          const bool ok = p < P && i < S && (!q.causal || (int64_t)p <= q.row0 + i);
+          const float w = __builtin_amdgcn_exp2f(__builtin_fmaf(acc[t][r], sc, nl2[r]));
+          v[r] += ok ? w : 0.f;
+        }
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+      for (int o = 1; o < 16; o <<= 1) v[r] += __shfl_xor(v[r], o, 64);
+    if (c16 == 0 && crow0 < S) *reinterpret_cast<f32x4*>(Ph + crow0) = f32x4{v[0], v[1], v[2], v[3]};
+#pragma unroll
+    for (int s_ = 0; s_ < KS; ++s_) qa[s_] = qn[s_];
+    ql = qln;
+  }
+}
+
+// A[b,i] = (Σ_h part[b,h,i]) / H in head order, plus K1's epilogue (β·pos, block min/max, zeroing).
+__global__ __launch_bounds__(256) void qk_head_reduce_kernel(const float* __restrict__ part, int64_t H, int64_t S,
+                                                             float* __restrict__ A, AggExtras ex) {
+  __shared__ float red[2][4];
+  zero_regions(ex);
+  const int b = blockIdx.y;
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  float mn = INFINITY, mx = -INFINITY;
+  if (i < S) {
+    const float* pp = part + (int64_t)b * H * S + i;
+    float s = 0.f;
+    for (int64_t h = 0; h < H; ++h) s += pp[h * S];
+    const float Ai = s / (float)H;
+    A[(int64_t)b * S + i] = Ai;
+    if (ex.t2 && b == 0) {
+      const int64_t n = ex.row0 + i + 1;
+      ex.t2[i] = ex.beta * ((ex.S_total > 1) ? torch_logf((uint32_t)n) / ex.logS : 0.f);
+    }
+    mn = mx = Ai;
+  }
+  if (ex.part) {
+    mn = wave_min(mn);
+    mx = wave_max(mx);
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    if (lane == 0) { red[0][wave] = mn; red[1][wave] = mx; }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      ex.part[((int64_t)b * gridDim.x + blockIdx.x) * 2] = fminf(fminf(red[0][0], red[0][1]), fminf(red[0][2], red[0][3]));
+      ex.part[((int64_t)b * gridDim.x + blockIdx.x) * 2 + 1] = fmaxf(fmaxf(red[1][0], red[1][1]), fmaxf(red[1][2], red[1][3]));
+    }
+  }
+}
+
+template <int DT, int NT, int KS>
+static int launch_qk_head(const QKArgs& a, float* part, hipStream_t st, int* nparts) {
+  constexpr size_t lds = (size_t)(16 * NT) * (64 * KS);
+  const int64_t S = a.q.S;
+  // rows per wave: 16-row tiles, enough workgroups to fill the chip (>= 1024 with the heads)
+  static const int target = [] {  // RTKV_QK_WGS: measurement knob (workgroups to aim for)
+    const char* e = getenv("RTKV_QK_WGS");
+    return e ? atoi(e) : 2048;
+  }();
+  int rpw = 256;
+  while (rpw > 16 && (S + 4 * rpw - 1) / (4 * rpw) * a.q.H * a.q.B < target) rpw /= 2;
+  const dim3 grid((unsigned)((S + 4 * rpw - 1) / (4 * rpw)), (unsigned)a.q.H, (unsigned)a.q.B);
+  hipLaunchKernelGGL((qk_head_kernel<DT, NT, KS>), grid, dim3(256), lds, st, a, part, rpw);
+  RTKV_HIP_CHECK(hipGetLastError());
+  const dim3 rgrid((unsigned)((S + 255) / 256), (unsigned)a.q.B);
+  if (nparts) *nparts = (int)rgrid.x;
+  hipLaunchKernelGGL(qk_head_reduce_kernel, rgrid, dim3(256), 0, st, part, a.q.H, S, a.A, a.ex);
+  RTKV_HIP_CHECK(hipGetLastError());
+  return RTKV_OK;
+}
+
 template <int DT, int NT, int KS>
 static int launch_qk_tpl(const QKArgs& a, dim3 grid, hipStream_t st) {
   constexpr size_t lds = (size_t)kQKStages * ((size_t)(16 * NT) * (64 * KS) + (size_t)kQKRows * (64 * KS) + kQKRows * 4);
@@ -247,7 +420,10 @@ static int launch_qk_dt(const QKArgs& a, dim3 grid, hipStream_t st) {
   RTKV_REQUIRE(false, "importance_qk_lse: unsupported head_dim");
 }
 
-int launch_qk_importance(const rtkv_qk_desc& q, int P, float* A, hipStream_t st, const AggExtras& x, int* nparts) {
+size_t qk_scratch_bytes(int64_t B, int64_t H, int64_t S) { return (size_t)(B * H * S) * sizeof(float); }
+
+int launch_qk_importance(const rtkv_qk_desc& q, int P, float* A, hipStream_t st, const AggExtras& x, int* nparts,
+                         float* scratch, size_t scratch_bytes) {
   RTKV_REQUIRE(q.q_dev && q.k_dev && q.lse_dev && A, "importance_qk_lse: null pointer");
   RTKV_REQUIRE(q.B >= 1 && q.B <= 65535 && q.H >= 1 && q.S >= 4 && q.Hkv >= 1, "importance_qk_lse: bad shape (S >= 4)");
   RTKV_REQUIRE(q.H % q.Hkv == 0, "importance_qk_lse: H must be a multiple of Hkv");
@@ -266,6 +442,14 @@ int launch_qk_importance(const rtkv_qk_desc& q, int P, float* A, hipStream_t st,
   a.P = P;
   a.A = A;
   a.ex = x;
+  // head-major kernel when a scratch is given (the C ABI entries that take a workspace); RTKV_QK_RING
+  // forces the head-walking kernel (cross-check knob)
+  static const bool ring = getenv("RTKV_QK_RING") != nullptr;
+  if (scratch && scratch_bytes >= qk_scratch_bytes(q.B, q.H, q.S) && q.S % 4 == 0 && !ring &&
+      q.H <= 65535 && P > 64 && q.D == 128) {
+    if (q.dtype == RTKV_F16) return launch_qk_head<RTKV_F16, 8, 4>(a, scratch, st, nparts);
+    return launch_qk_head<RTKV_BF16, 8, 4>(a, scratch, st, nparts);
+  }
   const dim3 grid((unsigned)((q.S + kQKRows - 1) / kQKRows), (unsigned)q.B);
   if (nparts) *nparts = (int)grid.x;
   if (q.dtype == RTKV_F16) return launch_qk_dt<RTKV_F16>(a, grid, st);

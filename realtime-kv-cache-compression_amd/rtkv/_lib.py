@@ -108,6 +108,9 @@ _SIGS = {
     "rtkv_quantize_rows_shard": ([c_p, c_i64, c_i64, c_i32, c_i32, c_p, c_p, c_p, c_p, c_p, c_p], c_i32),
     "rtkv_shard_ranges": ([c_p, c_p, c_p, c_i64, c_i64, c_i64, c_i32, c_p, c_p], c_i32),
     "rtkv_importance_qk_lse": ([c_p, c_i32, c_p, c_p], c_i32),
+    "rtkv_qk_scratch_size": ([c_i64, c_i64, c_i64], c_sz),
+    "rtkv_workspace_size_qk": ([c_i64, c_i64, c_i64], c_sz),
+    "rtkv_importance_qk_lse_ws": ([c_p, c_i32, c_p, c_p, c_sz, c_p], c_i32),
     "rtkv_attention_lse": ([c_p, c_p, c_p], c_i32),
     "rtkv_compress_layer_qk": ([c_p, c_p, c_p, c_p, c_p, c_sz, c_p], c_i32),
     "rtkv_compress_layer_qk_events": ([c_p, c_p, c_p, c_p, c_p, c_sz, c_p, c_p], c_i32),

@@ -184,8 +184,9 @@ class Workspace:
         self.device = torch.device(device)
         self.buf = torch.empty(0, dtype=torch.uint8, device=self.device)
 
-    def get(self, B: int, S: int) -> torch.Tensor:
-        need = int(L.lib().rtkv_workspace_size(B, S))
+    def get(self, B: int, S: int, H: Optional[int] = None) -> torch.Tensor:
+        """H: query heads of the fused importance mode (room for the head-major K1' scratch)."""
+        need = int(L.lib().rtkv_workspace_size(B, S) if H is None else L.lib().rtkv_workspace_size_qk(B, H, S))
         if self.buf.numel() < need:
             self.buf = torch.empty(need, dtype=torch.uint8, device=self.device)
         return self.buf
@@ -308,7 +309,7 @@ def compress_layer_qk(K, V, Q, lse, params: L.LayerParams, bufs: LayerBuffers, w
     qd = qk_desc(Q, K, lse, scale=scale, causal=causal, k_layout=layout)
     if qd.B != kd.B or qd.S != kd.S:
         raise ValueError(f"queries {tuple(Q.shape)} do not match key states {tuple(K.shape)}")
-    ws = workspace.get(kd.B, kd.S)
+    ws = workspace.get(kd.B, kd.S, H=qd.H)
     out = bufs.out_struct()
     out.o_stride_h = kd.D
     st = L.stream_ptr(K.device) if stream is None else stream
@@ -331,8 +332,9 @@ def importance_qk_lse(Q, K, lse, prompt_len: int, causal: bool = True, scale: Op
     L.require_device(Q, K, lse)
     qd = qk_desc(Q, K, lse, scale=scale, causal=causal, k_layout=k_layout)
     A = torch.empty(qd.B, qd.S, dtype=torch.float32, device=Q.device)
-    L.check(L.lib().rtkv_importance_qk_lse(ctypes.byref(qd), int(prompt_len), A.data_ptr(), L.stream_ptr(Q.device)),
-            "rtkv_importance_qk_lse")
+    scratch = torch.empty(int(L.lib().rtkv_qk_scratch_size(qd.B, qd.H, qd.S)), dtype=torch.uint8, device=Q.device)
+    L.check(L.lib().rtkv_importance_qk_lse_ws(ctypes.byref(qd), int(prompt_len), A.data_ptr(), scratch.data_ptr(),
+                                              scratch.numel(), L.stream_ptr(Q.device)), "rtkv_importance_qk_lse_ws")
     return A
 
 

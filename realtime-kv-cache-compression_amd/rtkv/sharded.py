@@ -48,6 +48,7 @@ class HipShardStages:
     def __init__(self, device):
         self.device = torch.device(device)
         self.ws = Workspace(self.device)
+        self._qk_scratch = None
 
     def _stream(self):
         return L.stream_ptr(self.device)
@@ -75,8 +76,11 @@ class HipShardStages:
         [B, P, Hkv*D] and its rows' lse; row0 places the causal mask (rtkv_importance_qk_lse)."""
         L.require_device(Q, K_prompt, lse, A_out)
         qd = qk_desc(Q, K_prompt, lse, causal=causal, k_layout="bsf", row0=row0)
-        L.check(L.lib().rtkv_importance_qk_lse(ctypes.byref(qd), int(P), A_out.data_ptr(), self._stream()),
-                "rtkv_importance_qk_lse")
+        n = int(L.lib().rtkv_qk_scratch_size(qd.B, qd.H, qd.S))
+        if self._qk_scratch is None or self._qk_scratch.numel() < n:
+            self._qk_scratch = torch.empty(n, dtype=torch.uint8, device=self.device)
+        L.check(L.lib().rtkv_importance_qk_lse_ws(ctypes.byref(qd), int(P), A_out.data_ptr(), self._qk_scratch.data_ptr(),
+                                                  self._qk_scratch.numel(), self._stream()), "rtkv_importance_qk_lse_ws")
 
     def quantize(self, K, V, layout: str, row0: int, rank: int, world: int, params, bufs: "ShardBuffers"):
         L.require_device(K, V)
