@@ -1,7 +1,7 @@
 // select_fast.hip — K2 for one batch row (B = 1, S <= 32768: every reference configuration that
-// fits one GPU) in two launches instead of select.hip's four, with every per-token pass spread over
+// fits one GPU) in ONE launch instead of select.hip's four, with every per-token pass spread over
 // the whole grid.  Same outputs, bit for bit (scores, classes, mask, kept_index, row_offset,
-// statistics).
+// row_label, counts; the double statistics to 1e-12 relative).
 //
 // Reference (per batch row), as in select.hip:
 //   scores      token_importance.py:134-176   s = α·N·w_l + β·log(i+1)/log(S) + γ·min(1, P/S)
@@ -11,34 +11,44 @@
 //   fallback    selective_propagation.py:205-211  topk(max(1, int(0.1·S))) if nothing selected
 //   compaction  selective_propagation.py:214-232  kept rows in ascending original index
 //
-// F1  fsel_score_kernel: G = ceil(S/1024) workgroups of 1024 threads, one token per thread.
-//     Scores and classes; per-workgroup class counts and score sums; a 4096-bin histogram per
-//     class over a FIXED linear binning of the score range (any monotone map of the score works:
-//     the histogram only has to tell which bin holds each class's threshold), and every token's
-//     (key, index) appended to a 64-entry slot list of its bin (slot = the histogram atomic's
-//     return value).  The LAST workgroup to arrive: quotas n_g from the class counts (the greedy
-//     in closed form), per partially kept class the bin where the count from the top reaches n_g,
-//     and the exact threshold from that bin's slot list (≤ 64 entries, one wave): key T and the
-//     number of tokens at T to take in index order.  A bin with more than 64 tokens (heavy ties)
-//     takes the exact rescan path: all S keys in registers, ≤ 3 LDS-histogram rounds.
-// F2  fsel_compact_kernel: the same G workgroups, one token per thread.  Keep decisions from
-//     (mode, T, ties) per class; per-workgroup aggregates (surely kept tokens per class, ties per
-//     group) published with sc1 stores + a flag; each workgroup sums its predecessors' aggregates
-//     (decoupled look-back: every aggregate is published before any is awaited, and workgroups are
-//     dispatched in index order, so the wait always ends), then ranks its tokens with block scans:
-//     mask, kept_index, row_offset; its kept-token statistics are added atomically.
+// G = ceil(S/1024) workgroups of 1024 threads, one token per thread, three phases:
+// 1 scores  Scores and classes; per-workgroup class counts and score sums; a 4096-bin histogram per
+//           class over a FIXED linear binning of the score range (any monotone map of the score
+//           works: the histogram only has to tell which bin holds each class's threshold), and every
+//           token's (key, index) appended to a 64-entry slot list of its bin (slot = the histogram
+//           atomic's return value, one atomic per bin and wave).
+// 2 select  Workgroup G−1 (dispatched last): once every workgroup's counts are published, the quotas
+//           n_g from the class counts (the greedy in closed form), per partially kept class the bin
+//           where the count from the top reaches n_g, and the exact threshold from that bin's slot
+//           list (≤ 64 entries, one wave): key T and the number of tokens at T to take in index
+//           order.  A bin with more than 64 tokens (heavy ties) takes the exact rescan path: all S
+//           keys in registers, ≤ 3 LDS-histogram rounds.
+// 3 compact Every workgroup, its token still in registers: keep decisions from (mode, T, ties) per
+//           group; per-workgroup aggregates (surely kept tokens per class, ties per group); each
+//           workgroup sums its predecessors' aggregates (decoupled look-back: every aggregate is
+//           published before any is awaited, and all G <= 32 workgroups are resident at once), then
+//           ranks its tokens with block scans: mask, kept_index, row_label, row_offset; its
+//           kept-token statistics are added atomically.
 //
-// Cross-workgroup hand-offs (MI355X_MICROARCH.md "Valid forms"): sc1 stores of every handed-off
-// word, every storing wave drains with s_waitcnt vmcnt(0), one lane signals (agent-scope atomic add,
-// or an sc1 flag store); the consumer reads with sc1 loads.
+// Hand-offs between workgroups are TAGGED 8-byte words (bit 63 set on a zeroed word: the region is
+// cleared before every launch), written with sc1 stores and polled with sc1 loads, so a consumer sees
+// data and flag in one round trip and producers need no drain between them (MI355X_MICROARCH.md
+// hand-off rows: each separate flag or drain costs a memory round trip, ≈1–2 µs).  The one drain
+// left is phase 1's: a workgroup's slot-list entries and score sums are complete (s_waitcnt
+// vmcnt(0)) before its tagged counts word, which is what the selecting workgroup polls.
 #include "common.h"
 
-#ifdef RTKV_SELECT_PROBE  // diagnostic build (tools/k2_probe.hip): phase timestamps of the last F1 workgroup
-__device__ unsigned long long g_k2_probe[16];
+#ifdef RTKV_SELECT_PROBE  // diagnostic build (tools/k2_probe.hip): phase timestamps (s_memrealtime, 100 MHz)
+__device__ unsigned long long g_k2_probe[16];   // the selecting workgroup's phases
 __device__ unsigned long long g_k2_clock[16];
-#define K2_PROBE(k) do { if (threadIdx.x == 0) { g_k2_probe[k] = __builtin_amdgcn_s_memrealtime(); g_k2_clock[k] = __builtin_amdgcn_s_memtime(); } } while (0)
+__device__ unsigned long long g_k2_wg[32][10];  // per workgroup phase timestamps
+__device__ int g_k2_rep;  // the probe's second pass over phase 2 (warm instruction cache) records at k + 8
+#define K2_PROBE(k) do { if (threadIdx.x == 0) { g_k2_probe[(k) + 8 * g_k2_rep] = __builtin_amdgcn_s_memrealtime(); g_k2_clock[(k) + 8 * g_k2_rep] = __builtin_amdgcn_s_memtime(); } } while (0)
+#define K2_WG(k) do { if (threadIdx.x == 0) g_k2_wg[blockIdx.x][k] = __builtin_amdgcn_s_memrealtime(); } while (0)
+__device__ int g_k2_twice;  // set by the probe: run phase 2 twice (the first pass cold)
 #else
 #define K2_PROBE(k) do { } while (0)
+#define K2_WG(k) do { } while (0)
 #endif
 
 namespace rtkv {
@@ -53,41 +63,22 @@ constexpr int kGrp = 4;            // classes LOW, MEDIUM, HIGH + "all tokens" (
 constexpr int kCap = 64;           // slot list entries per bin (one per lane of a wave)
 constexpr int kMaxS = 32 * kST;    // 32 tokens per thread in the rescan path
 constexpr int kMaxG = kMaxS / kST; // workgroups
+constexpr uint64_t kTag = 1ull << 63;
 enum { M_NONE = 0, M_ALL = 1, M_PART = 2 };
 
-struct FastPartial {               // per F1 workgroup, sc1 stores
-  uint32_t cnt[3];
-  uint32_t pad;
+struct FastHead {                  // zeroed before the launch (K1 or a memset): tagged hand-off words
+  uint64_t part[kMaxG];            // phase 1, per workgroup: kTag | class counts (3 x 11 bits)
+  uint64_t sel[8];                 // phase 2: [q] kTag | fallback<<50 | mode<<48 | ties<<32 | T; [4], [5] the mean
+  uint64_t agg[kMaxG][2];          // phase 3, per workgroup: kTag | sure (3 x 11 bits), kTag | ties (4 x 11 bits)
+};
+struct FastPartial {               // phase 1, per workgroup (complete before its counts word)
   double ssum;
-};
-struct FastAgg {                   // per F2 workgroup, sc1 stores
-  uint64_t sure3;                  // 3 x 16-bit: kept tokens per class, ties at T excluded
-  uint64_t ties4;                  // 4 x 16-bit: tokens at each partial group's T
-  uint64_t pad[6];
-};
-struct FastSel {                   // F1's last workgroup -> F2
-  int32_t mode[kGrp];
-  uint32_t thr[kGrp];              // threshold key T of each partial group
-  int32_t ties[kGrp];              // tokens at T to take, in index order
-  int32_t fallback;
-  int32_t pad;
-  double mean;                     // score mean (for Σ (s - mean)^2)
-  double ssum;
-  int64_t ccount[3];
-};
-struct FastHead {                  // zeroed before F1 (K1 or a memset)
-  uint32_t done1, pad0;
-  uint32_t smin_c, smax;           // score keys: ~min and max (atomic max from zero)
-  uint32_t pad[60];
-  uint32_t flag[kMaxG];            // F2 aggregates published
-  uint32_t pad2[64 - kMaxG];
+  uint32_t kmn, kmx;               // score key range
 };
 struct FastLayout {
   FastHead* head;                  // zeroed
   uint32_t* hist;                  // [kGrp][kNBin] (zeroed)
   FastPartial* part;               // [G]
-  FastAgg* agg;                    // [G]
-  FastSel* sel;
   uint64_t* slots;                 // [kGrp][kNBin][kCap] of (key << 32 | index)
 };
 
@@ -97,7 +88,7 @@ struct FastArgs {
   float bin_lo[kGrp];              // bin(s) = clamp(floor((s - lo) * inv), 0, kNBin - 1): monotone in s
   float bin_inv[kGrp];
   int hist_fb;                     // histogram the fallback group too (fallback possible)
-  rtkv_early_stats* early;         // host-mapped stats mirror (nullable), published by F1's last workgroup
+  rtkv_early_stats* early;         // host-mapped stats mirror (nullable), published by the selecting workgroup
   uint64_t early_seq;
 };
 
@@ -119,6 +110,66 @@ __device__ __forceinline__ int bin_of(float s, float lo, float inv) {
 template <typename T> __device__ __forceinline__ void opaque(T& v) { asm volatile("" : "+v"(v)); }
 
 __device__ __forceinline__ uint32_t fld(uint64_t v, int g) { return (uint32_t)(v >> (16 * g)) & 0xffffu; }
+
+// Exclusive block scan of a uint32 (block total < 2^32); *total = the block total.  `sh` is a [kSW]
+// LDS array private to this call site.
+// Inclusive wave scan on DPP lane moves (row_shr within rows of 16, then row_bcast:15 / :31 across
+// rows): register-to-register, no LDS round trips as __shfl's ds_bpermute takes.
+__device__ __forceinline__ uint32_t wave_scan_dpp(uint32_t v) {
+  int x = (int)v;
+  x += __builtin_amdgcn_update_dpp(0, x, 0x111, 0xf, 0xf, false);  // row_shr:1
+  x += __builtin_amdgcn_update_dpp(0, x, 0x112, 0xf, 0xf, false);  // row_shr:2
+  x += __builtin_amdgcn_update_dpp(0, x, 0x114, 0xf, 0xf, false);  // row_shr:4
+  x += __builtin_amdgcn_update_dpp(0, x, 0x118, 0xf, 0xf, false);  // row_shr:8
+  x += __builtin_amdgcn_update_dpp(0, x, 0x142, 0xa, 0xf, false);  // row_bcast:15 into rows 1, 3
+  x += __builtin_amdgcn_update_dpp(0, x, 0x143, 0xc, 0xf, false);  // row_bcast:31 into rows 2, 3
+  return (uint32_t)x;
+}
+
+__device__ __forceinline__ uint32_t block_excl_scan32(uint32_t v, uint32_t* sh, uint32_t* total) {
+  const int lane = threadIdx.x & (kWave - 1), wid = threadIdx.x / kWave;
+  const uint32_t inc = wave_scan_dpp(v);
+  if (lane == kWave - 1) sh[wid] = inc;
+  __syncthreads();
+  uint32_t ws = sh[lane & (kSW - 1)];
+#pragma unroll
+  for (int o = 1; o < kSW; o <<= 1) {
+    const uint32_t n = __shfl_up(ws, o, kWave);
+    if ((lane & (kSW - 1)) >= o) ws += n;
+  }
+  *total = __shfl(ws, kSW - 1, kWave);
+  const uint32_t base = wid > 0 ? __shfl(ws, wid - 1, kWave) : 0u;
+  return base + inc - v;
+}
+
+// Ranks in thread order of NF one-bit flags per thread, and their workgroup totals, from wave
+// ballots (the popcount below the lane plus the counts of the preceding waves): one barrier, no
+// shuffles.  `sh` is an [NF][kSW] LDS array private to the call site.
+template <int NF>
+__device__ __forceinline__ void block_flag_ranks(const bool (&f)[NF], uint32_t (&rank)[NF], uint32_t (&total)[NF],
+                                                 uint32_t (*sh)[kSW]) {
+  const int lane = threadIdx.x & (kWave - 1), wid = threadIdx.x / kWave;
+  const uint64_t lt = (1ull << lane) - 1ull;
+  uint64_t b[NF];
+#pragma unroll
+  for (int q = 0; q < NF; ++q) {
+    b[q] = __ballot(f[q]);
+    if (lane == 0) sh[q][wid] = (uint32_t)__popcll(b[q]);
+  }
+  __syncthreads();
+#pragma unroll
+  for (int q = 0; q < NF; ++q) {
+    uint32_t before = 0, tot = 0;
+#pragma unroll
+    for (int w = 0; w < kSW; ++w) {
+      const uint32_t v = sh[q][w];
+      tot += v;
+      before += w < wid ? v : 0u;
+    }
+    rank[q] = before + (uint32_t)__popcll(b[q] & lt);
+    total[q] = tot;
+  }
+}
 
 // Exclusive block scan of a packed uint64 (independent 16-bit fields whose block totals stay
 // < 65536); *total = the block total.  `sh` is a [kSW] LDS array private to this call site.
@@ -152,6 +203,67 @@ __device__ __forceinline__ float bin_inv_of(const FastArgs& g, int q) {
 
 __device__ __forceinline__ int class_of(float s, const rtkv_layer_params& p) {
   return (s >= p.theta_h) ? 2 : ((s >= p.theta_m && s < p.theta_h) ? 1 : 0);  // dynamic_quantization.py:41-45
+}
+
+
+// 16-bit packed fields <-> 11-bit packed fields (per-workgroup counts are <= 1024)
+__device__ __forceinline__ uint64_t to11(uint64_t v16, int n) {
+  uint64_t r = 0;
+#pragma unroll
+  for (int q = 0; q < 4; ++q)
+    if (q < n) r |= (uint64_t)fld(v16, q) << (11 * q);
+  return r;
+}
+__device__ __forceinline__ uint64_t from11(uint64_t v11, int n) {
+  uint64_t r = 0;
+#pragma unroll
+  for (int q = 0; q < 4; ++q)
+    if (q < n) r |= ((v11 >> (11 * q)) & 0x7ffull) << (16 * q);
+  return r;
+}
+
+// A histogram increment whose return value is the token's slot, aggregated over the wave: lanes with
+// the same bin id v (< 2^14) share one atomic by the lowest of them, and each takes base + its rank
+// among those peers (the slot order within a bin is arbitrary anyway: slot lists are ranked by
+// (key, index)).  Attention-like importance piles thousands of tokens into a few bins, where one
+// returning atomic per token serialises on the address (~11 ns each).
+__device__ __forceinline__ uint32_t hist_slot(uint32_t* addr, uint32_t v, bool part) {
+  uint64_t peers = __ballot(part);
+#pragma unroll
+  for (int k = 0; k < 14; ++k) {
+    const uint64_t bk = __ballot((v >> k) & 1u);
+    peers &= ((v >> k) & 1u) ? bk : ~bk;
+  }
+  const int lane = threadIdx.x & (kWave - 1);
+  const uint64_t below = peers & ((1ull << lane) - 1ull);
+  const int leader = peers ? __ffsll((unsigned long long)peers) - 1 : 0;
+  uint32_t base = 0u;
+  if (part && below == 0ull) base = atomicAdd(addr, (uint32_t)__popcll(peers));
+  base = (uint32_t)__shfl((int)base, leader, kWave);
+  return base + (uint32_t)__popcll(below);
+}
+
+// A 16-byte coherent load (global_load_dwordx4 ... sc1, as ld_sc1 for one word).  The compiler does not
+// track inline-asm loads: the caller waits (s_waitcnt vmcnt(0)) before the first use.
+__device__ __forceinline__ rtkv_u32x4 ld16_sc1(const uint32_t* p) {
+  rtkv_u32x4 v;
+  asm volatile("global_load_dwordx4 %0, %1, off sc1" : "=v"(v) : "v"(p) : "memory");
+  return v;
+}
+
+// Poll tagged words: lanes l < n of the calling wave wait for words[l * stride] to carry kTag and
+// return it (0 for the other lanes).
+__device__ __forceinline__ uint64_t poll_tagged(const uint64_t* words, int stride, int n) {
+  const int lane = threadIdx.x & (kWave - 1);
+  uint64_t w = 0;
+  if (lane < n) {
+    w = ld_sc1(words + (size_t)lane * stride);
+    while (!(w & kTag)) {
+      __builtin_amdgcn_s_sleep(1);
+      w = ld_sc1(words + (size_t)lane * stride);
+    }
+  }
+  return w;
 }
 
 // ------------------------------------------------------------------------------------ rescan path
@@ -295,92 +407,133 @@ __device__ __forceinline__ void rescan_thresholds(const FastArgs& g, uint32_t* h
     if ((heavy >> q) & 1) thr[q] = lo[q];
 }
 
-// ------------------------------------------------------------------------------------ thresholds
-// The last F1 workgroup: quotas, threshold bins, exact thresholds.  Writes FastSel.
+// ------------------------------------------------------------------------------------ phase 2
+// Workgroup G−1, after its own phase 1: quotas, threshold bins, exact thresholds; publishes the
+// selection words and the statistics.  s_selw receives the selection words (thread 0 writes them;
+// the caller's barrier publishes them to the workgroup).
 template <int TPT>
-__device__ __forceinline__ void select_thresholds(const FastArgs& g, uint32_t* hist_lds) {
+__device__ __forceinline__ void select_thresholds(const FastArgs& g, uint32_t* hist_lds, uint64_t* s_selw) {
   const FinalizeArgs& a = g.f;
-  __shared__ uint64_t s_scan[kSW];
+  __shared__ uint32_t s_scan32[kGrp][kSW];
+  __shared__ uint64_t s_part[kMaxG];
   __shared__ uint32_t s_pick[kGrp][3];
   __shared__ uint32_t s_thr[kGrp];
   __shared__ int s_tie[kGrp];
+  __shared__ double s_ssum;
+  __shared__ uint32_t s_kr[2];
   const int t = threadIdx.x, lane = t & (kWave - 1), wid = t / kWave;
   const int S = (int)a.S;
   const int G = (S + kST - 1) / kST;
   K2_PROBE(0);
-  // ---- partials of the F1 workgroups (lane l of every wave reads workgroup l; G <= 32)
-  uint32_t c0 = 0, c1 = 0, c2 = 0;
-  double ssum = 0.0;
-  if (lane < G) {
+  // ---- every workgroup's class counts (tagged words; their slot lists and sums are complete)
+  if (wid == 0) {
+    const uint64_t w = poll_tagged(g.L.head->part, 1, G);
+    if (lane < G) s_part[lane] = w;
+  }
+  __syncthreads();
+  K2_PROBE(1);
+  // ---- issue every histogram load the thresholds may need (thread t owns descending bins 4t..4t+3)
+  // before the quotas are known, and wave 0 the score sums and ranges, in one round trip
+  const int ngrp = g.hist_fb ? 4 : 3;
+  double p_ss = 0.0;
+  uint32_t p_kmn = 0xffffffffu, p_kmx = 0u;
+  if (wid == 0 && lane < G) {
     const FastPartial* pp = g.L.part + lane;
-    c0 = ld_sc1(&pp->cnt[0]);
-    c1 = ld_sc1(&pp->cnt[1]);
-    c2 = ld_sc1(&pp->cnt[2]);
-    ssum = ld_sc1(&pp->ssum);
+    p_ss = ld_sc1(&pp->ssum);
+    p_kmn = ld_sc1(&pp->kmn);
+    p_kmx = ld_sc1(&pp->kmx);
   }
-#pragma unroll
-  for (int o = kWave / 2; o > 0; o >>= 1) {  // lanes >= G hold zeros
-    c0 += __shfl_xor(c0, o, kWave);
-    c1 += __shfl_xor(c1, o, kWave);
-    c2 += __shfl_xor(c2, o, kWave);
-    ssum += __shfl_xor(ssum, o, kWave);
-  }
-  const int64_t ccount[3] = {(int64_t)c0, (int64_t)c1, (int64_t)c2};
-  // ---- quotas: the greedy in closed form (selective_propagation.py:93-131), every thread
-  int mode[kGrp];
-  int need[kGrp];
-  int64_t quota[3];  // kept tokens per class (final unless the fallback runs)
+  uint32_t c[kGrp][4];
   {
-    const double u8 = 8.0 * ((double)S * a.p.propagation_ratio);
-    const int64_t U = (u8 >= 0.0) ? (u8 >= 9.0e18 ? (int64_t)9000000000000000000LL : (int64_t)floor(u8)) : -1;
-    int64_t used = 0, kept = 0;
+    rtkv_u32x4 h[kGrp];
 #pragma unroll
-    for (int k = 2; k >= 0; --k) {
-      const int64_t N = ccount[k], bb = a.p.bits[k];
-      int64_t n;
-      if (a.mode_select == 2) n = N;
-      else if (U < 0) n = 0;
-      else if (bb <= 0) n = N;
-      else {
-        const int64_t fit = (U - used) / bb;
-        n = fit < N ? fit : N;
-      }
-      used += n * (bb > 0 ? bb : 0);
-      kept += n;
-      need[k] = (int)n;
-      quota[k] = n;
-      mode[k] = (n == 0) ? M_NONE : (n == N ? M_ALL : M_PART);
+    for (int q = 0; q < kGrp; ++q) {
+      h[q] = rtkv_u32x4{0u, 0u, 0u, 0u};
+      if (q < ngrp) h[q] = ld16_sc1(g.L.hist + q * kNBin + (kNBin - 4 - 4 * t));
     }
-    int64_t kf = (int64_t)((double)S * 0.1);
-    if (kf < 1) kf = 1;
-    const bool fb = a.mode_select == 1 && !(a.p.flags & RTKV_NO_FALLBACK) && kept == 0;
-    need[3] = (int)kf;
-    mode[3] = !fb ? M_NONE : (kf >= S ? M_ALL : M_PART);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+    for (int q = 0; q < kGrp; ++q) { c[q][0] = h[q].w; c[q][1] = h[q].z; c[q][2] = h[q].y; c[q][3] = h[q].x; }
   }
+  if (wid == 0) {
+#pragma unroll
+    for (int o = kWave / 2; o > 0; o >>= 1) {  // lanes >= G hold the neutral values
+      p_ss += __shfl_xor(p_ss, o, kWave);
+      p_kmn = min(p_kmn, (uint32_t)__shfl_xor((int)p_kmn, o, kWave));
+      p_kmx = max(p_kmx, (uint32_t)__shfl_xor((int)p_kmx, o, kWave));
+    }
+    if (lane == 0) { s_ssum = p_ss; s_kr[0] = p_kmn; s_kr[1] = p_kmx; }
+  }
+#ifdef RTKV_SELECT_PROBE
+  {
+    uint32_t z = 0;
+#pragma unroll
+    for (int q = 0; q < kGrp; ++q) z += c[q][0] + c[q][1] + c[q][2] + c[q][3];
+    if (z == 0xffffffffu) g_k2_probe[15] = z;  // waits for the histogram loads
+    K2_PROBE(4);
+  }
+#endif
+  // ---- class counts and quotas in wave 0 (the other waves wait at the barrier, their histogram
+  // loads in flight): lane l reads workgroup l (G <= 32); the greedy in closed form
+  // (selective_propagation.py:93-131)
+  __shared__ int s_q[2 * kGrp];
+  __shared__ int64_t s_cc[3], s_quota[3];
+  if (wid == 0) {
+    uint64_t cnt = lane < G ? from11(s_part[lane] & ~kTag, 3) : 0ull;
+#pragma unroll
+    for (int o = kWave / 2; o > 0; o >>= 1) cnt += __shfl_xor(cnt, o, kWave);
+    if (lane == 0) {
+      // In 32-bit integers: N <= S <= 2^15 and bits <= 32, so every product and quotient that can
+      // decide n fits; the budget U = floor(8·S·ratio) (int64 in the reference) is compared as a
+      // double, exact below 2^53 (beyond, every class fits whole).
+      const double u8 = 8.0 * ((double)S * a.p.propagation_ratio);
+      const double Ud = u8 >= 9.0e18 ? 9.0e18 : floor(u8);
+      int used = 0, kept = 0;
+      for (int k = 2; k >= 0; --k) {
+        const int N = (int)fld(cnt, k), bb = a.p.bits[k];
+        int n;
+        if (a.mode_select == 2) n = N;
+        else if (!(u8 >= 0.0)) n = 0;  // U = -1 (selective_propagation.py: nothing fits)
+        else if (bb <= 0) n = N;
+        else {
+          const double x = Ud - (double)used;  // U - used >= 0
+          n = x >= (double)bb * (double)N ? N : (int)((uint32_t)x / (uint32_t)bb);
+        }
+        used += n * (bb > 0 ? bb : 0);
+        kept += n;
+        s_q[kGrp + k] = n;
+        s_quota[k] = n;
+        s_cc[k] = N;
+        s_q[k] = (n == 0) ? M_NONE : (n == N ? M_ALL : M_PART);
+      }
+      int64_t kf = (int64_t)((double)S * 0.1);
+      if (kf < 1) kf = 1;
+      const bool fb = a.mode_select == 1 && !(a.p.flags & RTKV_NO_FALLBACK) && kept == 0;
+      s_q[kGrp + 3] = (int)kf;
+      s_q[3] = !fb ? M_NONE : (kf >= S ? M_ALL : M_PART);
+    }
+  }
+  __syncthreads();
+  int mode[kGrp], need[kGrp];
+#pragma unroll
+  for (int q = 0; q < kGrp; ++q) { mode[q] = s_q[q]; need[q] = s_q[kGrp + q]; }
   const bool fallback = mode[3] != M_NONE;
   int part = 0;
 #pragma unroll
   for (int q = 0; q < kGrp; ++q) part |= (mode[q] == M_PART) << q;
   uint32_t thr[kGrp] = {0u, 0u, 0u, 0u};
+  K2_PROBE(5);
   if (part) {
-    // ---- the bin holding each partial group's threshold: thread t owns descending bins 4t..4t+3
-    uint32_t c[kGrp][4];
-    uint64_t pk = 0;
-#pragma unroll
-    for (int q = 0; q < kGrp; ++q) {
-      const uint32_t* hq = g.L.hist + q * kNBin + (kNBin - 4 - 4 * t);
-#pragma unroll
-      for (int j = 0; j < 4; ++j) c[q][j] = ((part >> q) & 1) ? ld_sc1(hq + 3 - j) : 0u;
-      pk |= (uint64_t)(c[q][0] + c[q][1] + c[q][2] + c[q][3]) << (16 * q);
-    }
+    // ---- the bin holding each partial group's threshold: one 32-bit scan per partial group
     if (t < kGrp) { s_pick[t][0] = 0u; s_pick[t][1] = 0u; s_pick[t][2] = 0u; }
-    uint64_t tot;
-    const uint64_t ex = block_excl_scan(pk, s_scan, &tot);
 #pragma unroll
     for (int q = 0; q < kGrp; ++q) {
       if (!((part >> q) & 1)) continue;
-      int run = (int)fld(ex, q);
-      if (run < need[q] && need[q] <= run + (int)fld(pk, q)) {
+      const uint32_t sum = c[q][0] + c[q][1] + c[q][2] + c[q][3];
+      uint32_t tot;
+      int run = (int)block_excl_scan32(sum, s_scan32[q], &tot);
+      K2_PROBE(6);
+      if (run < need[q] && need[q] <= run + (int)sum) {
         bool found = false;
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
@@ -394,6 +547,7 @@ __device__ __forceinline__ void select_thresholds(const FastArgs& g, uint32_t* h
         }
       }
     }
+    K2_PROBE(7);
     __syncthreads();
     int bstar[kGrp] = {0, 0, 0, 0};
     int heavy = 0;
@@ -404,7 +558,7 @@ __device__ __forceinline__ void select_thresholds(const FastArgs& g, uint32_t* h
       need[q] -= (int)s_pick[q][1];
       if ((int)s_pick[q][2] > kCap) heavy |= 1 << q;
     }
-    K2_PROBE(1);
+    K2_PROBE(2);
     // ---- light bins: wave q ranks its group's slot list (≤ 64 entries, one per lane)
     if (wid < kGrp && ((part >> wid) & 1) && !((heavy >> wid) & 1)) {
       const int q = wid;
@@ -434,24 +588,43 @@ __device__ __forceinline__ void select_thresholds(const FastArgs& g, uint32_t* h
       thr[q] = s_thr[q];
       need[q] = s_tie[q];
     }
+  } else {
+    __syncthreads();  // s_ssum / s_kr
   }
-  K2_PROBE(2);
+  K2_PROBE(3);
   if (t != 0) return;
-  // statistics known here; F2's workgroups add the kept-token ones (stats zeroed before F1)
+  // ---- the selection words first (the other workgroups wait on them), then the statistics
+  const double ssum = s_ssum;
+  const double mean = ssum / (double)S;
+  const uint64_t mb = __builtin_bit_cast(uint64_t, mean);
+  for (int q = 0; q < kGrp; ++q) {
+    const uint64_t w = kTag | ((uint64_t)(fallback ? 1 : 0) << 50) | ((uint64_t)mode[q] << 48) |
+                       ((uint64_t)(need[q] & 0xffff) << 32) | thr[q];
+    st_sc1(&g.L.head->sel[q], w);
+    s_selw[q] = w;
+  }
+  const uint64_t m_lo = kTag | (mb & 0xffffffffu), m_hi = kTag | (mb >> 32);
+  st_sc1(&g.L.head->sel[4], m_lo);
+  st_sc1(&g.L.head->sel[5], m_hi);
+  s_selw[4] = m_lo;
+  s_selw[5] = m_hi;
+  // statistics known here; phase 3 adds the kept-token sums (stats zeroed before the launch)
+  const int64_t ccount[3] = {s_cc[0], s_cc[1], s_cc[2]};
+  const int64_t quota[3] = {s_quota[0], s_quota[1], s_quota[2]};
   rtkv_layer_stats* hs = a.stats;
   rtkv_batch_stats* bs = reinterpret_cast<rtkv_batch_stats*>(hs + 1);
   for (int q = 0; q < 3; ++q) bs->class_count[q] = ccount[q];
   bs->fallback = fallback ? 1 : 0;
   hs->score_sum = ssum;
-  hs->score_min = key_score(~ld_sc1(&g.L.head->smin_c));
-  hs->score_max = key_score(ld_sc1(&g.L.head->smax));
+  hs->score_min = key_score(s_kr[0]);
+  hs->score_max = key_score(s_kr[1]);
   int flags = 0;
   if (a.kv_dtype == RTKV_F16)
     for (int q = 0; q < 3; ++q)
       if (ccount[q] > 0 && a.p.bits[q] >= 16) flags |= RTKV_FLAG_F16_QMAX_OVERFLOW;
   hs->error_flags = flags;
   hs->B = 1;
-  if (!fallback) {  // the kept counts are the quotas: final here (F2 adds only the score sums)
+  if (!fallback) {  // the kept counts are the quotas: final here (phase 3 adds only the score sums)
     int64_t n = 0, units = 0, bytes = 0;
     for (int q = 0; q < 3; ++q) {
       bs->kept_class[q] = quota[q];
@@ -493,29 +666,156 @@ __device__ __forceinline__ void select_thresholds(const FastArgs& g, uint32_t* h
     }
     __hip_atomic_store(&e->seq, g.early_seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
   }
-  FastSel* fs = g.L.sel;
-  for (int q = 0; q < kGrp; ++q) {
-    fs->mode[q] = mode[q];
-    fs->thr[q] = thr[q];
-    fs->ties[q] = need[q];
-  }
-  fs->fallback = fallback ? 1 : 0;
-  fs->mean = ssum / (double)S;
-  fs->ssum = ssum;
-  for (int q = 0; q < 3; ++q) fs->ccount[q] = ccount[q];
 }
 
-// ------------------------------------------------------------------------------------ F1
+// ------------------------------------------------------------------------------------ phase 3
+// Every workgroup: keep decisions for its token (s, l) still in registers, ranked across the row.
+// selw: the selection words in LDS.
+__device__ __forceinline__ void compact_phase(const FastArgs& g, float s, int l, int i, bool valid,
+                                              const uint64_t* selw) {
+  const FinalizeArgs& a = g.f;
+  __shared__ uint32_t s_f7[7][kSW];
+  __shared__ uint32_t s_f3[3][kSW];
+  __shared__ double s_d[2][kSW];
+  __shared__ uint64_t s_base[2];
+  const int t = threadIdx.x, lane = t & (kWave - 1), wid = t / kWave;
+  const int blk = blockIdx.x;
+  int mode[kGrp], tq[kGrp];
+  uint32_t thr[kGrp];
+#pragma unroll
+  for (int q = 0; q < kGrp; ++q) {
+    const uint64_t w = selw[q];
+    mode[q] = (int)((w >> 48) & 3u);
+    tq[q] = (int)((w >> 32) & 0xffffu);
+    thr[q] = (uint32_t)w;
+  }
+  const bool fallback = ((selw[0] >> 50) & 1u) != 0;
+  const double mean = __builtin_bit_cast(double, (selw[4] & 0xffffffffull) | ((selw[5] & 0xffffffffull) << 32));
+  // the class of group q's tokens at its threshold: q for a class; for the fallback group, the class
+  // of the threshold score (equal scores have equal classes)
+  const int tcls3 = class_of(key_score(thr[3]), a.p);
+  const uint32_t key = score_key(s);
+  const int e = valid ? (fallback ? 3 : l) : 4;
+  // ---- flags: surely kept (per class) and ties at T (per group); their in-workgroup ranks and
+  // totals (the aggregates, published before any wait)
+  bool f7[7] = {false, false, false, false, false, false, false};
+  bool sure = false;  // kept regardless of the tie order
+#pragma unroll
+  for (int q = 0; q < kGrp; ++q) {
+    const bool mine = e == q;
+    sure |= mine & ((mode[q] == M_ALL) | ((mode[q] == M_PART) & (key > thr[q])));
+    f7[3 + q] = mine & (mode[q] == M_PART) & (key == thr[q]);
+  }
+#pragma unroll
+  for (int c = 0; c < 3; ++c) f7[c] = sure & (l == c);  // under the token's class (also in the fallback group)
+  uint32_t r7[7], t7[7];
+  block_flag_ranks<7>(f7, r7, t7, s_f7);
+  if (wid == 0) {
+    if (lane == 0) {
+      const uint64_t x = (uint64_t)t7[0] | ((uint64_t)t7[1] << 16) | ((uint64_t)t7[2] << 32);
+      const uint64_t y = (uint64_t)t7[3] | ((uint64_t)t7[4] << 16) | ((uint64_t)t7[5] << 32) | ((uint64_t)t7[6] << 48);
+      st_sc1(&g.L.head->agg[blk][0], kTag | to11(x, 3));
+      st_sc1(&g.L.head->agg[blk][1], kTag | to11(y, 4));
+    }
+    K2_WG(6);
+    // look-back: lane p < blk waits for workgroup p's aggregate
+    const uint64_t w0 = poll_tagged(&g.L.head->agg[0][0], 2, blk);
+    const uint64_t w1 = poll_tagged(&g.L.head->agg[0][1], 2, blk);
+    uint64_t ps = lane < blk ? from11(w0 & ~kTag, 3) : 0ull;
+    uint64_t pt = lane < blk ? from11(w1 & ~kTag, 4) : 0ull;
+    // ties that predecessor p takes: those of its ties whose row-wide rank is below the quota
+    const uint64_t before = wave_inclusive_scan(pt) - pt;
+    uint64_t taken = 0;  // per class
+#pragma unroll
+    for (int q = 0; q < kGrp; ++q) {
+      const int b4 = (int)fld(before, q), mine_t = (int)fld(pt, q);
+      int take = tq[q] - b4;
+      take = take < 0 ? 0 : (take > mine_t ? mine_t : take);
+      taken += (uint64_t)take << (16 * (q < 3 ? q : tcls3));
+    }
+    ps = wave_sum(ps);
+    taken = wave_sum(taken);
+    pt = wave_sum(pt);
+    if (lane == 0) { s_base[0] = ps + taken; s_base[1] = pt; }
+  }
+  __syncthreads();
+  K2_WG(7);
+  const uint64_t kept_before = s_base[0], ties_before = s_base[1];
+  // ---- keep decisions (ties by their row-wide rank), then kept-row ranks per class in index order
+  bool take = false;
+#pragma unroll
+  for (int q = 0; q < kGrp; ++q) take |= f7[3 + q] & ((int)(r7[3 + q] + fld(ties_before, q)) < tq[q]);
+  const bool kept = valid & (f7[0] | f7[1] | f7[2] | take);
+  bool f3[3];
+#pragma unroll
+  for (int c = 0; c < 3; ++c) f3[c] = kept & (l == c);
+  uint32_t r3[3], t3[3];
+  block_flag_ranks<3>(f3, r3, t3, s_f3);
+  const uint64_t kept_tot = (uint64_t)t3[0] | ((uint64_t)t3[1] << 16) | ((uint64_t)t3[2] << 32);
+  K2_WG(9);
+  int64_t rb[3];
+#pragma unroll
+  for (int q = 0; q < 3; ++q) rb[q] = row_bytes(a, q);
+  if (valid) {
+    a.mask[i] = kept ? 1 : 0;
+    if (kept) {
+      const int64_t k0 = (int64_t)r3[0] + fld(kept_before, 0), k1 = (int64_t)r3[1] + fld(kept_before, 1),
+                    k2 = (int64_t)r3[2] + fld(kept_before, 2);
+      const int64_t row = k0 + k1 + k2;
+      if (row < a.row_capacity) {
+        a.kept_index[row] = i;
+        if (a.row_label) a.row_label[row] = (uint8_t)l;
+        if (a.row_offset) a.row_offset[row] = k0 * rb[0] + k1 * rb[1] + k2 * rb[2];
+      }
+    }
+  }
+  // ---- statistics: Σ kept scores, Σ (s - mean)^2 and the kept-token counts, added per workgroup
+  const double d = (double)s - mean;
+  const double ks = wave_sum(kept ? (double)s : 0.0), m2 = wave_sum(valid ? d * d : 0.0);
+  if (lane == 0) { s_d[0][wid] = ks; s_d[1][wid] = m2; }
+  __syncthreads();
+  if (wid == 0) {
+    double x = s_d[0][lane & (kSW - 1)], y = s_d[1][lane & (kSW - 1)];
+#pragma unroll
+    for (int o = kSW / 2; o > 0; o >>= 1) { x += __shfl_xor(x, o, kWave); y += __shfl_xor(y, o, kWave); }
+    if (lane == 0) {
+      rtkv_layer_stats* hs = a.stats;
+      rtkv_batch_stats* bs = reinterpret_cast<rtkv_batch_stats*>(hs + 1);
+      unsigned long long n = 0, units = 0, bytes = 0;
+      for (int q = 0; q < 3; ++q) {
+        const unsigned long long nq = fld(kept_tot, q);
+        if (nq && fallback) atomicAdd((unsigned long long*)&bs->kept_class[q], nq);
+        n += nq;
+        units += nq * (unsigned long long)a.p.bits[q];
+        bytes += nq * (unsigned long long)rb[q];
+      }
+      if (n) {
+        if (fallback) {  // otherwise phase 2 wrote the final counts (the quotas)
+          atomicAdd((unsigned long long*)&bs->kept, n);
+          atomicAdd((unsigned long long*)&bs->cost_units, units);
+          atomicAdd((unsigned long long*)&bs->packed_bytes, bytes);
+          atomicAdd((unsigned long long*)&hs->max_kept, n);
+          atomicAdd((unsigned long long*)&hs->total_packed_bytes, bytes);
+        }
+        atomicAdd(&bs->kept_score_sum, x);
+      }
+      atomicAdd(&hs->score_m2, y);
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------ kernel
 template <int TPT, bool HAS_T2, int DT>
-__global__ __launch_bounds__(kST) void fsel_score_kernel(FastArgs g) {
+__global__ __launch_bounds__(kST) void fsel_kernel(FastArgs g) {
   const FinalizeArgs& a = g.f;
   extern __shared__ uint32_t hist_lds[];   // [kGrp][kNBin] (the rescan path's rounds)
   __shared__ float s_mm[2][kSW];
   __shared__ double s_sum[kSW];
   __shared__ uint32_t s_c[5][kSW];
-  __shared__ int s_flag;
+  __shared__ uint64_t s_selw[8];
   const int t = threadIdx.x, lane = t & (kWave - 1), wid = t / kWave;
   const int S = (int)a.S;
+  K2_WG(0);
   // ---- global min/max of A (token_importance.py:71-83): K1's per-block partials, or the row
   float mn = INFINITY, mx = -INFINITY;
   if (a.A_part) {
@@ -531,8 +831,9 @@ __global__ __launch_bounds__(kST) void fsel_score_kernel(FastArgs g) {
   mx = s_mm[1][lane & (kSW - 1)];
 #pragma unroll
   for (int o = kSW / 2; o > 0; o >>= 1) { mn = fminf(mn, __shfl_xor(mn, o, kWave)); mx = fmaxf(mx, __shfl_xor(mx, o, kWave)); }
+  K2_WG(1);
   const float den = Dt<DT>::rnd(mx - mn), eps = Dt<DT>::rnd(1e-8f);
-  // ---- this thread's token: score, class, histogram bin + slot
+  // ---- phase 1: this thread's token: score, class, histogram bin + slot
   const int i = blockIdx.x * kST + t;
   const bool valid = i < S;
   float s = 0.f;
@@ -556,18 +857,20 @@ __global__ __launch_bounds__(kST) void fsel_score_kernel(FastArgs g) {
     l = class_of(s, a.p);
     st_sc1(a.scores + i, s);
     a.labels[i] = (uint8_t)l;
-    if (a.mode_select == 1) {
-      const uint64_t entry = ((uint64_t)score_key(s) << 32) | (uint32_t)i;
-      const int b = l * kNBin + bin_of(s, bin_lo_of(g, l), bin_inv_of(g, l));
-      const uint32_t slot = atomicAdd(&g.L.hist[b], 1u);
-      if (slot < kCap) st_sc1(g.L.slots + (size_t)b * kCap + slot, entry);
-      if (g.hist_fb) {
-        const int b3 = 3 * kNBin + bin_of(s, g.bin_lo[3], g.bin_inv[3]);
-        const uint32_t slot3 = atomicAdd(&g.L.hist[b3], 1u);
-        if (slot3 < kCap) st_sc1(g.L.slots + (size_t)b3 * kCap + slot3, entry);
-      }
+  }
+  K2_WG(2);
+  if (a.mode_select == 1) {  // wave-uniform: every lane takes part in the peer matching
+    const uint64_t entry = ((uint64_t)score_key(s) << 32) | (uint32_t)i;
+    const int b = l * kNBin + bin_of(s, bin_lo_of(g, l), bin_inv_of(g, l));
+    const uint32_t slot = hist_slot(&g.L.hist[b], (uint32_t)b, valid);
+    if (valid && slot < kCap) st_sc1(g.L.slots + (size_t)b * kCap + slot, entry);
+    if (g.hist_fb) {
+      const int b3 = 3 * kNBin + bin_of(s, g.bin_lo[3], g.bin_inv[3]);
+      const uint32_t slot3 = hist_slot(&g.L.hist[b3], (uint32_t)b3, valid);
+      if (valid && slot3 < kCap) st_sc1(g.L.slots + (size_t)b3 * kCap + slot3, entry);
     }
   }
+  K2_WG(3);
   // ---- workgroup partials: class counts, score sum, score key range
   const uint64_t b0 = __ballot(valid && l == 0), b1 = __ballot(valid && l == 1), b2 = __ballot(valid && l == 2);
   const double sw = wave_sum(valid ? (double)s : 0.0);
@@ -583,6 +886,7 @@ __global__ __launch_bounds__(kST) void fsel_score_kernel(FastArgs g) {
     s_sum[wid] = sw;
   }
   __syncthreads();
+  uint64_t cw = 0;
   if (wid == 0) {
     const int src = lane & (kSW - 1);
     uint32_t c0 = s_c[0][src], c1 = s_c[1][src], c2 = s_c[2][src], m0 = s_c[3][src], m1 = s_c[4][src];
@@ -596,164 +900,40 @@ __global__ __launch_bounds__(kST) void fsel_score_kernel(FastArgs g) {
       m1 = max(m1, (uint32_t)__shfl_xor((int)m1, o, kWave));
       ss += __shfl_xor(ss, o, kWave);
     }
+    cw = kTag | (uint64_t)c0 | ((uint64_t)c1 << 11) | ((uint64_t)c2 << 22);
     if (lane == 0) {
       FastPartial* pp = g.L.part + blockIdx.x;
-      st_sc1(&pp->cnt[0], c0);
-      st_sc1(&pp->cnt[1], c1);
-      st_sc1(&pp->cnt[2], c2);
       st_sc1(&pp->ssum, ss);
-      atomicMax(&g.L.head->smin_c, ~m0);  // minima complemented: the head starts at 0
-      atomicMax(&g.L.head->smax, m1);
+      st_sc1(&pp->kmn, m0);
+      st_sc1(&pp->kmx, m1);
     }
   }
-  // ---- the last workgroup to arrive finds the thresholds for the whole row
+  K2_WG(4);
+  // ---- publish the counts once this workgroup's slot entries and partials are complete
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  if (t == 0) {
-    const uint32_t old = __hip_atomic_fetch_add(&g.L.head->done1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    s_flag = (old + 1 == gridDim.x);
-    if (s_flag) {
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if (t == 0) st_sc1(&g.L.head->part[blockIdx.x], cw);
+  // ---- phase 2 in workgroup G−1; the others wait for the selection words
+  if (blockIdx.x == gridDim.x - 1) {
+#ifdef RTKV_SELECT_PROBE
+    if (g_k2_twice) {
+      if (t == 0) g_k2_rep = 1;
+      __syncthreads();
+      select_thresholds<TPT>(g, hist_lds, s_selw);
+      __syncthreads();
+      if (t == 0) g_k2_rep = 0;
+      __syncthreads();
     }
+#endif
+    select_thresholds<TPT>(g, hist_lds, s_selw);
+  } else if (wid == 0) {
+    const uint64_t w = poll_tagged(g.L.head->sel, 1, 6);
+    if (lane < 6) s_selw[lane] = w;
   }
   __syncthreads();
-  if (!s_flag) return;
-  select_thresholds<TPT>(g, hist_lds);
-}
-
-// ------------------------------------------------------------------------------------ F2
-__global__ __launch_bounds__(kST) void fsel_compact_kernel(FastArgs g) {
-  const FinalizeArgs& a = g.f;
-  __shared__ uint64_t s_scan[2][kSW];
-  __shared__ uint64_t s_r[2][kSW];
-  __shared__ double s_d[2][kSW];
-  __shared__ uint64_t s_base[3];
-  const int t = threadIdx.x, lane = t & (kWave - 1), wid = t / kWave;
-  const int S = (int)a.S;
-  const int blk = blockIdx.x;
-  const FastSel& fs = *g.L.sel;
-  int mode[kGrp], tq[kGrp];
-  uint32_t thr[kGrp];
-#pragma unroll
-  for (int q = 0; q < kGrp; ++q) { mode[q] = fs.mode[q]; thr[q] = fs.thr[q]; tq[q] = fs.ties[q]; }
-  const bool fallback = fs.fallback != 0;
-  // the class of group q's tokens at its threshold: q for a class; for the fallback group, the class
-  // of the threshold score (equal scores have equal classes)
-  const int tcls3 = class_of(key_score(thr[3]), a.p);
-  // ---- this thread's token
-  const int i = blk * kST + t;
-  const bool valid = i < S;
-  float s = 0.f;
-  int l = 0;
-  if (valid) { s = a.scores[i]; l = a.labels[i]; }
-  const uint32_t key = score_key(s);
-  const int e = valid ? (fallback ? 3 : l) : 4;
-  bool sure = false;  // kept regardless of the tie order
-  uint64_t tie = 0;
-#pragma unroll
-  for (int q = 0; q < kGrp; ++q) {
-    const bool mine = e == q;
-    sure |= mine & ((mode[q] == M_ALL) | ((mode[q] == M_PART) & (key > thr[q])));
-    tie |= (mine & (mode[q] == M_PART) & (key == thr[q])) ? 1ull << (16 * q) : 0ull;
-  }
-  const uint64_t sure3 = (valid & sure) ? 1ull << (16 * l) : 0ull;
-  // ---- workgroup aggregates: surely kept per class, ties per group (published before any wait)
-  const uint64_t as = wave_sum(sure3), at = wave_sum(tie);
-  if (lane == 0) { s_r[0][wid] = as; s_r[1][wid] = at; }
-  __syncthreads();
-  if (wid == 0) {
-    uint64_t x = s_r[0][lane & (kSW - 1)], y = s_r[1][lane & (kSW - 1)];
-#pragma unroll
-    for (int o = kSW / 2; o > 0; o >>= 1) { x += __shfl_xor(x, o, kWave); y += __shfl_xor(y, o, kWave); }
-    if (lane == 0) {
-      st_sc1(&g.L.agg[blk].sure3, x);
-      st_sc1(&g.L.agg[blk].ties4, y);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      st_sc1(&g.L.head->flag[blk], 1u);
-    }
-    // look-back: lane p < blk waits for workgroup p's aggregate
-    uint64_t ps = 0, pt = 0;
-    if (lane < blk) {
-      while (ld_sc1(&g.L.head->flag[lane]) == 0u) __builtin_amdgcn_s_sleep(1);
-      ps = ld_sc1(&g.L.agg[lane].sure3);
-      pt = ld_sc1(&g.L.agg[lane].ties4);
-    }
-    // ties that predecessor p takes: those of its ties whose row-wide rank is below the quota
-    const uint64_t before = wave_inclusive_scan(pt) - pt;
-    uint64_t taken = 0;  // per class
-#pragma unroll
-    for (int q = 0; q < kGrp; ++q) {
-      const int b4 = (int)fld(before, q), mine_t = (int)fld(pt, q);
-      int take = tq[q] - b4;
-      take = take < 0 ? 0 : (take > mine_t ? mine_t : take);
-      taken += (uint64_t)take << (16 * (q < 3 ? q : tcls3));
-    }
-    ps = wave_sum(ps);
-    taken = wave_sum(taken);
-    pt = wave_sum(pt);
-    if (lane == 0) { s_base[0] = ps + taken; s_base[1] = pt; }
-  }
-  __syncthreads();
-  const uint64_t kept_before = s_base[0], ties_before = s_base[1];
-  // ---- ties: ranks in index order across the whole row
-  uint64_t tie_tot;
-  const uint64_t tie_rank = block_excl_scan(tie, s_scan[0], &tie_tot) + ties_before;
-  bool take = false;
-#pragma unroll
-  for (int q = 0; q < kGrp; ++q) take |= (((tie >> (16 * q)) & 1ull) != 0) & ((int)fld(tie_rank, q) < tq[q]);
-  const bool kept = valid & (sure | take);
-  const uint64_t k3 = kept ? 1ull << (16 * l) : 0ull;
-  uint64_t kept_tot;
-  const uint64_t rank3 = block_excl_scan(k3, s_scan[1], &kept_tot) + kept_before;
-  int64_t rb[3];
-#pragma unroll
-  for (int q = 0; q < 3; ++q) rb[q] = row_bytes(a, q);
-  if (valid) {
-    a.mask[i] = kept ? 1 : 0;
-    if (kept) {
-      const int64_t row = (int64_t)fld(rank3, 0) + fld(rank3, 1) + fld(rank3, 2);
-      if (row < a.row_capacity) {
-        a.kept_index[row] = i;
-        if (a.row_label) a.row_label[row] = (uint8_t)l;
-        if (a.row_offset)
-          a.row_offset[row] = (int64_t)fld(rank3, 0) * rb[0] + (int64_t)fld(rank3, 1) * rb[1] + (int64_t)fld(rank3, 2) * rb[2];
-      }
-    }
-  }
-  // ---- statistics: Σ kept scores, Σ (s - mean)^2 and the kept-token counts, added per workgroup
-  const double d = (double)s - fs.mean;
-  const double ks = wave_sum(kept ? (double)s : 0.0), m2 = wave_sum(valid ? d * d : 0.0);
-  if (lane == 0) { s_d[0][wid] = ks; s_d[1][wid] = m2; }
-  __syncthreads();
-  if (wid == 0) {
-    double x = s_d[0][lane & (kSW - 1)], y = s_d[1][lane & (kSW - 1)];
-#pragma unroll
-    for (int o = kSW / 2; o > 0; o >>= 1) { x += __shfl_xor(x, o, kWave); y += __shfl_xor(y, o, kWave); }
-    if (lane == 0) {
-      rtkv_layer_stats* hs = a.stats;
-      rtkv_batch_stats* bs = reinterpret_cast<rtkv_batch_stats*>(hs + 1);
-      unsigned long long n = 0, units = 0, bytes = 0;
-      for (int q = 0; q < 3; ++q) {
-        const unsigned long long nq = fld(kept_tot, q);
-        if (nq && fallback) atomicAdd((unsigned long long*)&bs->kept_class[q], nq);
-        n += nq;
-        units += nq * (unsigned long long)a.p.bits[q];
-        bytes += nq * (unsigned long long)rb[q];
-      }
-      if (n) {
-        if (fallback) {  // otherwise F1 wrote the final counts (the quotas)
-          atomicAdd((unsigned long long*)&bs->kept, n);
-          atomicAdd((unsigned long long*)&bs->cost_units, units);
-          atomicAdd((unsigned long long*)&bs->packed_bytes, bytes);
-          atomicAdd((unsigned long long*)&hs->max_kept, n);
-          atomicAdd((unsigned long long*)&hs->total_packed_bytes, bytes);
-        }
-        atomicAdd(&bs->kept_score_sum, x);
-      }
-      atomicAdd(&hs->score_m2, y);
-    }
-  }
+  K2_WG(5);
+  compact_phase(g, s, l, i, valid, s_selw);
+  K2_WG(8);
 }
 
 }  // namespace
@@ -766,32 +946,31 @@ bool select_fast_eligible(const FinalizeArgs& f) {
          (f.mode_select == 1 || f.mode_select == 2) && f.mask && f.kept_index;
 }
 
-// Workspace: [FastHead][hist][partials][aggregates][sel][slots]; the first select_fast_zero_bytes()
-// must be zero before F1 (K1 clears them in rtkv_compress_layer).
+// Workspace: [FastHead][hist][partials][slots]; the first select_fast_zero_bytes() must be zero
+// before the launch (K1 clears them in rtkv_compress_layer).
 size_t select_fast_zero_bytes() { return sizeof(FastHead) + (size_t)kGrp * kNBin * 4; }
 size_t select_fast_workspace_bytes(int64_t) {
-  return select_fast_zero_bytes() + kMaxG * sizeof(FastPartial) + kMaxG * sizeof(FastAgg) + 256 +
-         (size_t)kGrp * kNBin * kCap * 8;
+  return select_fast_zero_bytes() + kMaxG * sizeof(FastPartial) + 256 + (size_t)kGrp * kNBin * kCap * 8;
 }
 
-template <int TPT, bool HAS_T2, int DT> static int launch_f1(const FastArgs& g, int G, hipStream_t st) {
+template <int TPT, bool HAS_T2, int DT> static int launch_fsel(const FastArgs& g, int G, hipStream_t st) {
   const size_t lds = (size_t)kGrp * kNBin * sizeof(uint32_t);
   static bool attr = false;  // per instantiation
   if (!attr) {
-    RTKV_HIP_CHECK(hipFuncSetAttribute((const void*)fsel_score_kernel<TPT, HAS_T2, DT>,
+    RTKV_HIP_CHECK(hipFuncSetAttribute((const void*)fsel_kernel<TPT, HAS_T2, DT>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     attr = true;
   }
-  hipLaunchKernelGGL((fsel_score_kernel<TPT, HAS_T2, DT>), dim3(G), dim3(kST), lds, st, g);
+  hipLaunchKernelGGL((fsel_kernel<TPT, HAS_T2, DT>), dim3(G), dim3(kST), lds, st, g);
   RTKV_HIP_CHECK(hipGetLastError());
   return RTKV_OK;
 }
 
-template <int TPT, bool HAS_T2> static int launch_f1_dt(const FastArgs& g, int G, hipStream_t st) {
+template <int TPT, bool HAS_T2> static int launch_fsel_dt(const FastArgs& g, int G, hipStream_t st) {
   switch (g.f.a_dtype) {
-    case RTKV_F16: return launch_f1<TPT, HAS_T2, RTKV_F16>(g, G, st);
-    case RTKV_BF16: return launch_f1<TPT, HAS_T2, RTKV_BF16>(g, G, st);
-    default: return launch_f1<TPT, HAS_T2, RTKV_F32>(g, G, st);
+    case RTKV_F16: return launch_fsel<TPT, HAS_T2, RTKV_F16>(g, G, st);
+    case RTKV_BF16: return launch_fsel<TPT, HAS_T2, RTKV_BF16>(g, G, st);
+    default: return launch_fsel<TPT, HAS_T2, RTKV_F32>(g, G, st);
   }
 }
 
@@ -807,12 +986,8 @@ int launch_select_fast(const FinalizeArgs& f, void* ws, bool zeroed, hipStream_t
   g.L.hist = reinterpret_cast<uint32_t*>(p);
   p += (size_t)kGrp * kNBin * 4;
   g.L.part = reinterpret_cast<FastPartial*>(p);
-  p += kMaxG * sizeof(FastPartial);
-  g.L.agg = reinterpret_cast<FastAgg*>(p);
-  p += kMaxG * sizeof(FastAgg);
-  g.L.sel = reinterpret_cast<FastSel*>(p);
-  p += 256;
-  g.L.slots = reinterpret_cast<uint64_t*>(p);
+  p += kMaxG * sizeof(FastPartial) + 256;
+  g.L.slots = reinterpret_cast<uint64_t*>((reinterpret_cast<uintptr_t>(p) + 255) & ~(uintptr_t)255);
   // Fixed score binning.  s = t1 + t2 + t3 with t1 = α·w·N (N in [0, 1]), t2 = β·pos (pos in
   // [0, 1]), t3 = γ·ctx: any range works for correctness (bins are clamped, the map stays
   // monotone); this one spreads the scores over the bins.
@@ -838,14 +1013,11 @@ int launch_select_fast(const FinalizeArgs& f, void* ws, bool zeroed, hipStream_t
     RTKV_HIP_CHECK(hipMemsetAsync(ws, 0, select_fast_zero_bytes(), st));
     RTKV_HIP_CHECK(hipMemsetAsync(f.stats, 0, rtkv_stats_bytes(f.B), st));
   }
+  // All G <= 32 workgroups (1024 threads, 64 KB of LDS: one per CU) are resident at once, which the
+  // waits of phases 2 and 3 rely on; a busy GPU only delays the last ones.
   const int G = (int)((f.S + kST - 1) / kST);
-  int rc;
-  if (f.S <= 16 * kST) rc = f.T2 ? launch_f1_dt<16, true>(g, G, st) : launch_f1_dt<16, false>(g, G, st);
-  else rc = f.T2 ? launch_f1_dt<32, true>(g, G, st) : launch_f1_dt<32, false>(g, G, st);
-  if (rc) return rc;
-  hipLaunchKernelGGL(fsel_compact_kernel, dim3(G), dim3(kST), 0, st, g);
-  RTKV_HIP_CHECK(hipGetLastError());
-  return RTKV_OK;
+  if (f.S <= 16 * kST) return f.T2 ? launch_fsel_dt<16, true>(g, G, st) : launch_fsel_dt<16, false>(g, G, st);
+  return f.T2 ? launch_fsel_dt<32, true>(g, G, st) : launch_fsel_dt<32, false>(g, G, st);
 }
 
 }  // namespace rtkv
