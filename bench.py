@@ -24,7 +24,9 @@ Rank 0 prints ONE JSON line.  ``value`` = algorithmic bytes of the whole job ÷ 
 same workload.  Extra legs (``--legs``, single GPU, same inputs): ``f16`` (the workload in fp16),
 ``packed_only`` (codes + scale/zp, no dequantized K'/V' — what the packed consumers read) and
 ``drop_in`` (the reference caller's path, RealTimePrefillCompressor.compress_layer_kv_cache with
-its per-layer host sync; ``ttft_ms`` = Σ processing_time as longbench_eval.py:160 defines TTFT).
+its per-layer host sync; ``ttft_ms`` = Σ processing_time as longbench_eval.py:160 defines TTFT) and
+``streams2`` (the main workload with consecutive layers on two streams, so that one layer's
+latency-bound selection overlaps the neighbouring layers' bandwidth-bound kernels).
 """
 from __future__ import annotations
 
@@ -55,9 +57,9 @@ def parse():
                     help="K/V/attention dtype (default: the reference model's fp32)")
     ap.add_argument("--no-packed", action="store_true", help="skip the packed-code output")
     ap.add_argument("--no-dequant", action="store_true", help="skip the dequantized K'/V' output (packed only)")
-    ap.add_argument("--legs", default="f16,packed_only,drop_in",
-                    help="extra single-GPU legs after the main line: comma list of f16, packed_only, drop_in "
-                         "(or 'none')")
+    ap.add_argument("--legs", default="f16,packed_only,drop_in,streams2",
+                    help="extra single-GPU legs after the main line: comma list of f16, packed_only, drop_in, "
+                         "streams2 (or 'none')")
     ap.add_argument("--leg-steps", type=int, default=5)
     ap.add_argument("--cpu-baseline-seconds", type=float, default=12.0,
                     help="CPU work budget of the oracle sample (layers are added until it is spent; 0 = skip)")
@@ -150,7 +152,18 @@ class Job:
             self.params.append(rtkv.params_from_config(self.cfg, l, self.P, prop.get_layer_propagation_ratio(l), flags))
         self.ws = rtkv.Workspace(device)
         self.ws.get(1, self.S)
+        # layer pipelining (streams2 leg): layer l runs on stream l % n with that stream's workspace;
+        # a layer's buffers always see the same stream, so steps stay ordered per layer
+        self.streams, self.wss = [None], [self.ws]
         torch.cuda.synchronize(device)
+
+    def set_streams(self, n):
+        import rtkv
+        self.streams = [None] + [torch.cuda.Stream(self.device) for _ in range(n - 1)]
+        self.wss = [self.ws] + [rtkv.Workspace(self.device) for _ in range(n - 1)]
+        for w in self.wss:
+            w.get(1, self.S)
+        torch.cuda.synchronize(self.device)
 
     def step(self, events=None):
         """Compress every layer (single GPU); events: list of 4-tuples of torch events or None."""
@@ -158,7 +171,22 @@ class Job:
         from rtkv import _lib as L
         import ctypes
         qk = self.args.importance == "qk"
+        n = len(self.streams) if events is None else 1
+        if n > 1:
+            main = torch.cuda.current_stream(self.device)
+            for st in self.streams[1:]:
+                st.wait_stream(main)
         for l in range(self.args.layers):
+            if n > 1:
+                st = self.streams[l % n]
+                with torch.cuda.stream(st if st is not None else torch.cuda.current_stream(self.device)):
+                    if qk:
+                        K, V, Q, lse = self.inputs[l]
+                        rtkv.compress_layer_qk(K, V, Q, lse, self.params[l], self.bufs[l], self.wss[l % n])
+                    else:
+                        K, V, W = self.inputs[l]
+                        rtkv.compress_layer(K, V, W, self.params[l], self.bufs[l], self.wss[l % n])
+                continue
             if qk:
                 K, V, Q, lse = self.inputs[l]
                 if events is None:
@@ -179,6 +207,12 @@ class Job:
             L.check(fn(ctypes.byref(kd), ctypes.byref(wd), ctypes.byref(self.params[l]), ctypes.byref(out),
                        self.ws.buf.data_ptr(), self.ws.buf.numel(), L.stream_ptr(self.device), ev),
                     "compress_layer_events")
+
+    def join(self):
+        """The main stream waits for the pipelining streams (end of a step)."""
+        main = torch.cuda.current_stream(self.device)
+        for st in self.streams[1:]:
+            main.wait_stream(st)
 
     def elem(self):
         return torch.tensor([], dtype=self.dtype).element_size()
@@ -212,10 +246,12 @@ class Job:
         """(ms per step, per-layer event times [K1, K2, K4] in µs) of this job alone."""
         for _ in range(warmup):
             self.step()
+            self.join()
         torch.cuda.synchronize(self.device)
         t0 = time.perf_counter()
         for _ in range(steps):
             self.step()
+            self.join()
         torch.cuda.synchronize(self.device)
         ms = (time.perf_counter() - t0) / steps * 1e3
         return ms, self.kernel_times()
@@ -533,6 +569,15 @@ def main():
                     leg = Job(args, device, rank, world, emit_dequant=False, emit_packed=True, inputs=job.inputs)
                     legs["packed_only"] = leg_summary(args, leg, *leg.timed(args.leg_steps, 2))
                     del leg
+                elif name == "streams2":  # the main workload, consecutive layers on two streams
+                    job.set_streams(2)
+                    ms2, _ = job.timed(args.leg_steps, 2)
+                    job.set_streams(1)
+                    tot, _ = job.layer_bytes()
+                    legs["streams2"] = {"value": round(sum(tot) / (ms2 / 1e3) / 1e9, 2), "unit": "GB/s",
+                                        "ms_per_step": round(ms2, 4),
+                                        "path": "layer l on stream l % 2 (one workspace per stream): K2's "
+                                                "16-workgroup latency chain overlaps the other stream's K1/K4"}
                 elif name == "drop_in":
                     legs["drop_in"] = drop_in_leg(args, job, args.leg_steps, 2)
                     legs["drop_in"]["raw_driver_ms_per_layer"] = round(ms_per_step / args.layers, 4)

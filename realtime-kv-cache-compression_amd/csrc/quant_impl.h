@@ -182,6 +182,57 @@ template <int DT> __device__ __forceinline__ float dequant(float q, const RowPar
   return Dt<DT>::rnd(Dt<DT>::rnd(q - rp.zp) * rp.scale);  // :124
 }
 
+// ------------------------------------------------------------------------------------ fp16 rows
+// After the fp32 quotient, every step of an fp16 row is a native f16 op on pairs (v_pk_add_f16,
+// v_pk_mul_f16, v_pk_max/min_f16): RN16(a ∘ b) of f16 operands equals RN16(RN32(a ∘ b)), the fp32 op
+// rounded to fp16 that torch performs on the CPU — double rounding through a format of p' >= 2p + 2
+// bits is innocuous for + − × ÷ (Figueroa 1995; 24 >= 2·11 + 2).  The quotient itself stays the
+// proven fp32 fast quotient, rounded once to f16 (RN16(RN32(x / s)) = RN16(x / s) by the same rule).
+typedef _Float16 h2_t __attribute__((ext_vector_type(2)));
+typedef unsigned short u16x2_t __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ h2_t as_h2(uint32_t w) { return __builtin_bit_cast(h2_t, w); }
+__device__ __forceinline__ uint32_t h2_bits(h2_t v) { return __builtin_bit_cast(uint32_t, v); }
+
+// Codes (and, with DEQ, the dequantized f16 pair words) of one 8-element f16 chunk of a row without
+// NaN.  DEQ keeps torch.clamp's compare-select (the sign of a zero code reaches the dequantized
+// value); codes alone take the packed max/min (equal codes: a zero is code 0 either way).
+template <bool DEQ>
+__device__ __forceinline__ void f16_chunk_codes(const uint4 raw, float s, float r, h2_t zp2, h2_t s2, _Float16 qmax,
+                                                uint32_t (&qi)[8], uint32_t (&dq)[4]) {
+  const uint32_t w[4] = {raw.x, raw.y, raw.z, raw.w};
+  const h2_t zero2 = {(_Float16)0.f, (_Float16)0.f}, qmax2 = {qmax, qmax};
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const h2_t xh = as_h2(w[k]);
+    float q[2];
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const float x = (float)xh[j];
+      const float q0 = x * r;
+      const float e = __builtin_fmaf(-q0, s, x);
+      // without DEQ the e == 0 guard (which only keeps the sign of a zero quotient) is moot
+      float qq = DEQ ? (e == 0.f ? q0 : __builtin_fmaf(e, r, q0)) : __builtin_fmaf(e, r, q0);
+      asm volatile("" : "+v"(qq));  // the fp32 quotient, then its f16 rounding (no v_fma_mix)
+      q[j] = qq;
+    }
+    const h2_t qh = {(_Float16)q[0], (_Float16)q[1]};
+    const h2_t t = __builtin_elementwise_roundeven(qh + zp2);  // dynamic_quantization.py:120
+    h2_t c;
+    if constexpr (DEQ) {
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        _Float16 v = t[j] < (_Float16)0.f ? (_Float16)0.f : t[j];  // :121
+        c[j] = v > qmax ? qmax : v;
+      }
+      dq[k] = h2_bits((c - zp2) * s2);  // :124
+    } else {
+      c = __builtin_elementwise_min(__builtin_elementwise_max(t, zero2), qmax2);
+    }
+    qi[2 * k] = (uint32_t)c[0];
+    qi[2 * k + 1] = (uint32_t)c[1];
+  }
+}
+
 // ------------------------------------------------------------------------------------ K4
 // Pack 8 codes of W bits (compile-time W in {2,4,8,16}) and store them at dst (W bytes).
 template <int W> __device__ __forceinline__ void pack_store(uint8_t* dst, const uint32_t (&q)[8], bool aligned) {
@@ -300,16 +351,38 @@ __global__ __launch_bounds__(256, (DT == RTKV_F32 && NCH == 8 && FULL && CONTIG)
     for (int k = 0; k < NCH; ++k)
       if (valid(k)) raw[k] = load_chunk_nt<DT>(src + in_off[k]);
     float mn = INFINITY, mx = -INFINITY, anz = INFINITY;
+    bool row_nan = false;
+    if constexpr (DT == RTKV_F16) {  // packed f16 min/max (NaN ignored, as fminf); NaN flagged from the bits
+      const _Float16 pinf = (_Float16)INFINITY;
+      h2_t mn2 = {pinf, pinf}, mx2 = {-pinf, -pinf};
+      u16x2_t ab = {0, 0};
 #pragma unroll
-    for (int k = 0; k < NCH; ++k) {
-      if (valid(k)) {
-        float x[8];
-        chunk_to_f32<DT>(raw[k], x);
+      for (int k = 0; k < NCH; ++k) {
+        if (valid(k)) {
+          const uint32_t w4[4] = {raw[k].a.x, raw[k].a.y, raw[k].a.z, raw[k].a.w};
 #pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          mn = fminf(mn, x[e]);
-          mx = fmaxf(mx, x[e]);
-          if constexpr (DT != RTKV_F16) anz = fminf(anz, x[e] != 0.f ? __builtin_fabsf(x[e]) : INFINITY);
+          for (int j = 0; j < 4; ++j) {
+            mn2 = __builtin_elementwise_min(mn2, as_h2(w4[j]));
+            mx2 = __builtin_elementwise_max(mx2, as_h2(w4[j]));
+            ab = __builtin_elementwise_max(ab, __builtin_bit_cast(u16x2_t, w4[j] & 0x7fff7fffu));
+          }
+        }
+      }
+      mn = fminf((float)mn2[0], (float)mn2[1]);
+      mx = fmaxf((float)mx2[0], (float)mx2[1]);
+      row_nan = __ballot(ab[0] > 0x7c00 || ab[1] > 0x7c00) != 0ull;
+    } else {
+#pragma unroll
+      for (int k = 0; k < NCH; ++k) {
+        if (valid(k)) {
+          float x[8];
+          chunk_to_f32<DT>(raw[k], x);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            mn = fminf(mn, x[e]);
+            mx = fmaxf(mx, x[e]);
+            anz = fminf(anz, x[e] != 0.f ? __builtin_fabsf(x[e]) : INFINITY);
+          }
         }
       }
     }
@@ -355,6 +428,38 @@ __global__ __launch_bounds__(256, (DT == RTKV_F32 && NCH == 8 && FULL && CONTIG)
         default: process(std::integral_constant<int, 16>{}, ftag); break;  // launcher guarantees w in {2,4,8,16}
       }
     };
+    if constexpr (DT == RTKV_F16) {
+      if (__builtin_amdgcn_readfirstlane((int)(rp.fast && !row_nan))) {
+        const _Float16 zph = (_Float16)rp.zp, sh = (_Float16)rp.scale, qmh = (_Float16)rp.qmaxT;
+        const h2_t zp2 = {zph, zph}, s2 = {sh, sh};
+        auto native = [&](auto wtag, auto dtag) {
+          constexpr int W = decltype(wtag)::value;
+          constexpr bool DEQ = decltype(dtag)::value;
+          const bool aligned = FULL || (((uintptr_t)pk & 15) == 0 && (nch * W) % 16 == 0);
+#pragma unroll
+          for (int k = 0; k < NCH; ++k) {
+            const int c = k * 64 + lane;
+            __builtin_amdgcn_sched_barrier(0);  // keep one chunk's temporaries live at a time
+            if (!valid(k)) continue;
+            uint32_t qi[8], dq[4];
+            f16_chunk_codes<DEQ>(raw[k].a, rp.scale, rp.rcp, zp2, s2, qmh, qi, dq);
+            if (emit_pk) pack_store<W>(pk + c * W, qi, aligned);
+            if constexpr (DEQ) nt_store16(orow + out_off[k], dq[0], dq[1], dq[2], dq[3]);
+          }
+        };
+        auto by_w = [&](auto dtag) {
+          switch (w) {
+            case 2: native(std::integral_constant<int, 2>{}, dtag); break;
+            case 4: native(std::integral_constant<int, 4>{}, dtag); break;
+            case 8: native(std::integral_constant<int, 8>{}, dtag); break;
+            default: native(std::integral_constant<int, 16>{}, dtag); break;
+          }
+        };
+        if (emit_deq) by_w(std::true_type{});
+        else by_w(std::false_type{});
+        continue;
+      }
+    }
     if (__builtin_amdgcn_readfirstlane((int)rp.fast)) by_width(std::true_type{});
     else by_width(std::false_type{});
   }
