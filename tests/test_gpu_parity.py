@@ -464,6 +464,40 @@ def test_native_bhsd_layout_matches_bsf():
     assert torch.equal(outs[0][2], outs[1][2])
 
 
+@pytest.mark.parametrize("dtype", ["float16", "bfloat16", "float32"])
+def test_packed_only_mode_matches_dual_output(dtype):
+    """EMIT_PACKED alone (the packed consumers' mode; fp16 rows take their own code path: packed
+    clamp, no dequantized stores) writes the same codes and scale/zp as the dual-output launch,
+    on ordinary rows, the division-gate edge rows, and rows holding NaN or ±inf."""
+    import rtkv
+    from rtkv import _lib as L
+    F, S = 4096, 512
+    K, V = synth.kv(21, 1, S, F, "float32")
+    edge = synth.to_f32(_division_edge_rows(dtype, F), dtype)[0]
+    K[0, 1:1 + edge.shape[0]] = edge
+    V[0, 40:40 + edge.shape[0]] = edge[::-1]
+    K[0, 30, ::97] = np.nan
+    K[0, 31, 5] = np.inf
+    V[0, 32, 7] = -np.inf
+    V[0, 33, ::3] = np.nan
+    W = synth.attention_slice(21, 1, 8, S, rtkv.prompt_length(S), dtype)
+    Kd, Vd, Wd = dev(synth.cast(K, dtype), dtype), dev(synth.cast(V, dtype), dtype), dev(W, dtype)
+    cfg = config(COVERAGE, 4)
+    P = rtkv.prompt_length(S)
+    got = []
+    for flags, deq in ((L.EMIT_DEQUANT | L.EMIT_PACKED, True), (L.EMIT_PACKED, False)):
+        p = rtkv.params_from_config(cfg, 1, P, 0.8, flags | L.NO_SELECTION)  # every row quantized
+        bufs = rtkv.LayerBuffers(1, S, F, TD[dtype], "cuda", (2, 4, 8), emit_dequant=deq, emit_packed=True)
+        res = rtkv.compress_layer(Kd, Vd, Wd, p, bufs, rtkv.Workspace("cuda"))
+        st = res.stats()
+        n = st.total_packed_bytes
+        got.append((bufs.packed_k[:n].clone(), bufs.packed_v[:n].clone(),
+                    bufs.scale_zp[:, :st.max_kept].clone().view(torch.int32), st.max_kept))
+    assert got[0][3] == got[1][3]
+    for a, b in zip(got[0][:3], got[1][:3]):
+        assert torch.equal(a, b)
+
+
 # ----------------------------------------------------------------------------- full-size properties
 @pytest.mark.parametrize("S,dtype,ratio,H", [(16384, "float16", 0.6, 32), (65536, "float16", 0.4, 32),
                                              (32768, "bfloat16", 0.8, 32),
