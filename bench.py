@@ -25,8 +25,9 @@ same workload.  Extra legs (``--legs``, single GPU, same inputs): ``f16`` (the w
 ``packed_only`` (codes + scale/zp, no dequantized K'/V' — what the packed consumers read) and
 ``drop_in`` (the reference caller's path, RealTimePrefillCompressor.compress_layer_kv_cache with
 its per-layer host sync; ``ttft_ms`` = Σ processing_time as longbench_eval.py:160 defines TTFT) and
-``streams2`` (the main workload with consecutive layers on two streams, so that one layer's
-latency-bound selection overlaps the neighbouring layers' bandwidth-bound kernels).
+``one_stream`` (the main workload with every layer strictly after the previous one; the main line
+runs consecutive layers on ``--streams`` streams, default 2, so that one layer's latency-bound
+selection overlaps its neighbours' bandwidth-bound kernels).
 """
 from __future__ import annotations
 
@@ -57,9 +58,13 @@ def parse():
                     help="K/V/attention dtype (default: the reference model's fp32)")
     ap.add_argument("--no-packed", action="store_true", help="skip the packed-code output")
     ap.add_argument("--no-dequant", action="store_true", help="skip the dequantized K'/V' output (packed only)")
-    ap.add_argument("--legs", default="f16,packed_only,drop_in,streams2",
+    ap.add_argument("--legs", default="f16,packed_only,drop_in,one_stream",
                     help="extra single-GPU legs after the main line: comma list of f16, packed_only, drop_in, "
-                         "streams2 (or 'none')")
+                         "one_stream (or 'none')")
+    ap.add_argument("--streams", type=int, default=2,
+                    help="single GPU: consecutive layers go to this many streams (layer l on stream l %% n, one "
+                         "workspace each), so one layer's latency-bound selection (K2, 16-32 workgroups) "
+                         "overlaps its neighbours' bandwidth-bound kernels; 1 = strictly sequential")
     ap.add_argument("--leg-steps", type=int, default=5)
     ap.add_argument("--cpu-baseline-seconds", type=float, default=12.0,
                     help="CPU work budget of the oracle sample (layers are added until it is spent; 0 = skip)")
@@ -484,18 +489,22 @@ def main():
     else:
         dist = None
         job = Job(args, device, rank, world)
+        job.set_streams(max(1, args.streams))
 
     def barrier():
         if dist is not None:
             dist.barrier()
         torch.cuda.synchronize(device)
 
+    join = getattr(job, "join", lambda: None)
     for _ in range(args.warmup):
         job.step()
+        join()
     barrier()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         job.step()
+        join()
     barrier()
     elapsed = time.perf_counter() - t0
     if dist is not None:
@@ -535,7 +544,8 @@ def main():
                                    f"S={job.S * world} ({job.S}/rank), {args.heads}x{args.head_dim}, {args.dtype}, "
                                    f"P={job.P}, bits 8/4/2, ratios .8/.6/.4, {outs} outputs",
                        "model": "Llama-2-7B (KV shapes only)", "global_batch": 1, "seq_len": job.S * world,
-                       "parallelism": f"sequence-shard x{world}" if world > 1 else "single GPU"},
+                       "parallelism": f"sequence-shard x{world}" if world > 1 else "single GPU",
+                       "layer_streams": 1 if sharded else max(1, args.streams)},
         }
         if sharded:
             line["exchange"] = {"received_bytes_per_rank_per_step": job.exchanged_bytes(),
@@ -563,21 +573,23 @@ def main():
                 if name == "f16" and args.dtype != "float16":
                     inputs = None
                     leg = Job(args, device, rank, world, dtype="float16")
+                    leg.set_streams(max(1, args.streams))
                     legs["f16"] = leg_summary(args, leg, *leg.timed(args.leg_steps, 2))
                     del leg
                 elif name == "packed_only":
                     leg = Job(args, device, rank, world, emit_dequant=False, emit_packed=True, inputs=job.inputs)
+                    leg.set_streams(max(1, args.streams))
                     legs["packed_only"] = leg_summary(args, leg, *leg.timed(args.leg_steps, 2))
                     del leg
-                elif name == "streams2":  # the main workload, consecutive layers on two streams
-                    job.set_streams(2)
-                    ms2, _ = job.timed(args.leg_steps, 2)
+                elif name == "one_stream":  # the main workload with its layers strictly in sequence
                     job.set_streams(1)
+                    ms1, _ = job.timed(args.leg_steps, 2)
+                    job.set_streams(args.streams)
                     tot, _ = job.layer_bytes()
-                    legs["streams2"] = {"value": round(sum(tot) / (ms2 / 1e3) / 1e9, 2), "unit": "GB/s",
-                                        "ms_per_step": round(ms2, 4),
-                                        "path": "layer l on stream l % 2 (one workspace per stream): K2's "
-                                                "16-workgroup latency chain overlaps the other stream's K1/K4"}
+                    legs["one_stream"] = {"value": round(sum(tot) / (ms1 / 1e3) / 1e9, 2), "unit": "GB/s",
+                                          "ms_per_step": round(ms1, 4),
+                                          "path": "every layer on one stream, each layer's K1 -> K2 -> K4 after "
+                                                  "the previous layer's"}
                 elif name == "drop_in":
                     legs["drop_in"] = drop_in_leg(args, job, args.leg_steps, 2)
                     legs["drop_in"]["raw_driver_ms_per_layer"] = round(ms_per_step / args.layers, 4)
