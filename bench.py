@@ -75,6 +75,9 @@ def parse():
                          "(Q + prompt keys + row LSE, K1' on MFMA)")
     ap.add_argument("--sharded", action="store_true",
                     help="use the sequence-sharded driver even at world size 1 (plumbing check)")
+    ap.add_argument("--collectives", default="torch", choices=["torch", "rtkv"],
+                    help="sharded driver: torch.distributed, or the C ABI's RCCL communicators "
+                         "(rtkv_allgather_rows / rtkv_allgather_packed)")
     ap.add_argument("--no-overlap", action="store_true",
                     help="sharded driver: exchange every layer's packed KV after the last layer instead of "
                          "overlapping each layer's exchange with the following layers")
@@ -324,7 +327,8 @@ class ShardedJob:
                                           num_hidden_layers=args.layers)
         self.bits = (2, 4, 8)
         self.comp = ShardedPrefillCompressor(self.cfg, emit_packed=not args.no_packed, emit_dequant=True,
-                                             device=device, overlap=not args.no_overlap)
+                                             device=device, overlap=not args.no_overlap,
+                                             collectives=args.collectives)
         gen = torch.Generator(device=device)
         gen.manual_seed(1234 + 7919 * rank)
         self.inputs, self.params = [], []

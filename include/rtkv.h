@@ -344,6 +344,26 @@ int rtkv_shard_ranges(const int32_t* kept_index_dev, const int64_t* row_offset_d
                       const rtkv_layer_stats* stats_dev, int64_t B, int64_t row_capacity, int64_t S_local,
                       int32_t nranks, int64_t* ranges_dev, void* stream);
 
+/* Shard collectives on RCCL (xGMI), for a host without torch.distributed.  The communicator is
+ * RCCL's (ncclComm_t), created from a 128-byte id that rank 0 makes and the host broadcasts by any
+ * means (rtkv/sharded.py uses its process group).  RCCL is loaded on first use (dlopen
+ * "librccl.so.1"); RTKV_ERR_UNSUPPORTED when it cannot be.  Both exchanges are grouped
+ * point-to-point launches of exact ranges on `stream`, stream-ordered like the kernels.
+ * Replace the torch.distributed calls of rtkv/sharded.py (ShardedPrefillCompressor: the A
+ * all-gather and _send_recv), which have no reference counterpart (the reference is one device). */
+#define RTKV_COMM_ID_BYTES 128
+int rtkv_comm_unique_id(uint8_t* id, size_t id_bytes);
+int rtkv_comm_init(void** comm, const uint8_t* id, size_t id_bytes, int32_t nranks, int32_t rank);
+int rtkv_comm_destroy(void* comm);
+/* Step 2: a_dev[b][j*S_local + i] = rank j's a_local_dev[b][i] on every rank (fp32, B batch rows). */
+int rtkv_allgather_rows(void* comm, const float* a_local_dev, float* a_dev, int64_t B, int64_t S_local,
+                        void* stream);
+/* The end of a layer: rank j's packed K/V bytes [first byte(j), first byte(j+1)) and scale/zp rows
+ * [first row(j), first row(j+1)) of every batch row, from j to every other rank, in place in `out`
+ * (the single-GPU layout).  ranges_host: this layer's rtkv_shard_ranges table copied to the host. */
+int rtkv_allgather_packed(void* comm, const int64_t* ranges_host, int64_t B, int64_t row_capacity,
+                          const rtkv_layer_out* out, void* stream);
+
 /* ------------------------------------------------------------------------------------------------
  * Fused importance mode (MFMA): the aggregation A from Q, K_prompt and the row LSE instead of W.
  * A is fp32 (W is not rounded to the input dtype: the reference model runs in fp32); parity with the

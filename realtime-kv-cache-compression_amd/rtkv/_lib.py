@@ -119,6 +119,11 @@ _SIGS = {
     "rtkv_wait_early": ([c_p, ctypes.c_uint64, c_i64], c_i32),
     "rtkv_host_alloc": ([c_sz], c_p),
     "rtkv_host_free": ([c_p], None),
+    "rtkv_comm_unique_id": ([c_p, c_sz], c_i32),
+    "rtkv_comm_init": ([c_p, c_p, c_sz, c_i32, c_i32], c_i32),
+    "rtkv_comm_destroy": ([c_p], c_i32),
+    "rtkv_allgather_rows": ([c_p, c_p, c_p, c_i64, c_i64, c_p], c_i32),
+    "rtkv_allgather_packed": ([c_p, c_p, c_i64, c_i64, c_p, c_p], c_i32),
     "rtkv_gather_rows": ([c_p, c_i64, c_i64, c_i64, c_p, c_i64, c_i64, c_p, c_i64, c_i64, c_p, c_p], c_i32),
     "rtkv_decode_workspace_size": ([c_i64, c_i64, c_i64, c_i64, c_i64], c_sz),
     "rtkv_decode_attention_packed": ([c_p, c_p, c_i64, c_p, c_p, c_p, c_p, c_i64, c_i64, c_i64, c_p, c_i64, c_i64, c_i32, c_p,

@@ -143,7 +143,7 @@ class ShardedPrefillCompressor:
     rank's own token chunk (it returns the rank's dequantized rows)."""
 
     def __init__(self, config, group=None, stages=None, emit_packed: bool = True, emit_dequant: bool = True,
-                 device=None, overlap: bool = True, lag: int = 2):
+                 device=None, overlap: bool = True, lag: int = 2, collectives: str = "torch"):
         if not dist.is_initialized():
             raise RuntimeError("ShardedPrefillCompressor needs torch.distributed to be initialised")
         self.config = config
@@ -167,6 +167,20 @@ class ShardedPrefillCompressor:
         if self.overlap:
             ranks = dist.get_process_group_ranks(self.group) if self.group is not None else list(range(self.world))
             self.xgroup = dist.new_group(ranks=ranks)
+        # collectives: "torch" (torch.distributed on the group) or "rtkv" (the C ABI's RCCL
+        # communicators: rtkv_allgather_rows for A, rtkv_allgather_packed for the exchange on its own
+        # stream), the path a host binding of include/rtkv.h takes
+        if collectives not in ("torch", "rtkv"):
+            raise ValueError("collectives: 'torch' or 'rtkv'")
+        self.collectives = collectives
+        self.comm = self.xcomm = self._xstream = None
+        if collectives == "rtkv":
+            if self.device.type != "cuda":
+                raise RuntimeError("collectives='rtkv' runs RCCL: it needs ROCm devices")
+            from .comm import RcclComm
+            self.comm = RcclComm.from_group(self.group)
+            self.xcomm = RcclComm.from_group(self.group) if self.emit_packed else None
+            self._xstream = torch.cuda.Stream(self.device)
         self._prompt_keys = {}
         self._queued = []   # (layer_idx, host ranges, event) not yet exchanged
         self._issued = []   # ShardLayer whose exchange is in flight
@@ -253,12 +267,16 @@ class ShardedPrefillCompressor:
         S_total = S_local * self.world
         row0 = self.rank * S_local
         A_local, A_parts, A = self._A_buffers(B, S_local)
-        dist.all_gather_into_tensor(A_parts.view(-1), A_local.view(-1), group=self.group)
-        if B == 1:
-            A_glob = A_parts.view(1, S_total)  # rank-major = token order
-        else:
-            A.copy_(A_parts.permute(1, 0, 2).reshape(B, S_total))
+        if self.comm is not None:
+            self.comm.allgather_rows(A_local, A)  # straight into token order, any B
             A_glob = A
+        else:
+            dist.all_gather_into_tensor(A_parts.view(-1), A_local.view(-1), group=self.group)
+            if B == 1:
+                A_glob = A_parts.view(1, S_total)  # rank-major = token order
+            else:
+                A.copy_(A_parts.permute(1, 0, 2).reshape(B, S_total))
+                A_glob = A
         self.stages.finalize(A_glob, a_dtype, p, bufs)
         self.stages.ranges(bufs, self.world)
         self.stages.quantize(K, V, layout, row0, self.rank, self.world, p, bufs)
@@ -289,7 +307,10 @@ class ShardedPrefillCompressor:
             if ev is not None:
                 ev.synchronize()  # that layer's bounds are on the host (a layer or more ago)
             sl = ShardLayer(layer_idx, self._bufs[layer_idx], host.clone())  # a snapshot: the pinned buffer is reused
-            self._works.extend(self._send_recv(sl, self.xgroup))
+            if self.xcomm is not None:
+                self._rtkv_exchange(sl)
+            else:
+                self._works.extend(self._send_recv(sl, self.xgroup))
             self._issued.append(sl)
 
     def _send_recv(self, sl: ShardLayer, group):
@@ -319,6 +340,14 @@ class ShardedPrefillCompressor:
                         ops.append(dist.P2POp(dist.irecv, buf[lo:hi], peer, group))
         return dist.batch_isend_irecv(ops) if ops else []
 
+    def _rtkv_exchange(self, sl: ShardLayer):
+        """rtkv_allgather_packed on the exchange stream, after the layer's kernels on this stream."""
+        xs = self._xstream
+        xs.wait_stream(torch.cuda.current_stream(self.device))
+        out = sl.bufs.g.out_struct()
+        self.xcomm.allgather_packed(sl.ranges.reshape(-1).contiguous(), sl.bufs.B, sl.bufs.S_total, out,
+                                    stream=xs.cuda_stream)
+
     def exchange(self) -> List[ShardLayer]:
         """Finish the exchange of every layer enqueued so far and return their host views.  Overlapped
         mode: issue the layers still queued, wait for everything in flight.  Otherwise: one host read
@@ -327,6 +356,8 @@ class ShardedPrefillCompressor:
             self._issue(keep=0)
             for w in self._works:
                 w.wait()
+            if self._xstream is not None:
+                torch.cuda.current_stream(self.device).wait_stream(self._xstream)
             out, self._issued, self._works = self._issued, [], []
             return out
         layers = list(self._pending)
@@ -336,6 +367,11 @@ class ShardedPrefillCompressor:
         host = torch.stack([self._bufs[l].ranges for l in layers]).cpu()  # the single sync
         out = [ShardLayer(l, self._bufs[l], host[k]) for k, l in enumerate(layers)]
         if self.world == 1 or not self.emit_packed:
+            return out
+        if self.xcomm is not None:
+            for sl in out:
+                self._rtkv_exchange(sl)
+            torch.cuda.current_stream(self.device).wait_stream(self._xstream)
             return out
         works = []
         for sl in out:  # one grouped launch per layer: every peer pair of the layer at once

@@ -161,3 +161,61 @@ def test_fused_mode_shards_union_equals_single_gpu(dtype, S_total, world, H, Hkv
         assert torch.equal(bufs[j].k_local[:, : r1 - r0], k_ref[:, r0:r1])
         assert torch.equal(bufs[j].v_local[:, : r1 - r0], v_ref[:, r0:r1])
     assert torch.equal(pk[:tot], ref.packed_k[:tot])
+
+
+def test_rtkv_collectives_single_rank():
+    """The C ABI's RCCL path (include/rtkv.h rtkv_comm_* / rtkv_allgather_rows / rtkv_allgather_packed,
+    driven by ShardedPrefillCompressor(collectives='rtkv')) on a one-rank group: the communicator is
+    made from a broadcast id, A goes through rtkv_allgather_rows, the exchange through
+    rtkv_allgather_packed, and the layer equals the single-GPU result byte for byte.  (More ranks need
+    more GPUs: the multi-rank exchange is the one rtkv/sharded.py's torch path runs, over the same
+    rank byte ranges.)"""
+    import os
+    import socket
+    import torch.distributed as dist
+    import rtkv
+    from rtkv.comm import RcclComm
+    from rtkv.sharded import ShardedPrefillCompressor
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    os.environ["MASTER_ADDR"], os.environ["MASTER_PORT"] = "127.0.0.1", str(port)
+    dist.init_process_group("gloo", rank=0, world_size=1)
+    try:
+        comm = RcclComm.from_group()
+        a_local = torch.randn(2, 300, device="cuda")
+        a = torch.full((2, 300), float("nan"), device="cuda")
+        comm.allgather_rows(a_local, a)
+        torch.cuda.synchronize()
+        assert torch.equal(a, a_local)
+        comm.close()
+        S, H, D, dtype = 2048, 8, 64, "float16"
+        F, P = H * D, rtkv.prompt_length(S)
+        K, V = synth.kv(91, 1, S, F, dtype)
+        W = synth.attention_slice(91, 1, H, S, P, dtype)
+        Kd, Vd, Wd = _dev(K, dtype), _dev(V, dtype), _dev(W, dtype)
+        cfg = rtkv.CompressionConfig(alpha=0.8, beta=0.1, gamma=0.1, theta_h=0.4, theta_m=0.25,
+                                     num_hidden_layers=1, layer_weights=[1.0], high_precision_bits=8,
+                                     medium_precision_bits=4, low_precision_bits=2)
+        outs = []
+        for coll in ("torch", "rtkv"):
+            comp = ShardedPrefillCompressor(cfg, collectives=coll, device="cuda")
+            comp.enqueue_layer(Kd, Vd, Wd, 0)
+            (sl,) = comp.exchange()
+            torch.cuda.synchronize()
+            g = sl.bufs.g
+            n, tot = int(sl.ranges[0, -1, 0]), int(sl.ranges[0, -1, 1])
+            outs.append((g.kept_index[:, :n].clone(), g.packed_k[:tot].clone(), g.packed_v[:tot].clone(),
+                         g.scale_zp[:, :n].clone(), sl.bufs.k_local[:, :n].clone()))
+        ref = rtkv.LayerBuffers(1, S, F, Kd.dtype, "cuda", (2, 4, 8))
+        p = comp.params(0, S)
+        res = rtkv.compress_layer(Kd, Vd, Wd, p, ref, rtkv.Workspace("cuda"))
+        st = res.stats()
+        k_ref, _ = res.kv()
+        n, tot = st.max_kept, st.total_packed_bytes
+        want = (ref.kept_index[:, :n], ref.packed_k[:tot], ref.packed_v[:tot], ref.scale_zp[:, :n], k_ref[:, :n])
+        for got in outs:
+            for x, y in zip(got, want):
+                assert torch.equal(x, y)
+    finally:
+        dist.destroy_process_group()
