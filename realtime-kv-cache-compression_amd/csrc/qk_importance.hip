@@ -229,8 +229,13 @@ __global__ __launch_bounds__(256) void qk_importance_kernel(QKArgs g) {
 // the H heads of each row in head order (deterministic) and does K1's epilogue (β·pos, per-block
 // min/max, zeroing).  Against the head-walking kernel above: the keys are staged once per
 // workgroup instead of once per head, and 8-16 waves per CU keep queries in flight.
+// 4 waves per SIMD: the register budget becomes 128 (no AGPR accumulators, no spills) and 16 waves
+// per CU keep their next query tiles in flight (3 waves per SIMD without the bound: 159 registers).
+#ifndef QK_HEAD_WPE
+#define QK_HEAD_WPE 4
+#endif
 template <int DT, int NT, int KS>
-__global__ __launch_bounds__(256) void qk_head_kernel(QKArgs g, float* __restrict__ part, int rpw) {
+__global__ __launch_bounds__(256, QK_HEAD_WPE) void qk_head_kernel(QKArgs g, float* __restrict__ part, int rpw) {
   using FT = typename Frag<DT>::T;
   using S_ = typename Dt<DT>::S;
   constexpr int D = 32 * KS;
