@@ -57,8 +57,12 @@ __device__ __forceinline__ void lds_dma16(const void* g, void* lds_base) {
   __builtin_amdgcn_global_load_lds(g, (__attribute__((address_space(3))) void*)lds_base, 16, 0, 0);
 }
 
+// One row group per wave fits 96 registers: 5 waves per SIMD (4 without the bound, at 98).
+#ifndef LSE_WPE
+#define LSE_WPE 5
+#endif
 template <int DT, int KS, int RG>
-__global__ __launch_bounds__(256) void attn_lse_kernel(LseArgs g) {
+__global__ __launch_bounds__(256, RG == 1 ? LSE_WPE : 1) void attn_lse_kernel(LseArgs g) {
   constexpr int kLRows = 64 * RG;            // query rows per workgroup (4 waves × RG groups of 16)
   using FT = typename LFrag<DT>::T;
   using S_ = typename Dt<DT>::S;
@@ -115,9 +119,28 @@ __global__ __launch_bounds__(256) void attn_lse_kernel(LseArgs g) {
       m[rg][r] = kLFloor;  // finite: exp2(-inf − m) = 0 and no −inf − (−inf)
       l[rg][r] = 0.f;
     }
-  // running (max, sum) update with the logits of tile kt: mask keys past S and (causal) past the
-  // query position (edge tiles only), then one FMA + exp2 + add per logit in the exp2 domain
-  auto update = [&](f32x4 (&acc)[RG][4], int kt) {
+  // Software pipeline: the MFMAs of key tile kt+1 are issued in the same basic block as tile kt's
+  // exp2 sums (independent registers), and sched_group_barrier interleaves them — 1 LDS read, 1 MFMA,
+  // 4 VALU — so the matrix core and the VALU work at once inside each wave.
+  auto mfma_tile = [&](int kt, f32x4 (&acc)[RG][4]) {
+    const uint8_t* st = lds + (kt & 1) * TILE;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+#pragma unroll
+      for (int rg = 0; rg < RG; ++rg) acc[rg][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+      const int kr = 16 * t + c16;
+      const uint8_t* krow = st + kr * RB;
+#pragma unroll
+      for (int s_ = 0; s_ < KS; ++s_) {
+        const FT bf = *reinterpret_cast<const FT*>(krow + (((4 * s_ + kg) ^ (kr & (CH - 1))) * 16));
+#pragma unroll
+        for (int rg = 0; rg < RG; ++rg) acc[rg][t] = LFrag<DT>::mfma(a[rg][s_], bf, acc[rg][t]);
+      }
+    }
+  };
+  // tile kt's logits: mask keys past S and (causal) past the query position (edge tiles only), raise
+  // the running max when a logit passes it by 8 (one wave-uniform branch)
+  auto prepare = [&](f32x4 (&acc)[RG][4], int kt) {
     bool up = false;
     float mt[RG][4];
 #pragma unroll
@@ -151,6 +174,8 @@ __global__ __launch_bounds__(256) void attn_lse_kernel(LseArgs g) {
           m[rg][r] = mn;
         }
     }
+  };
+  auto exp_sum = [&](const f32x4 (&acc)[RG][4]) {
 #pragma unroll
     for (int rg = 0; rg < RG; ++rg)
 #pragma unroll
@@ -160,32 +185,42 @@ __global__ __launch_bounds__(256) void attn_lse_kernel(LseArgs g) {
         for (int t = 0; t < 4; ++t) l[rg][r] += __builtin_amdgcn_exp2f(__builtin_fmaf(acc[rg][t][r], sc, nm));
       }
   };
+  f32x4 acc[RG][4], accn[RG][4];
   issue(0);
+  if (ntiles > 1) {
+    issue(1);
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(KI) : "memory");
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __builtin_amdgcn_s_barrier();  // every wave's pieces of tile 0
+  mfma_tile(0, acc);
   for (int kt = 0; kt < ntiles; ++kt) {
-    __builtin_amdgcn_s_barrier();  // every wave is done with tile kt-1: its slot is free
+    prepare(acc, kt);
     if (kt + 1 < ntiles) {
-      issue(kt + 1);
-      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(KI) : "memory");
-    } else {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    __builtin_amdgcn_s_barrier();  // ... and every other wave's pieces of tile kt
-    const uint8_t* st = lds + (kt & 1) * TILE;
-    f32x4 acc[RG][4];
-#pragma unroll
-    for (int t = 0; t < 4; ++t) {
-#pragma unroll
-      for (int rg = 0; rg < RG; ++rg) acc[rg][t] = f32x4{0.f, 0.f, 0.f, 0.f};
-      const int kr = 16 * t + c16;
-      const uint8_t* krow = st + kr * RB;
-#pragma unroll
-      for (int s_ = 0; s_ < KS; ++s_) {
-        const FT bf = *reinterpret_cast<const FT*>(krow + (((4 * s_ + kg) ^ (kr & (CH - 1))) * 16));
-#pragma unroll
-        for (int rg = 0; rg < RG; ++rg) acc[rg][t] = LFrag<DT>::mfma(a[rg][s_], bf, acc[rg][t]);
+      __builtin_amdgcn_s_barrier();  // every wave has read tile kt (its MFMAs are issued): slot kt&1 is free
+      if (kt + 2 < ntiles) {
+        issue(kt + 2);
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(KI) : "memory");
+      } else {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       }
+      __builtin_amdgcn_s_barrier();  // ... and every wave's pieces of tile kt+1 landed
+      mfma_tile(kt + 1, accn);
+      exp_sum(acc);
+#pragma unroll
+      for (int i = 0; i < 4 * KS * RG; ++i) {
+        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // 1 LDS read
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // 1 MFMA
+        __builtin_amdgcn_sched_group_barrier(0x002, 4, 0);  // 4 VALU
+      }
+#pragma unroll
+      for (int rg = 0; rg < RG; ++rg)
+#pragma unroll
+        for (int t = 0; t < 4; ++t) acc[rg][t] = accn[rg][t];
+    } else {
+      exp_sum(acc);
     }
-    update(acc, kt);
   }
   // combine the 16 lanes holding each row: M = max m, L = Σ l·2^(m − M); lse = (M + log2 L)·ln 2
 #pragma unroll
