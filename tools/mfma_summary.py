@@ -21,7 +21,7 @@ SIMDS, XCDS = 1024, 8
 def load(path):
     per = collections.defaultdict(dict)
     for r in csv.DictReader(open(path)):
-        if "rtkv" not in r["Kernel_Name"] or not any(k in r["Kernel_Name"] for k in ("attn_lse", "qk_importance")):
+        if "rtkv" not in r["Kernel_Name"] or not any(k in r["Kernel_Name"] for k in ("attn_lse", "qk_importance", "qk_head")):
             continue
         d = per[(r["Kernel_Name"], r["Grid_Size"], r["Dispatch_Id"])]
         d[r["Counter_Name"]] = float(r["Counter_Value"])
