@@ -349,12 +349,27 @@ __global__ __launch_bounds__(256) void qk_head_reduce_kernel(const float* __rest
   __shared__ float red[2][4];
   zero_regions(ex);
   const int b = blockIdx.y;
-  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   float mn = INFINITY, mx = -INFINITY;
   if (i < S) {
     const float* pp = part + (int64_t)b * H * S + i;
     float s = 0.f;
-    for (int64_t h = 0; h < H; ++h) s += pp[h * S];
+    int64_t h = 0;
+    for (; h + 32 <= H; h += 32) {  // 32 loads in flight, summed in head order
+      float v[32];
+#pragma unroll
+      for (int j = 0; j < 32; ++j) v[j] = __builtin_nontemporal_load(pp + (h + j) * S);
+#pragma unroll
+      for (int j = 0; j < 32; ++j) s += v[j];
+    }
+    for (; h + 8 <= H; h += 8) {
+      float v[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = __builtin_nontemporal_load(pp + (h + j) * S);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) s += v[j];
+    }
+    for (; h < H; ++h) s += pp[h * S];
     const float Ai = s / (float)H;
     A[(int64_t)b * S + i] = Ai;
     if (ex.t2 && b == 0) {
@@ -370,8 +385,10 @@ __global__ __launch_bounds__(256) void qk_head_reduce_kernel(const float* __rest
     if (lane == 0) { red[0][wave] = mn; red[1][wave] = mx; }
     __syncthreads();
     if (threadIdx.x == 0) {
-      ex.part[((int64_t)b * gridDim.x + blockIdx.x) * 2] = fminf(fminf(red[0][0], red[0][1]), fminf(red[0][2], red[0][3]));
-      ex.part[((int64_t)b * gridDim.x + blockIdx.x) * 2 + 1] = fmaxf(fmaxf(red[1][0], red[1][1]), fmaxf(red[1][2], red[1][3]));
+      float a = red[0][0], z = red[1][0];
+      for (int w = 1; w < (int)(blockDim.x >> 6); ++w) { a = fminf(a, red[0][w]); z = fmaxf(z, red[1][w]); }
+      ex.part[((int64_t)b * gridDim.x + blockIdx.x) * 2] = a;
+      ex.part[((int64_t)b * gridDim.x + blockIdx.x) * 2 + 1] = z;
     }
   }
 }
@@ -390,9 +407,10 @@ static int launch_qk_head(const QKArgs& a, float* part, hipStream_t st, int* npa
   const dim3 grid((unsigned)((S + 4 * rpw - 1) / (4 * rpw)), (unsigned)a.q.H, (unsigned)a.q.B);
   hipLaunchKernelGGL((qk_head_kernel<DT, NT, KS>), grid, dim3(256), lds, st, a, part, rpw);
   RTKV_HIP_CHECK(hipGetLastError());
-  const dim3 rgrid((unsigned)((S + 255) / 256), (unsigned)a.q.B);
+  // one wave per 64 tokens: every token's H loads in flight at once, over S/64 CUs
+  const dim3 rgrid((unsigned)((S + 63) / 64), (unsigned)a.q.B);
   if (nparts) *nparts = (int)rgrid.x;
-  hipLaunchKernelGGL(qk_head_reduce_kernel, rgrid, dim3(256), 0, st, part, a.q.H, S, a.A, a.ex);
+  hipLaunchKernelGGL(qk_head_reduce_kernel, rgrid, dim3(64), 0, st, part, a.q.H, S, a.A, a.ex);
   RTKV_HIP_CHECK(hipGetLastError());
   return RTKV_OK;
 }
