@@ -291,13 +291,24 @@ __global__ __launch_bounds__(256, (DT == RTKV_F32 && NCH == 8 && FULL && CONTIG)
   const int F = (int)(a.kv.H * a.kv.D);
   const int nch = FULL ? NCH * 64 : (F + 7) >> 3;
   const int cap = (int)a.out.row_capacity;
-  int R = a.kept_index ? (int)a.stats->max_kept : S;  // rows per batch row
-  if (R > cap) R = cap;
-  const int tasks = 2 * B * R;
+  // One batch row (every single-GPU reference configuration): a task's kept count, token index and
+  // class are independent loads, issued together — one round trip before the row loads instead of
+  // stats → batch row → index.  Rows past the kept count do not exist for B = 1 (no padding rows).
+  const bool one_row = B == 1;
+  int R = S;  // rows per batch row (B > 1: the runtime maximum, padding rows below it)
+  int64_t osb = 0;
+  int tasks;
+  if (one_row) {
+    tasks = 2 * (a.kept_index ? (cap < S ? cap : S) : S);
+  } else {
+    R = a.kept_index ? (int)a.stats->max_kept : S;
+    if (R > cap) R = cap;
+    tasks = 2 * B * R;
+    osb = a.out.o_stride_b >= 0 ? a.out.o_stride_b : (int64_t)R * a.out.o_stride_s;
+  }
   const rtkv_batch_stats* bst = a.stats ? reinterpret_cast<const rtkv_batch_stats*>(a.stats + 1) : nullptr;
   const bool emit_deq = a.out.k_out_dev != nullptr;
   const bool emit_pk = a.out.packed_k_dev != nullptr;
-  const int64_t osb = a.out.o_stride_b >= 0 ? a.out.o_stride_b : (int64_t)R * a.out.o_stride_s;
   // per-lane in-row offsets of each chunk (task independent)
   int in_off[NCH], out_off[NCH];
 #pragma unroll
@@ -317,10 +328,24 @@ __global__ __launch_bounds__(256, (DT == RTKV_F32 && NCH == 8 && FULL && CONTIG)
   for (int t = blockIdx.x * (blockDim.x >> 6) + wave; t < tasks; t += nw) {
     const int which = t & 1;
     const int rr = t >> 1;
-    const int b = rr / R, r = rr - b * R;
-    const int kept_b = a.kept_index ? (int)bst[b].kept : S;
-    int i = (r < kept_b) ? (a.kept_index ? a.kept_index[(int64_t)b * cap + r] : r) : 0;
-    int lab = (r < kept_b) ? (a.row_label ? (int)a.row_label[(int64_t)b * cap + r] : (int)a.labels[(int64_t)b * S + i]) : 0;
+    int b, r, kept_b, i, lab;
+    if (one_row) {
+      b = 0;
+      r = rr;
+      const int rs = r < cap ? r : cap - 1;
+      const int i_s = a.kept_index ? a.kept_index[rs] : r;
+      const int l_s = a.row_label ? (int)a.row_label[rs] : 0;
+      kept_b = a.kept_index ? (int)bst[0].kept : S;
+      if (r >= kept_b) continue;
+      i = i_s;
+      lab = a.row_label ? l_s : (int)a.labels[i];
+    } else {
+      b = rr / R;
+      r = rr - b * R;
+      kept_b = a.kept_index ? (int)bst[b].kept : S;
+      i = (r < kept_b) ? (a.kept_index ? a.kept_index[(int64_t)b * cap + r] : r) : 0;
+      lab = (r < kept_b) ? (a.row_label ? (int)a.row_label[(int64_t)b * cap + r] : (int)a.labels[(int64_t)b * S + i]) : 0;
+    }
     i = __builtin_amdgcn_readfirstlane(i);
     lab = __builtin_amdgcn_readfirstlane(lab);
     // shard: skip another rank's token; padding rows' zero scale/zp are written by every rank (the
