@@ -195,17 +195,18 @@ __global__ __launch_bounds__(256) void aggregation_vec_kernel(const typename Dt<
 // HB heads per load batch; PF: the next batch's loads are issued before the current batch is
 // summed (two batches in flight, so every wave keeps streaming).  The per-element addition order is
 // the same for every (HB, PF): heads in order, the cascade step after every 16th head.
-template <int DT, int CPR, int HB = 16, bool PF = false>
-__global__ __launch_bounds__(256) void aggregation_shfl_kernel(const typename Dt<DT>::S* __restrict__ W, int H,
+template <int DT, int CPR, int HB = 16, bool PF = false, int BT = 256>
+__global__ __launch_bounds__(BT) void aggregation_shfl_kernel(const typename Dt<DT>::S* __restrict__ W, int H,
                                                                int64_t S, int64_t sb, int64_t sh, int64_t ss,
                                                                int64_t lim, float* __restrict__ A, AggExtras ex) {
   using S_ = typename Dt<DT>::S;
   using V = uint4;
   constexpr int P = 8 * CPR;
-  constexpr int TT = 256 / CPR;  // tokens per block
+  constexpr int TT = BT / CPR;   // tokens per block
   constexpr int NV = CPR / 2;    // 16-column groups
   constexpr int NQ = NV / 4;
-  __shared__ float red[2][4];
+  constexpr int NW = BT / 64;
+  __shared__ float red[2][NW];
   zero_regions(ex);
   const int b = blockIdx.y;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -330,8 +331,11 @@ __global__ __launch_bounds__(256) void aggregation_shfl_kernel(const typename Dt
     if (lane == 0) { red[0][wave] = mn; red[1][wave] = mx; }
     __syncthreads();
     if (threadIdx.x == 0) {
-      ex.part[((int64_t)b * gridDim.x + blockIdx.x) * 2] = fminf(fminf(red[0][0], red[0][1]), fminf(red[0][2], red[0][3]));
-      ex.part[((int64_t)b * gridDim.x + blockIdx.x) * 2 + 1] = fmaxf(fmaxf(red[1][0], red[1][1]), fmaxf(red[1][2], red[1][3]));
+      float lo = red[0][0], hi = red[1][0];
+#pragma unroll
+      for (int w2 = 1; w2 < NW; ++w2) { lo = fminf(lo, red[0][w2]); hi = fmaxf(hi, red[1][w2]); }
+      ex.part[((int64_t)b * gridDim.x + blockIdx.x) * 2] = lo;
+      ex.part[((int64_t)b * gridDim.x + blockIdx.x) * 2 + 1] = hi;
     }
   }
 }
@@ -343,16 +347,17 @@ __global__ __launch_bounds__(256) void aggregation_shfl_kernel(const typename Dt
 //   part_k[l] = Σ_j x[8(4j+k) + l]   (j = 0..NV/4-1 sequential from 0, k = 0..3)   row_sum ilp 4
 //   lane[l]   = part_0 + part_1 + part_2 + part_3, A = Σ_l lane[l] (l = 0..7)      vectorized_inner_sum
 // Chunk ch < 8 holds part_{ch/2}[(ch%2)*4 + e] after the first step; chunk 0 folds.
-template <int CPR, int HB = 16>
-__global__ __launch_bounds__(256) void aggregation_shfl32_kernel(const float* __restrict__ W, int H, int64_t S,
+template <int CPR, int HB = 16, int BT = 256>
+__global__ __launch_bounds__(BT) void aggregation_shfl32_kernel(const float* __restrict__ W, int H, int64_t S,
                                                                  int64_t sb, int64_t sh, int64_t ss, int64_t lim,
                                                                  float* __restrict__ A, AggExtras ex) {
   constexpr int P = 4 * CPR;
-  constexpr int TT = 256 / CPR;  // tokens per block
+  constexpr int TT = BT / CPR;   // tokens per block
   constexpr int NV = CPR / 2;    // 8-column vectors
   constexpr int NQ = NV / 4;
+  constexpr int NW = BT / 64;
   static_assert(NV % 4 == 0 && CPR <= 64, "aggregation_shfl32: CPR must be a multiple of 8, at most 64");
-  __shared__ float red[2][4];
+  __shared__ float red[2][NW];
   zero_regions(ex);
   const int b = blockIdx.y;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -451,8 +456,11 @@ __global__ __launch_bounds__(256) void aggregation_shfl32_kernel(const float* __
     if (lane == 0) { red[0][wave] = mn; red[1][wave] = mx; }
     __syncthreads();
     if (threadIdx.x == 0) {
-      ex.part[((int64_t)b * gridDim.x + blockIdx.x) * 2] = fminf(fminf(red[0][0], red[0][1]), fminf(red[0][2], red[0][3]));
-      ex.part[((int64_t)b * gridDim.x + blockIdx.x) * 2 + 1] = fmaxf(fmaxf(red[1][0], red[1][1]), fmaxf(red[1][2], red[1][3]));
+      float lo = red[0][0], hi = red[1][0];
+#pragma unroll
+      for (int w2 = 1; w2 < NW; ++w2) { lo = fminf(lo, red[0][w2]); hi = fmaxf(hi, red[1][w2]); }
+      ex.part[((int64_t)b * gridDim.x + blockIdx.x) * 2] = lo;
+      ex.part[((int64_t)b * gridDim.x + blockIdx.x) * 2 + 1] = hi;
     }
   }
 }
@@ -545,22 +553,52 @@ static int launch_agg_dt(const rtkv_attn_desc& w, int P, float* A, hipStream_t s
   const int H = (int)w.H;
   if constexpr (DT != RTKV_F32) {
     if (aligned && P == 128) {  // register path (Llama prompts: P = 128)
-      dim3 grid((unsigned)((w.S + 15) / 16), (unsigned)w.B);
-      if (x.nparts) *x.nparts = (int)grid.x;
       // 16-head load batches: in the pipeline (after K4's write-back) 29.9 us, against 30.9 us for
-      // 4-head batches with the next one in flight (isolated, tools/k1_grid_probe.hip: 28.7 vs 24.9)
-      hipLaunchKernelGGL((aggregation_shfl_kernel<DT, 16>), grid, dim3(256), 0, st, W, H, w.S, w.stride_b,
-                         w.stride_h, w.stride_s, lim, A, x);
+      // 4-head batches with the next one in flight (isolated, tools/k1_grid_probe.hip: 28.7 vs 24.9).
+      // 1024-thread workgroups: 64 tokens, 16 KB contiguous per head per workgroup (cfg3 fp16 in the
+      // pipeline: 27.8 us against 30.0 for 512 threads and 30.1 for 256).  RTKV_K1_BT16: 256/512/1024.
+      static const int bt = [] {
+        const char* e = getenv("RTKV_K1_BT16");
+        const int v = e ? atoi(e) : 1024;
+        return v == 256 || v == 512 ? v : 1024;
+      }();
+      const int tt = bt / 16;
+      dim3 grid((unsigned)((w.S + tt - 1) / tt), (unsigned)w.B);
+      if (x.nparts) *x.nparts = (int)grid.x;
+      if (bt == 1024)
+        hipLaunchKernelGGL((aggregation_shfl_kernel<DT, 16, 16, false, 1024>), grid, dim3(1024), 0, st, W, H, w.S,
+                           w.stride_b, w.stride_h, w.stride_s, lim, A, x);
+      else if (bt == 512)
+        hipLaunchKernelGGL((aggregation_shfl_kernel<DT, 16, 16, false, 512>), grid, dim3(512), 0, st, W, H, w.S,
+                           w.stride_b, w.stride_h, w.stride_s, lim, A, x);
+      else
+        hipLaunchKernelGGL((aggregation_shfl_kernel<DT, 16>), grid, dim3(256), 0, st, W, H, w.S, w.stride_b,
+                           w.stride_h, w.stride_s, lim, A, x);
       RTKV_HIP_CHECK(hipGetLastError());
       return RTKV_OK;
     }
   } else {
     if (aligned && P == 128 && !getenv("RTKV_K1_LDS")) {  // register path; RTKV_K1_LDS: cross-check knob
-      dim3 grid((unsigned)((w.S + 7) / 8), (unsigned)w.B);
+      // 4 heads per load batch (tools/k1_grid_probe.hip: 46.5 us vs 56 us for 16-head batches at cfg3);
+      // 1024-thread workgroups: 32 tokens, i.e. 16 KB contiguous per head per workgroup (cfg3 in the
+      // pipeline: 47.1 us against 48.6 for 512 threads and 52.8 for 256).  RTKV_K1_BT: 256/512/1024.
+      static const int bt = [] {
+        const char* e = getenv("RTKV_K1_BT");
+        const int v = e ? atoi(e) : 1024;
+        return v == 256 || v == 512 ? v : 1024;
+      }();
+      const int tt = bt / 32;
+      dim3 grid((unsigned)((w.S + tt - 1) / tt), (unsigned)w.B);
       if (x.nparts) *x.nparts = (int)grid.x;
-      // 4 heads per load batch (tools/k1_grid_probe.hip: 46.5 us vs 56 us for 16-head batches at cfg3)
-      hipLaunchKernelGGL((aggregation_shfl32_kernel<32, 4>), grid, dim3(256), 0, st, W, H, w.S, w.stride_b,
-                         w.stride_h, w.stride_s, lim, A, x);
+      if (bt == 1024)
+        hipLaunchKernelGGL((aggregation_shfl32_kernel<32, 4, 1024>), grid, dim3(1024), 0, st, W, H, w.S, w.stride_b,
+                           w.stride_h, w.stride_s, lim, A, x);
+      else if (bt == 512)
+        hipLaunchKernelGGL((aggregation_shfl32_kernel<32, 4, 512>), grid, dim3(512), 0, st, W, H, w.S, w.stride_b,
+                           w.stride_h, w.stride_s, lim, A, x);
+      else
+        hipLaunchKernelGGL((aggregation_shfl32_kernel<32, 4, 256>), grid, dim3(256), 0, st, W, H, w.S, w.stride_b,
+                           w.stride_h, w.stride_s, lim, A, x);
       RTKV_HIP_CHECK(hipGetLastError());
       return RTKV_OK;
     }
