@@ -329,12 +329,14 @@ __global__ __launch_bounds__(256, (DT == RTKV_F32 && NCH == 8 && FULL && CONTIG)
     const int which = t & 1;
     const int rr = t >> 1;
     int b, r, kept_b, i, lab;
+    int64_t roff = -1;  // packed byte offset of the row, fetched with the index when B = 1
     if (one_row) {
       b = 0;
       r = rr;
       const int rs = r < cap ? r : cap - 1;
       const int i_s = a.kept_index ? a.kept_index[rs] : r;
       const int l_s = a.row_label ? (int)a.row_label[rs] : 0;
+      if (emit_pk) roff = a.out.row_offset_dev[rs];
       kept_b = a.kept_index ? (int)bst[0].kept : S;
       if (r >= kept_b) continue;
       i = i_s;
@@ -366,7 +368,7 @@ __global__ __launch_bounds__(256, (DT == RTKV_F32 && NCH == 8 && FULL && CONTIG)
       if (a.out.scale_zp_dev && lane < 2) a.out.scale_zp_dev[sz_idx + lane] = 0.f;
       continue;
     }
-    const int bits = a.bits[lab];
+    const int bits = lab == 0 ? a.bits[0] : (lab == 1 ? a.bits[1] : a.bits[2]);
     const int w = field_width(DT, bits);
     const S_* src = static_cast<const S_*>(which ? a.kv.v_dev : a.kv.k_dev) + b * a.kv.stride_b +
                     (int64_t)(i - row0) * a.kv.stride_s;
@@ -416,8 +418,8 @@ __global__ __launch_bounds__(256, (DT == RTKV_F32 && NCH == 8 && FULL && CONTIG)
     if constexpr (DT != RTKV_F16) anz = wave_min(anz);
     const RowParams rp = row_params<DT>(mn, mx, bits, anz);
     if (a.out.scale_zp_dev && lane < 2) a.out.scale_zp_dev[sz_idx + lane] = lane == 0 ? rp.scale : rp.zp;
-    uint8_t* pk = emit_pk ? (which ? a.out.packed_v_dev : a.out.packed_k_dev) + a.out.row_offset_dev[(int64_t)b * cap + r]
-                          : nullptr;
+    if (emit_pk && !one_row) roff = a.out.row_offset_dev[(int64_t)b * cap + r];
+    uint8_t* pk = emit_pk ? (which ? a.out.packed_v_dev : a.out.packed_k_dev) + roff : nullptr;
     // ---- quantize, pack, dequantize, store (one chunk at a time)
     auto process = [&](auto wtag, auto ftag) {
       constexpr int W = decltype(wtag)::value;
@@ -525,7 +527,7 @@ __global__ __launch_bounds__(256) void quant_rows_generic_kernel(QuantArgs a) {
       if (a.out.scale_zp_dev && lane < 2) a.out.scale_zp_dev[(b * cap + r) * 4 + which * 2 + lane] = 0.f;
       continue;
     }
-    const int bits = a.bits[lab];
+    const int bits = lab == 0 ? a.bits[0] : (lab == 1 ? a.bits[1] : a.bits[2]);
     const int w = field_width(DT, bits);
     const S_* src = static_cast<const S_*>(which ? a.kv.v_dev : a.kv.k_dev) + b * a.kv.stride_b + (i - row0) * a.kv.stride_s;
     auto load = [&](int64_t f) { return Dt<DT>::load(src[(f / D) * a.kv.stride_h + (f % D)]); };
