@@ -421,9 +421,16 @@ __global__ __launch_bounds__(256, (DT == RTKV_F32 && NCH == 8 && FULL && CONTIG)
     if (emit_pk && !one_row) roff = a.out.row_offset_dev[(int64_t)b * cap + r];
     uint8_t* pk = emit_pk ? (which ? a.out.packed_v_dev : a.out.packed_k_dev) + roff : nullptr;
     // ---- quantize, pack, dequantize, store (one chunk at a time)
-    auto process = [&](auto wtag, auto ftag) {
+    // DEQ = false (packed codes only): the code is clamp(rint(t), 0, qmax) as an integer — v_cvt_u32_f32
+    // saturates (negative and -0 -> 0, NaN -> 0, as the float clamp followed by the conversion), then an
+    // integer min with qmax; the fast quotient skips its e == 0 guard (it only keeps the sign of a zero
+    // quotient, which no code sees).  DEQ = true keeps torch.clamp's compare-select (the sign of a zero
+    // and NaN reach the dequantized value).
+    const uint32_t qmaxU = (uint32_t)rp.qmaxT;
+    auto process = [&](auto wtag, auto ftag, auto dtag) {
       constexpr int W = decltype(wtag)::value;
       constexpr bool FASTDIV = decltype(ftag)::value;
+      constexpr bool DEQ = decltype(dtag)::value;
       const bool aligned = FULL || (((uintptr_t)pk & 15) == 0 && (nch * W) % 16 == 0);
 #pragma unroll
       for (int k = 0; k < NCH; ++k) {
@@ -432,27 +439,49 @@ __global__ __launch_bounds__(256, (DT == RTKV_F32 && NCH == 8 && FULL && CONTIG)
         if (!valid(k)) continue;
         float x[8];
         chunk_to_f32<DT>(raw[k], x);
-        float qd[8];
-#pragma unroll
-        for (int e = 0; e < 8; ++e) qd[e] = FASTDIV ? fast_quotient(x[e], rp.scale, rp.rcp) : x[e] / rp.scale;
-        float d[8];
         uint32_t qi[8];
+        if constexpr (DEQ) {
+          float qd[8];
 #pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          const float q = code_from_quotient<DT>(qd[e], rp);
-          d[e] = dequant<DT>(q, rp);
-          qi[e] = (uint32_t)q;
+          for (int e = 0; e < 8; ++e) qd[e] = FASTDIV ? fast_quotient(x[e], rp.scale, rp.rcp) : x[e] / rp.scale;
+          float d[8];
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            const float q = code_from_quotient<DT>(qd[e], rp);
+            d[e] = dequant<DT>(q, rp);
+            qi[e] = (uint32_t)q;
+          }
+          if (emit_pk) pack_store<W>(pk + c * W, qi, aligned);
+          store_chunk_nt<DT>(reinterpret_cast<Chunk<DT>*>(orow + out_off[k]), f32_to_chunk<DT>(d));
+        } else {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            float qd;
+            if constexpr (FASTDIV) {
+              const float q0 = x[e] * rp.rcp;
+              qd = __builtin_fmaf(__builtin_fmaf(-q0, rp.scale, x[e]), rp.rcp, q0);
+            } else {
+              qd = x[e] / rp.scale;
+            }
+            const float t = __builtin_rintf(Dt<DT>::rnd(Dt<DT>::rnd(qd) + rp.zp));
+            uint32_t u;
+            asm("v_cvt_u32_f32 %0, %1" : "=v"(u) : "v"(t));
+            qi[e] = u < qmaxU ? u : qmaxU;
+          }
+          if (emit_pk) pack_store<W>(pk + c * W, qi, aligned);
         }
-        if (emit_pk) pack_store<W>(pk + c * W, qi, aligned);
-        if (emit_deq) store_chunk_nt<DT>(reinterpret_cast<Chunk<DT>*>(orow + out_off[k]), f32_to_chunk<DT>(d));
       }
     };
     auto by_width = [&](auto ftag) {
+      auto go = [&](auto wtag) {
+        if (emit_deq) process(wtag, ftag, std::true_type{});
+        else process(wtag, ftag, std::false_type{});
+      };
       switch (w) {
-        case 2: process(std::integral_constant<int, 2>{}, ftag); break;
-        case 4: process(std::integral_constant<int, 4>{}, ftag); break;
-        case 8: process(std::integral_constant<int, 8>{}, ftag); break;
-        default: process(std::integral_constant<int, 16>{}, ftag); break;  // launcher guarantees w in {2,4,8,16}
+        case 2: go(std::integral_constant<int, 2>{}); break;
+        case 4: go(std::integral_constant<int, 4>{}); break;
+        case 8: go(std::integral_constant<int, 8>{}); break;
+        default: go(std::integral_constant<int, 16>{}); break;  // launcher guarantees w in {2,4,8,16}
       }
     };
     if constexpr (DT == RTKV_F16) {

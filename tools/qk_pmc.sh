@@ -11,6 +11,10 @@ if [ "${PROG:-qk}" = lse ]; then
   CMD="$R/tools/lse_bench.py"
 elif [ "${PROG:-qk}" = k4 ]; then  # K4 at f16, packed codes only
   CMD="$R/bench.py --dtype float16 --no-dequant --layers 4 --steps 2 --warmup 1 --legs none --cpu-baseline-seconds 0 --streams 1"
+elif [ "${PROG:-qk}" = k4f32 ]; then  # K4 at fp32, dequant + packed (the headline workload)
+  CMD="$R/bench.py --layers 4 --steps 2 --warmup 1 --legs none --cpu-baseline-seconds 0 --streams 1"
+elif [ "${PROG:-qk}" = k4f32p ]; then  # K4 at fp32, packed codes only
+  CMD="$R/bench.py --no-dequant --layers 4 --steps 2 --warmup 1 --legs none --cpu-baseline-seconds 0 --streams 1"
 else
   CMD="$R/bench.py --importance qk --dtype float16 --layers 4 --steps 2 --warmup 1 --legs none --cpu-baseline-seconds 0 --streams 1"
 fi
