@@ -26,7 +26,7 @@ same workload.  Extra legs (``--legs``, single GPU, same inputs): ``f16`` (the w
 ``drop_in`` (the reference caller's path, RealTimePrefillCompressor.compress_layer_kv_cache with
 its per-layer host sync; ``ttft_ms`` = Σ processing_time as longbench_eval.py:160 defines TTFT) and
 ``one_stream`` (the main workload with every layer strictly after the previous one; the main line
-runs consecutive layers on ``--streams`` streams, default 3, so that one layer's latency-bound
+runs consecutive layers on ``--streams`` streams, default 4, so that one layer's latency-bound
 selection overlaps its neighbours' bandwidth-bound kernels).
 """
 from __future__ import annotations
@@ -61,7 +61,7 @@ def parse():
     ap.add_argument("--legs", default="f16,packed_only,drop_in,one_stream",
                     help="extra single-GPU legs after the main line: comma list of f16, packed_only, drop_in, "
                          "one_stream (or 'none')")
-    ap.add_argument("--streams", type=int, default=3,
+    ap.add_argument("--streams", type=int, default=4,
                     help="single GPU: consecutive layers go to this many streams (layer l on stream l %% n, one "
                          "workspace each), so one layer's latency-bound selection (K2, 16-32 workgroups) "
                          "overlaps its neighbours' bandwidth-bound kernels; 1 = strictly sequential")
