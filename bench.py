@@ -16,18 +16,20 @@ owns S tokens of an N·S-token prefill; RCCL all-gather of per-token attention m
 selection on every rank, local quantization, RCCL all-gather of the packed KV).
 
 Rank 0 prints ONE JSON line.  ``value`` = algorithmic bytes of the whole job ÷ wall time (GB/s);
-``ttft_ms`` = Σ per-layer compress time of the raw driver;
+``ttft_ms`` = the step's wall time with every layer strictly after the previous one (the reference
+caller's order: layer l+1's K/V come out of attention over layer l's compressed K'/V',
+modified_llama.py:113-157), i.e. Σ per-layer compress time;
 ``roofline`` = the path's HBM-read roofline as the north star defines it (R = 2·S·H·D·e
-+ H·S·P·e bytes per layer over the per-layer time of K1+K2+K4, HIP events on the launch stream);
-``roofline_k4`` = the dominant kernel (K4 quantize+pack+compact) on its own read+write bytes;
++ H·S·P·e bytes per layer over the per-layer time of the layer's kernels, HIP events on the launch
+stream); ``roofline_k4`` = the dominant kernel (quantize+pack+compact) on its own read+write bytes;
 ``cpu_baseline`` = the C oracle (OpenMP restatement of the reference) on a bounded sample of the
-same workload.  Extra legs (``--legs``, single GPU, same inputs): ``f16`` (the workload in fp16),
-``packed_only`` (codes + scale/zp, no dequantized K'/V' — what the packed consumers read) and
-``drop_in`` (the reference caller's path, RealTimePrefillCompressor.compress_layer_kv_cache with
-its per-layer host sync; ``ttft_ms`` = Σ processing_time as longbench_eval.py:160 defines TTFT) and
-``one_stream`` (the main workload with every layer strictly after the previous one; the main line
-runs consecutive layers on ``--streams`` streams, default 4, so that one layer's latency-bound
-selection overlaps its neighbours' bandwidth-bound kernels).
+same workload.  Extra legs (``--legs``, single GPU): ``f16`` (the workload in fp16), ``packed_only``
+(codes + scale/zp, no dequantized K'/V' — what the packed consumers read), ``drop_in`` (the reference
+caller's path, RealTimePrefillCompressor.compress_layer_kv_cache per layer; ``ttft_ms`` = Σ
+processing_time as longbench_eval.py:160 defines TTFT), ``s4096`` / ``s65536`` (the north star's other
+sequence lengths), ``cfg2_s4096_quant`` (BASELINE config 2: S = 4096, quantization only) and
+``independent_layers`` (layers on 4 streams: an upper bound for callers that own several layers'
+inputs at once, not the reference caller's order).
 """
 from __future__ import annotations
 
@@ -58,13 +60,13 @@ def parse():
                     help="K/V/attention dtype (default: the reference model's fp32)")
     ap.add_argument("--no-packed", action="store_true", help="skip the packed-code output")
     ap.add_argument("--no-dequant", action="store_true", help="skip the dequantized K'/V' output (packed only)")
-    ap.add_argument("--legs", default="f16,packed_only,drop_in,one_stream",
+    ap.add_argument("--legs", default="f16,packed_only,drop_in,s4096,cfg2_s4096_quant,s65536,independent_layers",
                     help="extra single-GPU legs after the main line: comma list of f16, packed_only, drop_in, "
-                         "one_stream (or 'none')")
-    ap.add_argument("--streams", type=int, default=4,
+                         "s4096, cfg2_s4096_quant, s65536, independent_layers (or 'none')")
+    ap.add_argument("--streams", type=int, default=1,
                     help="single GPU: consecutive layers go to this many streams (layer l on stream l %% n, one "
-                         "workspace each), so one layer's latency-bound selection (K2, 16-32 workgroups) "
-                         "overlaps its neighbours' bandwidth-bound kernels; 1 = strictly sequential")
+                         "workspace each).  Default 1: strictly sequential, the reference caller's order "
+                         "(layer l+1's K/V come out of attention over layer l's compressed K'/V')")
     ap.add_argument("--leg-steps", type=int, default=5)
     ap.add_argument("--cpu-baseline-seconds", type=float, default=12.0,
                     help="CPU work budget of the oracle sample (layers are added until it is spent; 0 = skip)")
@@ -122,15 +124,20 @@ class Job:
     dtype / emit_dequant / emit_packed override the command line (extra legs); ``inputs`` shares
     another job's resident inputs instead of generating new ones."""
 
-    def __init__(self, args, device, rank, world, dtype=None, emit_dequant=None, emit_packed=None, inputs=None):
+    def __init__(self, args, device, rank, world, dtype=None, emit_dequant=None, emit_packed=None, inputs=None,
+                 seq=None, slots=None, quant_only=False):
+        """seq: tokens (default --seq); slots: distinct input/output sets, layer l uses slot l % slots
+        (bounds the memory of long-sequence legs; default one per layer); quant_only: every token kept
+        (RTKV_NO_SELECTION: BASELINE config 2, quantization without propagation)."""
         import rtkv
         from rtkv import _lib as L
         self.args, self.device, self.rank, self.world = args, device, rank, world
         self.dtype = getattr(torch, dtype or args.dtype)
-        self.S, self.H, self.D = args.seq, args.heads, args.head_dim
+        self.S, self.H, self.D = seq or args.seq, args.heads, args.head_dim
         self.F = self.H * self.D
         self.S_total = self.S * world
         self.P = rtkv.prompt_length(self.S_total)
+        self.quant_only = quant_only
         self.cfg = rtkv.CompressionConfig(alpha=0.8, beta=0.1, gamma=0.1, theta_h=0.4, theta_m=0.25,
                                           high_precision_bits=8, medium_precision_bits=4, low_precision_bits=2,
                                           early_layer_ratio=0.8, middle_layer_ratio=0.6, later_layer_ratio=0.4,
@@ -140,14 +147,16 @@ class Job:
         self.emit_dequant = (not args.no_dequant) if emit_dequant is None else emit_dequant
         if not (self.emit_packed or self.emit_dequant):
             raise SystemExit("--no-packed and --no-dequant together leave nothing to compute")
-        flags = (L.EMIT_DEQUANT if self.emit_dequant else 0) | (L.EMIT_PACKED if self.emit_packed else 0)
+        flags = (L.EMIT_DEQUANT if self.emit_dequant else 0) | (L.EMIT_PACKED if self.emit_packed else 0) | \
+            (L.NO_SELECTION if quant_only else 0)
         prop = rtkv.SelectiveTokenPropagator(self.cfg)
         gen = torch.Generator(device=device)
         gen.manual_seed(1234 + 7919 * rank)
+        self.slots = min(args.layers, slots or args.layers)
         self.inputs = inputs if inputs is not None else []
         self.bufs, self.params = [], []
         for l in range(args.layers):
-            if inputs is None:
+            if inputs is None and l < self.slots:
                 K, V, W = synth_layer(l, self.S, self.H, self.D, self.P, self.dtype, device, gen)
                 if args.importance == "qk":
                     Q, lse = synth_qk(self.S, self.H, self.D, K, self.dtype, device, gen)
@@ -155,9 +164,12 @@ class Job:
                     del W
                 else:
                     self.inputs.append((K, V, W))
-            self.bufs.append(rtkv.LayerBuffers(1, self.S, self.F, self.dtype, device, self.bits,
-                                               emit_dequant=self.emit_dequant, emit_packed=self.emit_packed))
-            self.params.append(rtkv.params_from_config(self.cfg, l, self.P, prop.get_layer_propagation_ratio(l), flags))
+            if l < self.slots:
+                self.bufs.append(rtkv.LayerBuffers(1, self.S, self.F, self.dtype, device, self.bits,
+                                                   emit_dequant=self.emit_dequant, emit_packed=self.emit_packed))
+            ratio = 1.0 if quant_only else prop.get_layer_propagation_ratio(l)
+            self.params.append(rtkv.params_from_config(self.cfg, l, self.P, ratio, flags))
+        self._acct = None
         self.ws = rtkv.Workspace(device)
         self.ws.get(1, self.S)
         # layer pipelining (streams2 leg): layer l runs on stream l % n with that stream's workspace;
@@ -185,31 +197,32 @@ class Job:
             for st in self.streams[1:]:
                 st.wait_stream(main)
         for l in range(self.args.layers):
+            sl = l % self.slots
             if n > 1:
                 st = self.streams[l % n]
                 with torch.cuda.stream(st if st is not None else torch.cuda.current_stream(self.device)):
                     if qk:
-                        K, V, Q, lse = self.inputs[l]
-                        rtkv.compress_layer_qk(K, V, Q, lse, self.params[l], self.bufs[l], self.wss[l % n])
+                        K, V, Q, lse = self.inputs[sl]
+                        rtkv.compress_layer_qk(K, V, Q, lse, self.params[l], self.bufs[sl], self.wss[l % n])
                     else:
-                        K, V, W = self.inputs[l]
-                        rtkv.compress_layer(K, V, W, self.params[l], self.bufs[l], self.wss[l % n])
+                        K, V, W = self.inputs[sl]
+                        rtkv.compress_layer(K, V, W, self.params[l], self.bufs[sl], self.wss[l % n])
                 continue
             if qk:
-                K, V, Q, lse = self.inputs[l]
+                K, V, Q, lse = self.inputs[sl]
                 if events is None:
-                    rtkv.compress_layer_qk(K, V, Q, lse, self.params[l], self.bufs[l], self.ws)
+                    rtkv.compress_layer_qk(K, V, Q, lse, self.params[l], self.bufs[sl], self.ws)
                     continue
                 kd, wd = rtkv.engine.kv_desc(K, V), rtkv.engine.qk_desc(Q, K, lse)
                 fn = L.lib().rtkv_compress_layer_qk_events
             else:
-                K, V, W = self.inputs[l]
+                K, V, W = self.inputs[sl]
                 if events is None:
-                    rtkv.compress_layer(K, V, W, self.params[l], self.bufs[l], self.ws)
+                    rtkv.compress_layer(K, V, W, self.params[l], self.bufs[sl], self.ws)
                     continue
                 kd, wd = rtkv.engine.kv_desc(K, V), rtkv.engine.attn_desc(W)
                 fn = L.lib().rtkv_compress_layer_events
-            out = self.bufs[l].out_struct()
+            out = self.bufs[sl].out_struct()
             out.o_stride_h = kd.D
             ev = (ctypes.c_void_p * 4)(*[e.cuda_event for e in events[l]])
             L.check(fn(ctypes.byref(kd), ctypes.byref(wd), ctypes.byref(self.params[l]), ctypes.byref(out),
@@ -230,14 +243,35 @@ class Job:
         e = self.elem()
         return 2 * self.S * self.F * e + self.H * self.S * self.P * e
 
+    def accounting(self):
+        """(kept rows, packed bytes) of every layer: one untimed pass, each layer's statistics read right
+        after it (slots are reused by later layers)."""
+        if self._acct is None:
+            from rtkv.engine import decode_stats
+            torch.cuda.synchronize(self.device)
+            acct = []
+            for l in range(self.args.layers):
+                self._step_one(l)
+                st = decode_stats(self.bufs[l % self.slots].stats.cpu().numpy().tobytes(), 1)
+                acct.append((st.max_kept, st.total_packed_bytes))
+            self._acct = acct
+        return self._acct
+
+    def _step_one(self, l):
+        import rtkv
+        sl = l % self.slots
+        if self.args.importance == "qk":
+            K, V, Q, lse = self.inputs[sl]
+            rtkv.compress_layer_qk(K, V, Q, lse, self.params[l], self.bufs[sl], self.ws)
+        else:
+            K, V, W = self.inputs[sl]
+            rtkv.compress_layer(K, V, W, self.params[l], self.bufs[sl], self.ws)
+
     def layer_bytes(self):
         """Algorithmic HBM bytes per layer: total and the K4 (quantize+pack+compact) part."""
-        from rtkv.engine import decode_stats
         e = self.elem()
         tot, k4 = [], []
-        for l in range(self.args.layers):
-            st = decode_stats(self.bufs[l].stats.cpu().numpy().tobytes(), 1)
-            Sp, pk = st.max_kept, st.total_packed_bytes
+        for l, (Sp, pk) in enumerate(self.accounting()):
             if self.args.importance == "qk":                     # Q + row LSE + prompt keys
                 w_read = self.H * self.S * self.D * e + 4 * self.H * self.S + self.P * self.F * e
             else:
@@ -575,25 +609,36 @@ def main():
             wanted = [x for x in args.legs.split(",") if x and x != "none"] if args.importance == "w" else []
             for name in wanted:
                 if name == "f16" and args.dtype != "float16":
-                    inputs = None
                     leg = Job(args, device, rank, world, dtype="float16")
-                    leg.set_streams(max(1, args.streams))
                     legs["f16"] = leg_summary(args, leg, *leg.timed(args.leg_steps, 2))
                     del leg
                 elif name == "packed_only":
                     leg = Job(args, device, rank, world, emit_dequant=False, emit_packed=True, inputs=job.inputs)
-                    leg.set_streams(max(1, args.streams))
                     legs["packed_only"] = leg_summary(args, leg, *leg.timed(args.leg_steps, 2))
                     del leg
-                elif name == "one_stream":  # the main workload with its layers strictly in sequence
-                    job.set_streams(1)
-                    ms1, _ = job.timed(args.leg_steps, 2)
-                    job.set_streams(args.streams)
+                elif name == "independent_layers":
+                    # NOT the reference caller's order: consecutive layers on 4 streams (layer l on stream
+                    # l % 4), which only a caller holding several layers' K/V/W at once can do
+                    job.set_streams(4)
+                    ms4, _ = job.timed(args.leg_steps, 2)
+                    job.set_streams(max(1, args.streams))
                     tot, _ = job.layer_bytes()
-                    legs["one_stream"] = {"value": round(sum(tot) / (ms1 / 1e3) / 1e9, 2), "unit": "GB/s",
-                                          "ms_per_step": round(ms1, 4),
-                                          "path": "every layer on one stream, each layer's K1 -> K2 -> K4 after "
-                                                  "the previous layer's"}
+                    legs["independent_layers"] = {
+                        "value": round(sum(tot) / (ms4 / 1e3) / 1e9, 2), "unit": "GB/s", "ms_per_step": round(ms4, 4),
+                        "path": "layer l on stream l % 4 (cross-layer overlap of one layer's selection with its "
+                                "neighbours' kernels; not reachable from the reference's sequential prefill)"}
+                elif name in ("s4096", "cfg2_s4096_quant", "s65536"):
+                    # BASELINE configs: cfg2 (7B, S=4096, quantization only), the north star's S in {4k, 64k}
+                    seq = 65536 if name == "s65536" else 4096
+                    leg = Job(args, device, rank, world, seq=seq, slots=8 if seq > 16384 else None,
+                              quant_only=name.startswith("cfg2"))
+                    legs[name] = leg_summary(args, leg, *leg.timed(args.leg_steps, 2))
+                    legs[name]["seq"] = seq
+                    legs[name]["selection"] = "none (RTKV_NO_SELECTION, every token quantized)" \
+                        if leg.quant_only else ("pipeline K2 (S > 32768)" if seq > 32768 else "one-launch K2")
+                    if leg.slots < args.layers:
+                        legs[name]["inputs"] = f"{leg.slots} distinct layer inputs cycled over {args.layers} layers"
+                    del leg
                 elif name == "drop_in":
                     legs["drop_in"] = drop_in_leg(args, job, args.leg_steps, 2)
                     legs["drop_in"]["raw_driver_ms_per_layer"] = round(ms_per_step / args.layers, 4)

@@ -51,7 +51,12 @@ enum rtkv_error_flag {
   /* A populated class uses a bit width whose qmax = 2^b-1 overflows fp16 (b >= 16).  The reference
    * raises "value cannot be converted to type c10::Half without overflow" at
    * dynamic_quantization.py:121 in that case; the host wrapper raises the same RuntimeError. */
-  RTKV_FLAG_F16_QMAX_OVERFLOW = 1
+  RTKV_FLAG_F16_QMAX_OVERFLOW = 1,
+  /* A cross-workgroup hand-off of the one-launch selection did not arrive within its poll bound
+   * (a workgroup that never became resident, or a withheld hand-off in the test below): the waiting
+   * workgroups gave up, so the layer's outputs are invalid.  The host wrapper raises
+   * RTKV_ERR_TIMEOUT. */
+  RTKV_FLAG_SPIN_TIMEOUT = 2
 };
 
 /* Flags for rtkv_layer_params.flags */
@@ -60,8 +65,11 @@ enum rtkv_layer_flag {
   RTKV_EMIT_PACKED = 2,    /* write bit-packed integer codes + per-row scale/zero-point */
   RTKV_NO_SELECTION = 4,   /* keep every token (quantization only, BASELINE config 2) */
   RTKV_NO_FALLBACK = 8,    /* skip the top-10% emergency fallback (select_tokens_with_budget alone) */
-  RTKV_SELECT_PIPELINE = 16 /* use the multi-workgroup selection pipeline even where the one-workgroup
+  RTKV_SELECT_PIPELINE = 16, /* use the multi-workgroup selection pipeline even where the one-workgroup
                               selection applies (B = 1, S <= 32768); same results, for cross-checks */
+  RTKV_TEST_WITHHOLD_SELECTION = 1 << 16 /* test only: the one-launch selection never publishes its
+                              thresholds, so every waiting workgroup runs into its poll bound and the
+                              layer reports RTKV_FLAG_SPIN_TIMEOUT instead of hanging */
 };
 
 /* ------------------------------------------------------------------------------------------------

@@ -88,6 +88,28 @@ int need_rccl() {
   return RTKV_OK;
 }
 
+// Inside a group: remember the first failing send/recv and keep going, so that the group is always
+// closed (an RCCL group left open on this thread would capture every later RCCL call of the thread).
+struct GroupErr {
+  ncclResult_t r = ncclSuccess;
+  const char* what = nullptr;
+  void note(ncclResult_t x, const char* w) {
+    if (x != ncclSuccess && r == ncclSuccess) { r = x; what = w; }
+  }
+  int close() {  // ncclGroupEnd, then the first error of the group or of the end itself
+    const ncclResult_t e = rccl().group_end();
+    if (r != ncclSuccess) {
+      set_error(std::string(what) + ": " + rccl().error_string(r));
+      return RTKV_ERR_HIP;
+    }
+    if (e != ncclSuccess) {
+      set_error(std::string("ncclGroupEnd: ") + rccl().error_string(e));
+      return RTKV_ERR_HIP;
+    }
+    return RTKV_OK;
+  }
+};
+
 int comm_shape(ncclComm_t c, int* rank, int* nranks) {
   RTKV_RCCL(rccl().user_rank(c, rank));
   RTKV_RCCL(rccl().count(c, nranks));
@@ -143,14 +165,15 @@ int rtkv_allgather_rows(void* comm, const float* a_local_dev, float* a_dev, int6
                                   (size_t)S_local * 4, (size_t)S_local * 4, (size_t)B, hipMemcpyDeviceToDevice, st));
   if (n == 1) return RTKV_OK;
   RTKV_RCCL(rccl().group_start());
+  GroupErr ge;
   for (int64_t b = 0; b < B; ++b)
     for (int j = 0; j < n; ++j) {
       if (j == me) continue;
-      RTKV_RCCL(rccl().send(a_local_dev + b * S_local, (size_t)S_local, ncclFloat32, j, c, st));
-      RTKV_RCCL(rccl().recv(a_dev + b * S_total + (int64_t)j * S_local, (size_t)S_local, ncclFloat32, j, c, st));
+      ge.note(rccl().send(a_local_dev + b * S_local, (size_t)S_local, ncclFloat32, j, c, st), "ncclSend");
+      ge.note(rccl().recv(a_dev + b * S_total + (int64_t)j * S_local, (size_t)S_local, ncclFloat32, j, c, st),
+              "ncclRecv");
     }
-  RTKV_RCCL(rccl().group_end());
-  return RTKV_OK;
+  return ge.close();
 }
 
 int rtkv_allgather_packed(void* comm, const int64_t* ranges_host, int64_t B, int64_t row_capacity,
@@ -171,6 +194,7 @@ int rtkv_allgather_packed(void* comm, const int64_t* ranges_host, int64_t B, int
                        (!out->packed_k_dev || byte(b, n) <= out->packed_capacity),
                    "rtkv_allgather_packed: ranges not ascending or beyond the buffers");
   RTKV_RCCL(rccl().group_start());
+  GroupErr ge;
   for (int64_t b = 0; b < B; ++b)
     for (int j = 0; j < n; ++j) {
       if (j == me) continue;
@@ -185,13 +209,13 @@ int rtkv_allgather_packed(void* comm, const int64_t* ranges_host, int64_t B, int
           char* p = static_cast<char*>(base) + lo * (int64_t)esz;
           return dir == 0 ? rccl().send(p, (size_t)(hi - lo), t, j, c, st) : rccl().recv(p, (size_t)(hi - lo), t, j, c, st);
         };
-        RTKV_RCCL(xfer(out->packed_k_dev, b0, b1, ncclUint8));
-        RTKV_RCCL(xfer(out->packed_v_dev, b0, b1, ncclUint8));
-        RTKV_RCCL(xfer(out->scale_zp_dev, (b * row_capacity + r0) * 4, (b * row_capacity + r1) * 4, ncclFloat32));
+        const char* op = dir == 0 ? "ncclSend" : "ncclRecv";
+        ge.note(xfer(out->packed_k_dev, b0, b1, ncclUint8), op);
+        ge.note(xfer(out->packed_v_dev, b0, b1, ncclUint8), op);
+        ge.note(xfer(out->scale_zp_dev, (b * row_capacity + r0) * 4, (b * row_capacity + r1) * 4, ncclFloat32), op);
       }
     }
-  RTKV_RCCL(rccl().group_end());
-  return RTKV_OK;
+  return ge.close();
 }
 
 }  // extern "C"

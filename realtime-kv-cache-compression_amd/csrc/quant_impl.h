@@ -307,6 +307,8 @@ __global__ __launch_bounds__(256, (DT == RTKV_F32 && NCH == 8 && FULL && CONTIG)
     osb = a.out.o_stride_b >= 0 ? a.out.o_stride_b : (int64_t)R * a.out.o_stride_s;
   }
   const rtkv_batch_stats* bst = a.stats ? reinterpret_cast<const rtkv_batch_stats*>(a.stats + 1) : nullptr;
+  // a selection that timed out (RTKV_FLAG_SPIN_TIMEOUT) left kept_index unwritten: read nothing
+  if (a.stats && (a.stats->error_flags & RTKV_FLAG_SPIN_TIMEOUT)) return;
   const bool emit_deq = a.out.k_out_dev != nullptr;
   const bool emit_pk = a.out.packed_k_dev != nullptr;
   // per-lane in-row offsets of each chunk (task independent)
@@ -340,12 +342,14 @@ __global__ __launch_bounds__(256, (DT == RTKV_F32 && NCH == 8 && FULL && CONTIG)
       kept_b = a.kept_index ? (int)bst[0].kept : S;
       if (r >= kept_b) continue;
       i = i_s;
+      if ((unsigned)i >= (unsigned)S) continue;  // never read outside the layer (corrupt kept_index)
       lab = a.row_label ? l_s : (int)a.labels[i];
     } else {
       b = rr / R;
       r = rr - b * R;
       kept_b = a.kept_index ? (int)bst[b].kept : S;
       i = (r < kept_b) ? (a.kept_index ? a.kept_index[(int64_t)b * cap + r] : r) : 0;
+      if ((unsigned)i >= (unsigned)S) continue;  // never read outside the layer (corrupt kept_index)
       lab = (r < kept_b) ? (a.row_label ? (int)a.row_label[(int64_t)b * cap + r] : (int)a.labels[(int64_t)b * S + i]) : 0;
     }
     i = __builtin_amdgcn_readfirstlane(i);
@@ -536,6 +540,7 @@ __global__ __launch_bounds__(256) void quant_rows_generic_kernel(QuantArgs a) {
   int64_t R = a.kept_index ? a.stats->max_kept : S;
   if (R > cap) R = cap;
   const rtkv_batch_stats* bst = a.stats ? reinterpret_cast<const rtkv_batch_stats*>(a.stats + 1) : nullptr;
+  if (a.stats && (a.stats->error_flags & RTKV_FLAG_SPIN_TIMEOUT)) return;
   const bool emit_deq = a.out.k_out_dev != nullptr;
   const bool emit_pk = a.out.packed_k_dev != nullptr;
   const int64_t osb = a.out.o_stride_b >= 0 ? a.out.o_stride_b : R * a.out.o_stride_s;
@@ -544,6 +549,7 @@ __global__ __launch_bounds__(256) void quant_rows_generic_kernel(QuantArgs a) {
     const int64_t rr = t >> 1, b = rr / R, r = rr - b * R;
     const int64_t kept_b = a.kept_index ? bst[b].kept : S;
     const int64_t i = (r < kept_b) ? (a.kept_index ? a.kept_index[b * cap + r] : r) : 0;
+    if (i < 0 || i >= S) continue;  // never read outside the layer (corrupt kept_index)
     const int lab = (r < kept_b) ? a.labels[b * S + i] : 0;
     if (shard && r < kept_b && (i < row0 || i >= row1)) continue;  // padding rows: as quant_rows_kernel
     const int64_t rloc = a.shard_ranges ? r - a.shard_ranges[(b * (a.shard_nranks + 1) + a.shard_rank) * 2] : r;

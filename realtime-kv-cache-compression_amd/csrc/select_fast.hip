@@ -90,6 +90,8 @@ struct FastArgs {
   int hist_fb;                     // histogram the fallback group too (fallback possible)
   rtkv_early_stats* early;         // host-mapped stats mirror (nullable), published by the selecting workgroup
   uint64_t early_seq;
+  uint32_t spin_limit;             // polls before a hand-off wait gives up (poll_tagged)
+  int withhold;                    // RTKV_TEST_WITHHOLD_SELECTION: never publish the selection words
 };
 
 __device__ __forceinline__ float key_score(uint32_t k) {
@@ -252,13 +254,21 @@ __device__ __forceinline__ rtkv_u32x4 ld16_sc1(const uint32_t* p) {
 }
 
 // Poll tagged words: lanes l < n of the calling wave wait for words[l * stride] to carry kTag and
-// return it (0 for the other lanes).
-__device__ __forceinline__ uint64_t poll_tagged(const uint64_t* words, int stride, int n) {
+// return it (0 for the other lanes).  Bounded: after `limit` polls (≈1 µs each: a coherent load round
+// trip plus s_sleep) a lane gives up with an untagged 0 and RTKV_FLAG_SPIN_TIMEOUT is raised in the
+// layer statistics, so a hand-off that never comes ends the kernel instead of hanging the GPU.
+__device__ __forceinline__ uint64_t poll_tagged(const uint64_t* words, int stride, int n, uint32_t limit,
+                                                rtkv_layer_stats* stats) {
   const int lane = threadIdx.x & (kWave - 1);
   uint64_t w = 0;
   if (lane < n) {
     w = ld_sc1(words + (size_t)lane * stride);
-    while (!(w & kTag)) {
+    for (uint32_t it = 0; !(w & kTag); ++it) {
+      if (it >= limit) {
+        atomicOr(&stats->error_flags, (int)RTKV_FLAG_SPIN_TIMEOUT);
+        w = 0;
+        break;
+      }
       __builtin_amdgcn_s_sleep(1);
       w = ld_sc1(words + (size_t)lane * stride);
     }
@@ -427,7 +437,7 @@ __device__ __forceinline__ void select_thresholds(const FastArgs& g, uint32_t* h
   K2_PROBE(0);
   // ---- every workgroup's class counts (tagged words; their slot lists and sums are complete)
   if (wid == 0) {
-    const uint64_t w = poll_tagged(g.L.head->part, 1, G);
+    const uint64_t w = poll_tagged(g.L.head->part, 1, G, g.spin_limit, a.stats);
     if (lane < G) s_part[lane] = w;
   }
   __syncthreads();
@@ -600,12 +610,14 @@ __device__ __forceinline__ void select_thresholds(const FastArgs& g, uint32_t* h
   for (int q = 0; q < kGrp; ++q) {
     const uint64_t w = kTag | ((uint64_t)(fallback ? 1 : 0) << 50) | ((uint64_t)mode[q] << 48) |
                        ((uint64_t)(need[q] & 0xffff) << 32) | thr[q];
-    st_sc1(&g.L.head->sel[q], w);
+    if (!g.withhold) st_sc1(&g.L.head->sel[q], w);
     s_selw[q] = w;
   }
   const uint64_t m_lo = kTag | (mb & 0xffffffffu), m_hi = kTag | (mb >> 32);
-  st_sc1(&g.L.head->sel[4], m_lo);
-  st_sc1(&g.L.head->sel[5], m_hi);
+  if (!g.withhold) {
+    st_sc1(&g.L.head->sel[4], m_lo);
+    st_sc1(&g.L.head->sel[5], m_hi);
+  }
   s_selw[4] = m_lo;
   s_selw[5] = m_hi;
   // statistics known here; phase 3 adds the kept-token sums (stats zeroed before the launch)
@@ -622,7 +634,7 @@ __device__ __forceinline__ void select_thresholds(const FastArgs& g, uint32_t* h
   if (a.kv_dtype == RTKV_F16)
     for (int q = 0; q < 3; ++q)
       if (ccount[q] > 0 && a.p.bits[q] >= 16) flags |= RTKV_FLAG_F16_QMAX_OVERFLOW;
-  hs->error_flags = flags;
+  if (flags) atomicOr(&hs->error_flags, flags);  // a spin timeout may have been flagged already
   hs->B = 1;
   if (!fallback) {  // the kept counts are the quotas: final here (phase 3 adds only the score sums)
     int64_t n = 0, units = 0, bytes = 0;
@@ -646,14 +658,15 @@ __device__ __forceinline__ void select_thresholds(const FastArgs& g, uint32_t* h
     auto put32 = [](void* dst, uint32_t v) {
       __hip_atomic_store(reinterpret_cast<uint32_t*>(dst), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     };
-    put32(&e->complete, fallback ? 0u : 1u);
-    if (!fallback) {
+    const bool complete = !fallback && !g.withhold;  // withheld: the host takes the synchronised statistics
+    put32(&e->complete, complete ? 1u : 0u);
+    if (complete) {
       put64(&e->stats.max_kept, (uint64_t)bs->kept);
       put64(&e->stats.total_packed_bytes, (uint64_t)bs->packed_bytes);
       put64(&e->stats.score_sum, __builtin_bit_cast(uint64_t, ssum));
       put32(&e->stats.score_min, __builtin_bit_cast(uint32_t, hs->score_min));
       put32(&e->stats.score_max, __builtin_bit_cast(uint32_t, hs->score_max));
-      put32(&e->stats.error_flags, (uint32_t)flags);
+      put32(&e->stats.error_flags, (uint32_t)(flags | ld_sc1(&hs->error_flags)));
       put32(&e->stats.B, 1u);
       for (int q = 0; q < 3; ++q) {
         put64(&e->batch.class_count[q], (uint64_t)ccount[q]);
@@ -719,8 +732,8 @@ __device__ __forceinline__ void compact_phase(const FastArgs& g, float s, int l,
     }
     K2_WG(6);
     // look-back: lane p < blk waits for workgroup p's aggregate
-    const uint64_t w0 = poll_tagged(&g.L.head->agg[0][0], 2, blk);
-    const uint64_t w1 = poll_tagged(&g.L.head->agg[0][1], 2, blk);
+    const uint64_t w0 = poll_tagged(&g.L.head->agg[0][0], 2, blk, g.spin_limit, a.stats);
+    const uint64_t w1 = poll_tagged(&g.L.head->agg[0][1], 2, blk, g.spin_limit, a.stats);
     uint64_t ps = lane < blk ? from11(w0 & ~kTag, 3) : 0ull;
     uint64_t pt = lane < blk ? from11(w1 & ~kTag, 4) : 0ull;
     // ties that predecessor p takes: those of its ties whose row-wide rank is below the quota
@@ -927,7 +940,7 @@ __global__ __launch_bounds__(kST) void fsel_kernel(FastArgs g) {
 #endif
     select_thresholds<TPT>(g, hist_lds, s_selw);
   } else if (wid == 0) {
-    const uint64_t w = poll_tagged(g.L.head->sel, 1, 6);
+    const uint64_t w = poll_tagged(g.L.head->sel, 1, 6, g.spin_limit, a.stats);
     if (lane < 6) s_selw[lane] = w;
   }
   __syncthreads();
@@ -980,6 +993,12 @@ int launch_select_fast(const FinalizeArgs& f, void* ws, bool zeroed, hipStream_t
   g.f = f;
   g.early = f.early;
   g.early_seq = f.early_seq;
+  g.withhold = (f.p.flags & RTKV_TEST_WITHHOLD_SELECTION) ? 1 : 0;
+  static const uint32_t spin_limit = [] {  // RTKV_SPIN_LIMIT: polls per hand-off wait (default ≈ 2 s)
+    const char* e = getenv("RTKV_SPIN_LIMIT");
+    return e ? (uint32_t)strtoul(e, nullptr, 10) : (1u << 21);
+  }();
+  g.spin_limit = spin_limit;
   char* p = static_cast<char*>(ws);
   g.L.head = reinterpret_cast<FastHead*>(p);
   p += sizeof(FastHead);

@@ -164,12 +164,21 @@ class EarlyStatsBuffer:
         self.seq += 1
         return self.seq
 
-    def wait(self, seq: int) -> L.EarlyStats:
+    def _read(self) -> L.EarlyStats:
+        return L.EarlyStats.from_buffer_copy(ctypes.string_at(self.ptr, ctypes.sizeof(L.EarlyStats)))
+
+    def wait(self, seq: int, device=None) -> L.EarlyStats:
+        """The statistics of call `seq` once the device has published them.  A queue slower than the
+        spin timeout (a long backlog, preemption) is not an error: the device that runs the layer is
+        then synchronised and the mirror re-read; only a layer that finished without publishing
+        raises."""
         rc = self._lib.rtkv_wait_early(self.ptr, seq, self.TIMEOUT_US)
         if rc == L.ERR_TIMEOUT:
-            torch.cuda.synchronize()  # surfaces a device fault, if that is what happened
+            torch.cuda.synchronize(device)  # also surfaces a device fault, if that is what happened
+            if self._read().seq == seq:
+                rc = 0
         L.check(rc, "rtkv_wait_early")
-        return L.EarlyStats.from_buffer_copy(ctypes.string_at(self.ptr, ctypes.sizeof(L.EarlyStats)))
+        return self._read()
 
     def __del__(self):
         if getattr(self, "ptr", None):
@@ -201,7 +210,7 @@ class LayerBuffers:
 
     def __init__(self, B: int, S: int, F: int, dtype: torch.dtype, device, bits, emit_dequant=True, emit_packed=True):
         self.B, self.S, self.F, self.dtype = B, S, F, dtype
-        dev = torch.device(device)
+        dev = self.device = torch.device(device)
         esz = torch.tensor([], dtype=dtype).element_size()
         cap = 0
         if emit_packed:
@@ -268,28 +277,44 @@ class LayerResult:
     device's publication — K2's tail and K4 may still be running — and its score_m2 /
     kept_score_sum are NaN; ``final_stats()`` syncs the stream and reads them all."""
 
-    def __init__(self, bufs: LayerBuffers, B: int, early: Optional[EarlyStatsBuffer] = None, seq: int = 0):
+    def __init__(self, bufs: LayerBuffers, B: int, early: Optional[EarlyStatsBuffer] = None, seq: int = 0,
+                 stream: Optional[int] = None):
         self.bufs = bufs
         self.B = B
         self._early, self._seq = early, seq
         self._stats: Optional[LayerStats] = None
         self._final: Optional[LayerStats] = None
+        # the layer's completion on the stream it was launched on: final_stats() waits for exactly that,
+        # whatever stream is current when it is called
+        self.done = torch.cuda.Event()
+        cur = torch.cuda.current_stream(bufs.device)
+        self.done.record(cur if stream is None or stream == cur.cuda_stream
+                         else torch.cuda.ExternalStream(stream, device=bufs.device))
+
+    @staticmethod
+    def _checked(st: LayerStats) -> LayerStats:
+        if st.error_flags & L.FLAG_SPIN_TIMEOUT:
+            raise RuntimeError("rtkv: compress_layer failed (RTKV_ERR_TIMEOUT): a cross-workgroup hand-off of the "
+                               "selection kernel did not arrive within its poll bound; the layer's outputs are "
+                               "invalid (RTKV_FLAG_SPIN_TIMEOUT)")
+        return st
 
     def stats(self) -> LayerStats:
         if self._stats is None:
             if self._early is not None:
-                e = self._early.wait(self._seq)
+                e = self._early.wait(self._seq, self.bufs.device)
                 if e.complete:
-                    self._stats = _early_to_stats(e)
+                    self._stats = self._checked(_early_to_stats(e))
                     return self._stats
             self._stats = self.final_stats()
         return self._stats
 
     def final_stats(self) -> LayerStats:
         if self._final is None:
-            raw = self.bufs.stats.cpu().numpy().tobytes()  # D2H copy on the current stream + sync
+            self.done.synchronize()  # the layer's stream, not whichever stream is current here
+            raw = self.bufs.stats.cpu().numpy().tobytes()
             self._final = decode_stats(raw, self.B)
-        return self._final
+        return self._checked(self._final)
 
     def kv(self):
         """Dequantized (K', V') as contiguous [B, S'_max, F] views (reference return value)."""
@@ -319,11 +344,11 @@ def compress_layer_qk(K, V, Q, lse, params: L.LayerParams, bufs: LayerBuffers, w
                                                   ctypes.byref(out), ws.data_ptr(), ws.numel(), st, early.ptr, seq,
                                                   ctypes.byref(pub))
         L.check(rc, "rtkv_compress_layer_qk_early")
-        return LayerResult(bufs, kd.B, early if pub.value else None, seq)
+        return LayerResult(bufs, kd.B, early if pub.value else None, seq, stream=st)
     rc = L.lib().rtkv_compress_layer_qk(ctypes.byref(kd), ctypes.byref(qd), ctypes.byref(params), ctypes.byref(out),
                                         ws.data_ptr(), ws.numel(), st)
     L.check(rc, "rtkv_compress_layer_qk")
-    return LayerResult(bufs, kd.B)
+    return LayerResult(bufs, kd.B, stream=st)
 
 
 def importance_qk_lse(Q, K, lse, prompt_len: int, causal: bool = True, scale: Optional[float] = None,
@@ -368,8 +393,8 @@ def compress_layer(K, V, W, params: L.LayerParams, bufs: LayerBuffers, workspace
                                                ctypes.byref(out), ws.data_ptr(), ws.numel(), st, early.ptr, seq,
                                                ctypes.byref(pub))
         L.check(rc, "rtkv_compress_layer_early")
-        return LayerResult(bufs, kd.B, early if pub.value else None, seq)
+        return LayerResult(bufs, kd.B, early if pub.value else None, seq, stream=st)
     rc = L.lib().rtkv_compress_layer(ctypes.byref(kd), ctypes.byref(wd), ctypes.byref(params), ctypes.byref(out),
                                      ws.data_ptr(), ws.numel(), st)
     L.check(rc, "rtkv_compress_layer")
-    return LayerResult(bufs, kd.B)
+    return LayerResult(bufs, kd.B, stream=st)

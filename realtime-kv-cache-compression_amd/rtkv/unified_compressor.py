@@ -7,6 +7,7 @@ scores/classes/selection, quantize+pack+compact) with one host synchronisation f
 """
 from __future__ import annotations
 
+import collections
 import os
 import time
 from typing import Dict, List, Optional, Tuple
@@ -30,7 +31,17 @@ class _Lazy:
 
 
 class _LazyDict(dict):
-    """A dict whose _Lazy values are computed on first access (then stored); key order is kept."""
+    """A dict whose _Lazy values are computed on first access (then stored); key order is kept.
+
+    Every read path resolves them: item access, get/values/items, iteration-based copies (dict(d),
+    {**d}, json.dumps, copy, pickle / torch.save: overriding __iter__ takes CPython off the raw-storage
+    fast path), and to_dict() (a plain, recursively resolved dict)."""
+
+    def __iter__(self):
+        return dict.__iter__(self)
+
+    def keys(self):
+        return list(dict.keys(self))
 
     def __getitem__(self, key):
         v = dict.__getitem__(self, key)
@@ -50,6 +61,12 @@ class _LazyDict(dict):
 
     def copy(self):
         return dict(self.items())
+
+    def to_dict(self):
+        return {k: (v.to_dict() if isinstance(v, _LazyDict) else v) for k, v in self.items()}
+
+    def __reduce__(self):
+        return (collections.OrderedDict, (list(self.to_dict().items()),))
 
     def __repr__(self):
         return repr(self.copy())

@@ -115,3 +115,34 @@ def test_drop_in_returns_before_the_layer_finishes_and_stays_correct():
         assert np.allclose(ga["avg_importance"], ra["avg_importance"], rtol=1e-9, atol=0)
         assert np.array_equal(gi["quantization_info"]["bit_assignments"], info["quantization_info"]["bit_assignments"])
     assert a.get_overall_compression_stats()["total_layers_processed"] == 6
+
+
+def test_withheld_selection_times_out_instead_of_hanging():
+    """The one-launch K2's cross-workgroup waits are bounded (select_fast.hip poll_tagged): with the
+    selection words withheld (RTKV_TEST_WITHHOLD_SELECTION) every waiting workgroup gives up after its
+    poll bound, the kernel ends, the statistics carry RTKV_FLAG_SPIN_TIMEOUT and the host raises
+    RTKV_ERR_TIMEOUT — both through the raw driver and through the drop-in (whose early publication is
+    then marked incomplete, so it takes the synchronised statistics).  The next layer is unaffected."""
+    import rtkv
+    from rtkv import _lib as L
+    from rtkv.engine import EarlyStatsBuffer
+    S, H, D, dtype = 4096, 8, 64, "float16"
+    F, P = H * D, rtkv.prompt_length(S)
+    K, V = synth.kv(5, 1, S, F, dtype)
+    W = synth.attention_slice(5, 1, H, S, P, dtype)
+    Kd, Vd, Wd = _dev(K, dtype), _dev(V, dtype), _dev(W, dtype)
+    cfg = rtkv.CompressionConfig(alpha=0.8, beta=0.1, gamma=0.1, theta_h=0.4, theta_m=0.25, num_hidden_layers=1,
+                                 layer_weights=[1.0], high_precision_bits=8, medium_precision_bits=4,
+                                 low_precision_bits=2)
+    ok = rtkv.params_from_config(cfg, 0, P, 0.6, L.EMIT_DEQUANT | L.EMIT_PACKED)
+    bad = rtkv.params_from_config(cfg, 0, P, 0.6, L.EMIT_DEQUANT | L.EMIT_PACKED | L.TEST_WITHHOLD_SELECTION)
+    ws = rtkv.Workspace("cuda")
+    for early in (None, EarlyStatsBuffer()):
+        bufs = rtkv.LayerBuffers(1, S, F, Kd.dtype, "cuda", (2, 4, 8))
+        res = rtkv.compress_layer(Kd, Vd, Wd, bad, bufs, ws, early=early)
+        with pytest.raises(RuntimeError, match="RTKV_ERR_TIMEOUT"):
+            res.stats()
+        torch.cuda.synchronize()
+        good = rtkv.LayerBuffers(1, S, F, Kd.dtype, "cuda", (2, 4, 8))
+        st = rtkv.compress_layer(Kd, Vd, Wd, ok, good, ws, early=early).final_stats()
+        assert st.error_flags == 0 and 0 < st.max_kept < S
