@@ -71,6 +71,9 @@ def parse():
     ap.add_argument("--cpu-baseline-seconds", type=float, default=12.0,
                     help="CPU work budget of the oracle sample (layers are added until it is spent; 0 = skip)")
     ap.add_argument("--cpu-baseline-layers", type=int, default=32, help="at most this many layers in the sample")
+    ap.add_argument("--separate-quant", action="store_true",
+                    help="run the selection and the quantization as two launches (RTKV_SEPARATE_QUANT) instead of "
+                         "the fused selection + quantization launch")
     ap.add_argument("--quiet", action="store_true")
     ap.add_argument("--importance", default="w", choices=["w", "qk"],
                     help="w: the reference's attention-weights input (prompt slice); qk: fused mode "
@@ -148,7 +151,11 @@ class Job:
         if not (self.emit_packed or self.emit_dequant):
             raise SystemExit("--no-packed and --no-dequant together leave nothing to compute")
         flags = (L.EMIT_DEQUANT if self.emit_dequant else 0) | (L.EMIT_PACKED if self.emit_packed else 0) | \
-            (L.NO_SELECTION if quant_only else 0)
+            (L.NO_SELECTION if quant_only else 0) | (L.SEPARATE_QUANT if args.separate_quant else 0)
+        # rtkv_compress_layer runs K2 + K4 as one launch for one batch row of <= 32768 tokens with 4096-element
+        # rows (5120 in fp16/bf16): then the K2 event interval is empty and the fused kernel is the K4 interval
+        self.fused = (not args.separate_quant and self.S <= 32768 and
+                      (self.F == 4096 or (self.F == 5120 and self.dtype != torch.float32)))
         prop = rtkv.SelectiveTokenPropagator(self.cfg)
         gen = torch.Generator(device=device)
         gen.manual_seed(1234 + 7919 * rank)
@@ -475,20 +482,24 @@ def roofline_objects(args, job, kus, k4_bytes):
         traffic = round(sum(v["hbm_bytes"] for v in pmc.values()))
     path = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_source": src,
-            "scope": "path: K1 + K2 + K4 per layer (HIP events on the launch stream)",
+            "scope": "path: every kernel of a layer (K1 + fused K2/K4, or K1 + K2 + K4), HIP events on the launch stream",
             "algorithmic_bytes_per_launch": R,
             "algorithmic_bytes_def": "R = 2*S*H*D*e + H*S*P*e (every K/V element once + W prompt columns; "
                                      "SURVEY §8d, the north star's HBM-read roofline)",
             "avg_launch_us": round(layer_us, 2)}
-    k4_us = kus[2]
-    k4_alg = sum(k4_bytes) / args.layers
+    fused = getattr(job, "fused", False)
+    k4_us = kus[1] + kus[2] if fused else kus[2]
+    k4_alg = sum(k4_bytes) / len(k4_bytes)
     k4_ach = k4_alg / (k4_us / 1e6) / 1e9
     k4_traffic = None
+    name = "fused_kernel" if fused else "quant_rows_kernel"
     if pmc:
-        k4_traffic = next((round(v["hbm_bytes"]) for k, v in pmc.items() if "quant_rows_kernel" in k), None)
+        k4_traffic = next((round(v["hbm_bytes"]) for k, v in pmc.items() if name in k), None)
     k4 = {"bound": "hbm", "achieved": round(k4_ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
           "frac": round(k4_ach / HBM_PEAK_GBS, 4), "traffic": k4_traffic, "traffic_source": src,
-          "algorithmic_bytes_per_launch": round(k4_alg), "kernel": "quant_rows_kernel (K4), read + write bytes",
+          "algorithmic_bytes_per_launch": round(k4_alg),
+          "kernel": ("fused_kernel (K2 selection + K4 quantize/pack/compact in one launch)" if fused else
+                     "quant_rows_kernel (K4)") + ", K4's read + write bytes",
           "avg_launch_us": round(k4_us, 2)}
     return path, k4
 
@@ -499,9 +510,14 @@ def leg_summary(args, job, ms, kus):
     return {"value": round(sum(tot) / (ms / 1e3) / 1e9, 2), "unit": "GB/s", "ms_per_step": round(ms, 4),
             "dtype": {"float16": "f16", "bfloat16": "bf16", "float32": "f32"}[str(job.dtype).split(".")[-1]],
             "outputs": "+".join(x for x, on in (("dequant", job.emit_dequant), ("packed", job.emit_packed)) if on),
-            "kernel_us_per_layer": {"K1_aggregation": round(kus[0], 2), "K2_finalize": round(kus[1], 2),
-                                    "K4_quant_pack": round(kus[2], 2)},
+            "kernel_us_per_layer": kernel_us(job, kus),
             "path_read_roofline_frac": path["frac"], "layer_us": round(sum(kus), 2)}
+
+
+def kernel_us(job, kus):
+    if getattr(job, "fused", False):
+        return {"K1_aggregation": round(kus[0], 2), "K24_fused_select_quant": round(kus[1] + kus[2], 2)}
+    return {"K1_aggregation": round(kus[0], 2), "K2_select": round(kus[1], 2), "K4_quant_pack": round(kus[2], 2)}
 
 
 def main():
@@ -597,8 +613,7 @@ def main():
             path, k4 = roofline_objects(args, job, kus, k4_bytes)
             line["roofline"] = path
             line["roofline_k4"] = k4
-            line["kernel_us_per_layer"] = {"K1_aggregation": round(kus[0], 2), "K2_finalize": round(kus[1], 2),
-                                           "K4_quant_pack": round(kus[2], 2)}
+            line["kernel_us_per_layer"] = kernel_us(job, kus)
             if args.importance == "qk":  # K1' on MFMA: the Q·K_P^T contraction against the dense peak
                 flops = 2.0 * job.H * job.S * job.P * job.D
                 tf = flops / (kus[0] / 1e6) / 1e12

@@ -15,7 +15,8 @@ import subprocess
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-_LIB_PATH = os.path.join(_HERE, "_build", "librtkv_oracle.so")
+# RTKV_ORACLE_LIB: an alternate build of the same source (run_sanitized.sh: the ASan/UBSan one)
+_LIB_PATH = os.environ.get("RTKV_ORACLE_LIB", os.path.join(_HERE, "_build", "librtkv_oracle.so"))
 _lib = None
 
 F32, F16, BF16 = 0, 1, 2

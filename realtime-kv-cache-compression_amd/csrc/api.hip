@@ -173,12 +173,8 @@ int rtkv_select_tokens(const float* scores_dev, const uint8_t* labels_dev, int64
   return launch_select(a, ws.sel, false, (hipStream_t)stream);
 }
 
-static int quantize_rows_impl(const rtkv_kv_desc* kv, const uint8_t* labels_dev, const int32_t* kept_index_dev,
-                              const rtkv_layer_params* p, const rtkv_layer_out* out, void* stream,
-                              const uint8_t* row_label) {
-  int rc = check_params(p);
-  if (rc) return rc;
-  RTKV_REQUIRE(kv && out, "null descriptor");
+static QuantArgs make_quant_args(const rtkv_kv_desc* kv, const uint8_t* labels_dev, const int32_t* kept_index_dev,
+                                 const rtkv_layer_params* p, const rtkv_layer_out* out, const uint8_t* row_label) {
   QuantArgs q;
   std::memset(&q, 0, sizeof(q));
   q.kv = *kv;
@@ -190,7 +186,16 @@ static int quantize_rows_impl(const rtkv_kv_desc* kv, const uint8_t* labels_dev,
   q.out = *out;
   if (!(p->flags & RTKV_EMIT_DEQUANT)) { q.out.k_out_dev = nullptr; q.out.v_out_dev = nullptr; }
   if (!(p->flags & RTKV_EMIT_PACKED)) { q.out.packed_k_dev = nullptr; q.out.packed_v_dev = nullptr; }
-  return launch_quant(q, (hipStream_t)stream);
+  return q;
+}
+
+static int quantize_rows_impl(const rtkv_kv_desc* kv, const uint8_t* labels_dev, const int32_t* kept_index_dev,
+                              const rtkv_layer_params* p, const rtkv_layer_out* out, void* stream,
+                              const uint8_t* row_label) {
+  int rc = check_params(p);
+  if (rc) return rc;
+  RTKV_REQUIRE(kv && out, "null descriptor");
+  return launch_quant(make_quant_args(kv, labels_dev, kept_index_dev, p, out, row_label), (hipStream_t)stream);
 }
 
 int rtkv_quantize_rows(const rtkv_kv_desc* kv, const uint8_t* labels_dev, const int32_t* kept_index_dev,
@@ -282,10 +287,17 @@ static int compress_layer_impl(const rtkv_kv_desc* kv, const rtkv_attn_desc* w, 
     a.early_seq = early_seq;
     if (published) *published = 1;
   }
+  const QuantArgs q = make_quant_args(kv, out->labels_dev, out->kept_index_dev, p, out, row_labels ? ws.labels : nullptr);
+  if (fused_eligible(a, q)) {  // K2 + K4 in one launch (fused.h): events 1 and 2 mark the same point
+    if ((rc = mark(2))) return rc;
+    rc = launch_select_quant_fused(a, ws.sel, q, st);
+    if (rc) return rc;
+    return mark(3);
+  }
   rc = launch_select(a, ws.sel, true, st);
   if (rc) return rc;
   if ((rc = mark(2))) return rc;
-  rc = quantize_rows_impl(kv, out->labels_dev, out->kept_index_dev, p, out, stream, row_labels ? ws.labels : nullptr);
+  rc = launch_quant(q, st);
   if (rc) return rc;
   return mark(3);
 }

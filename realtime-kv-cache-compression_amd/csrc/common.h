@@ -261,6 +261,12 @@ struct QuantArgs {
 };
 int launch_quant(const QuantArgs& a, hipStream_t st);
 
+// K2 + K4 in one launch (fused.h) for B = 1, S <= 32768, contiguous rows of 4096 or 5120 elements
+// (fp32: 4096), packed widths 2/4/8/16.  The selection scratch (select_fast_zero_bytes()) and the
+// statistics must be zero (K1 clears them), and a.T2 must be K1's position term.
+bool fused_eligible(const FinalizeArgs& a, const QuantArgs& q);
+int launch_select_quant_fused(const FinalizeArgs& a, void* sel_ws, const QuantArgs& q, hipStream_t st);
+
 int launch_shard_ranges(const int32_t* kept_index, const int64_t* row_offset, const rtkv_layer_stats* stats, int64_t B,
                         int64_t cap, int64_t S_local, int nranks, int64_t* ranges, hipStream_t st);
 int launch_gather(const void* src, int64_t B, int64_t S, int64_t row_bytes, const int32_t* kept_index, int64_t cap,

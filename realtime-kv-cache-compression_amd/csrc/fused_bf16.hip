@@ -1,0 +1,15 @@
+// fused_bf16.hip — the fused K2 + K4 launch (fused.h) for BF16 K/V rows (its own translation unit so the
+// per-dtype instantiations compile in parallel).
+#include "fused.h"
+
+namespace rtkv {
+
+int launch_fused_bf16(const FinalizeArgs& f, void* sel_ws, const QuantArgs& q, hipStream_t st) {
+  FusedArgs x;
+  x.g = make_fast_args(f, sel_ws);
+  x.g.fused = 1;
+  x.q = q;
+  return launch_fused_kv<RTKV_BF16>(x, (int)((q.kv.H * q.kv.D) / 8), st);
+}
+
+}  // namespace rtkv

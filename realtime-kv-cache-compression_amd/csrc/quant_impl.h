@@ -273,6 +273,164 @@ template <int W> __device__ __forceinline__ void pack_store(uint8_t* dst, const 
   }
 }
 
+// ---- per-row pieces of K4, shared by quant_rows_kernel and the fused selection + quantization kernel
+// (select_fast.hip).  Row geometry: lane l owns 8-element chunks k*64 + l (k < NCH); FULL: all NCH*64
+// chunks exist (F a multiple of 512), else chunk c exists iff c < nch.
+
+// Row min/max (NaN ignored, as fminf/fmaxf), min |x| over nonzero x (bf16/fp32 fast-division gate), and
+// whether the row holds a NaN (fp16 only: its native path must not see one).
+template <int DT, int NCH, bool FULL>
+__device__ __forceinline__ void row_minmax(const Chunk<DT> (&raw)[NCH], int nch, int lane, float& mn, float& mx,
+                                         float& anz, bool& row_nan) {
+  auto valid = [&](int k) { return FULL || (k * 64 + lane) < nch; };
+  mn = INFINITY; mx = -INFINITY; anz = INFINITY;
+  row_nan = false;
+  if constexpr (DT == RTKV_F16) {  // packed f16 min/max (NaN ignored, as fminf); NaN flagged from the bits
+    const _Float16 pinf = (_Float16)INFINITY;
+    h2_t mn2 = {pinf, pinf}, mx2 = {-pinf, -pinf};
+    u16x2_t ab = {0, 0};
+#pragma unroll
+    for (int k = 0; k < NCH; ++k) {
+      if (valid(k)) {
+        const uint32_t w4[4] = {raw[k].a.x, raw[k].a.y, raw[k].a.z, raw[k].a.w};
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          mn2 = __builtin_elementwise_min(mn2, as_h2(w4[j]));
+          mx2 = __builtin_elementwise_max(mx2, as_h2(w4[j]));
+          ab = __builtin_elementwise_max(ab, __builtin_bit_cast(u16x2_t, w4[j] & 0x7fff7fffu));
+        }
+      }
+    }
+    mn = fminf((float)mn2[0], (float)mn2[1]);
+    mx = fmaxf((float)mx2[0], (float)mx2[1]);
+    row_nan = __ballot(ab[0] > 0x7c00 || ab[1] > 0x7c00) != 0ull;
+  } else {
+#pragma unroll
+    for (int k = 0; k < NCH; ++k) {
+      if (valid(k)) {
+        float x[8];
+        chunk_to_f32<DT>(raw[k], x);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          mn = fminf(mn, x[e]);
+          mx = fmaxf(mx, x[e]);
+          anz = fminf(anz, x[e] != 0.f ? __builtin_fabsf(x[e]) : INFINITY);
+        }
+      }
+    }
+  }
+  mn = wave_min(mn);
+  mx = wave_max(mx);
+  if constexpr (DT != RTKV_F16) anz = wave_min(anz);
+}
+
+// Quantize, pack, dequantize and store one row (one chunk at a time): packed codes at pk (w bits per
+// element) and the dequantized row at orow, either output optional.
+template <int DT, int NCH, bool CONTIG, bool FULL>
+__device__ __forceinline__ void emit_row(const Chunk<DT> (&raw)[NCH], const RowParams& rp, bool row_nan, int w,
+                                       typename Dt<DT>::S* orow, const int (&out_off)[NCH], uint8_t* pk, int nch,
+                                       int lane, bool emit_deq, bool emit_pk) {
+  auto valid = [&](int k) { return FULL || (k * 64 + lane) < nch; };
+  // ---- quantize, pack, dequantize, store (one chunk at a time)
+  // DEQ = false (packed codes only): the code is clamp(rint(t), 0, qmax) as an integer — v_cvt_u32_f32
+  // saturates (negative and -0 -> 0, NaN -> 0, as the float clamp followed by the conversion), then an
+  // integer min with qmax; the fast quotient skips its e == 0 guard (it only keeps the sign of a zero
+  // quotient, which no code sees).  DEQ = true keeps torch.clamp's compare-select (the sign of a zero
+  // and NaN reach the dequantized value).
+  const uint32_t qmaxU = (uint32_t)rp.qmaxT;
+  auto process = [&](auto wtag, auto ftag, auto dtag) {
+    constexpr int W = decltype(wtag)::value;
+    constexpr bool FASTDIV = decltype(ftag)::value;
+    constexpr bool DEQ = decltype(dtag)::value;
+    const bool aligned = FULL || (((uintptr_t)pk & 15) == 0 && (nch * W) % 16 == 0);
+#pragma unroll
+    for (int k = 0; k < NCH; ++k) {
+      const int c = k * 64 + lane;
+      __builtin_amdgcn_sched_barrier(0);  // keep one chunk's temporaries live at a time
+      if (!valid(k)) continue;
+      float x[8];
+      chunk_to_f32<DT>(raw[k], x);
+      uint32_t qi[8];
+      if constexpr (DEQ) {
+        float qd[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) qd[e] = FASTDIV ? fast_quotient(x[e], rp.scale, rp.rcp) : x[e] / rp.scale;
+        float d[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const float q = code_from_quotient<DT>(qd[e], rp);
+          d[e] = dequant<DT>(q, rp);
+          qi[e] = (uint32_t)q;
+        }
+        if (emit_pk) pack_store<W>(pk + c * W, qi, aligned);
+        store_chunk_nt<DT>(reinterpret_cast<Chunk<DT>*>(orow + out_off[k]), f32_to_chunk<DT>(d));
+      } else {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          float qd;
+          if constexpr (FASTDIV) {
+            const float q0 = x[e] * rp.rcp;
+            qd = __builtin_fmaf(__builtin_fmaf(-q0, rp.scale, x[e]), rp.rcp, q0);
+          } else {
+            qd = x[e] / rp.scale;
+          }
+          const float t = __builtin_rintf(Dt<DT>::rnd(Dt<DT>::rnd(qd) + rp.zp));
+          uint32_t u;
+          asm("v_cvt_u32_f32 %0, %1" : "=v"(u) : "v"(t));
+          qi[e] = u < qmaxU ? u : qmaxU;
+        }
+        if (emit_pk) pack_store<W>(pk + c * W, qi, aligned);
+      }
+    }
+  };
+  auto by_width = [&](auto ftag) {
+    auto go = [&](auto wtag) {
+      if (emit_deq) process(wtag, ftag, std::true_type{});
+      else process(wtag, ftag, std::false_type{});
+    };
+    switch (w) {
+      case 2: go(std::integral_constant<int, 2>{}); break;
+      case 4: go(std::integral_constant<int, 4>{}); break;
+      case 8: go(std::integral_constant<int, 8>{}); break;
+      default: go(std::integral_constant<int, 16>{}); break;  // launcher guarantees w in {2,4,8,16}
+    }
+  };
+  if constexpr (DT == RTKV_F16) {
+    if (__builtin_amdgcn_readfirstlane((int)(rp.fast && !row_nan))) {
+      const _Float16 zph = (_Float16)rp.zp, sh = (_Float16)rp.scale, qmh = (_Float16)rp.qmaxT;
+      const h2_t zp2 = {zph, zph}, s2 = {sh, sh};
+      auto native = [&](auto wtag, auto dtag) {
+        constexpr int W = decltype(wtag)::value;
+        constexpr bool DEQ = decltype(dtag)::value;
+        const bool aligned = FULL || (((uintptr_t)pk & 15) == 0 && (nch * W) % 16 == 0);
+#pragma unroll
+        for (int k = 0; k < NCH; ++k) {
+          const int c = k * 64 + lane;
+          __builtin_amdgcn_sched_barrier(0);  // keep one chunk's temporaries live at a time
+          if (!valid(k)) continue;
+          uint32_t qi[8], dq[4];
+          f16_chunk_codes<DEQ>(raw[k].a, rp.scale, rp.rcp, zp2, s2, qmh, qi, dq);
+          if (emit_pk) pack_store<W>(pk + c * W, qi, aligned);
+          if constexpr (DEQ) nt_store16(orow + out_off[k], dq[0], dq[1], dq[2], dq[3]);
+        }
+      };
+      auto by_w = [&](auto dtag) {
+        switch (w) {
+          case 2: native(std::integral_constant<int, 2>{}, dtag); break;
+          case 4: native(std::integral_constant<int, 4>{}, dtag); break;
+          case 8: native(std::integral_constant<int, 8>{}, dtag); break;
+          default: native(std::integral_constant<int, 16>{}, dtag); break;
+        }
+      };
+      if (emit_deq) by_w(std::true_type{});
+      else by_w(std::false_type{});
+      return;
+    }
+  }
+  if (__builtin_amdgcn_readfirstlane((int)rp.fast)) by_width(std::true_type{});
+  else by_width(std::false_type{});
+}
+
 // Contiguous fp32 rows of exactly 4096 elements fit 128 VGPRs (4 waves/SIMD); the gate bookkeeping would push the
 // compiler to 129 (3 waves) without the bound.  Wider fp32 rows keep the 256-register budget.
 // Row geometry shared by every task of a launch: element f of a row lives at (f / D) * stride_h + f % D.
@@ -381,147 +539,14 @@ __global__ __launch_bounds__(256, (DT == RTKV_F32 && NCH == 8 && FULL && CONTIG)
 #pragma unroll
     for (int k = 0; k < NCH; ++k)
       if (valid(k)) raw[k] = load_chunk_nt<DT>(src + in_off[k]);
-    float mn = INFINITY, mx = -INFINITY, anz = INFINITY;
-    bool row_nan = false;
-    if constexpr (DT == RTKV_F16) {  // packed f16 min/max (NaN ignored, as fminf); NaN flagged from the bits
-      const _Float16 pinf = (_Float16)INFINITY;
-      h2_t mn2 = {pinf, pinf}, mx2 = {-pinf, -pinf};
-      u16x2_t ab = {0, 0};
-#pragma unroll
-      for (int k = 0; k < NCH; ++k) {
-        if (valid(k)) {
-          const uint32_t w4[4] = {raw[k].a.x, raw[k].a.y, raw[k].a.z, raw[k].a.w};
-#pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            mn2 = __builtin_elementwise_min(mn2, as_h2(w4[j]));
-            mx2 = __builtin_elementwise_max(mx2, as_h2(w4[j]));
-            ab = __builtin_elementwise_max(ab, __builtin_bit_cast(u16x2_t, w4[j] & 0x7fff7fffu));
-          }
-        }
-      }
-      mn = fminf((float)mn2[0], (float)mn2[1]);
-      mx = fmaxf((float)mx2[0], (float)mx2[1]);
-      row_nan = __ballot(ab[0] > 0x7c00 || ab[1] > 0x7c00) != 0ull;
-    } else {
-#pragma unroll
-      for (int k = 0; k < NCH; ++k) {
-        if (valid(k)) {
-          float x[8];
-          chunk_to_f32<DT>(raw[k], x);
-#pragma unroll
-          for (int e = 0; e < 8; ++e) {
-            mn = fminf(mn, x[e]);
-            mx = fmaxf(mx, x[e]);
-            anz = fminf(anz, x[e] != 0.f ? __builtin_fabsf(x[e]) : INFINITY);
-          }
-        }
-      }
-    }
-    mn = wave_min(mn);
-    mx = wave_max(mx);
-    if constexpr (DT != RTKV_F16) anz = wave_min(anz);
+    float mn, mx, anz;
+    bool row_nan;
+    row_minmax<DT, NCH, FULL>(raw, nch, lane, mn, mx, anz, row_nan);
     const RowParams rp = row_params<DT>(mn, mx, bits, anz);
     if (a.out.scale_zp_dev && lane < 2) a.out.scale_zp_dev[sz_idx + lane] = lane == 0 ? rp.scale : rp.zp;
     if (emit_pk && !one_row) roff = a.out.row_offset_dev[(int64_t)b * cap + r];
     uint8_t* pk = emit_pk ? (which ? a.out.packed_v_dev : a.out.packed_k_dev) + roff : nullptr;
-    // ---- quantize, pack, dequantize, store (one chunk at a time)
-    // DEQ = false (packed codes only): the code is clamp(rint(t), 0, qmax) as an integer — v_cvt_u32_f32
-    // saturates (negative and -0 -> 0, NaN -> 0, as the float clamp followed by the conversion), then an
-    // integer min with qmax; the fast quotient skips its e == 0 guard (it only keeps the sign of a zero
-    // quotient, which no code sees).  DEQ = true keeps torch.clamp's compare-select (the sign of a zero
-    // and NaN reach the dequantized value).
-    const uint32_t qmaxU = (uint32_t)rp.qmaxT;
-    auto process = [&](auto wtag, auto ftag, auto dtag) {
-      constexpr int W = decltype(wtag)::value;
-      constexpr bool FASTDIV = decltype(ftag)::value;
-      constexpr bool DEQ = decltype(dtag)::value;
-      const bool aligned = FULL || (((uintptr_t)pk & 15) == 0 && (nch * W) % 16 == 0);
-#pragma unroll
-      for (int k = 0; k < NCH; ++k) {
-        const int c = k * 64 + lane;
-        __builtin_amdgcn_sched_barrier(0);  // keep one chunk's temporaries live at a time
-        if (!valid(k)) continue;
-        float x[8];
-        chunk_to_f32<DT>(raw[k], x);
-        uint32_t qi[8];
-        if constexpr (DEQ) {
-          float qd[8];
-#pragma unroll
-          for (int e = 0; e < 8; ++e) qd[e] = FASTDIV ? fast_quotient(x[e], rp.scale, rp.rcp) : x[e] / rp.scale;
-          float d[8];
-#pragma unroll
-          for (int e = 0; e < 8; ++e) {
-            const float q = code_from_quotient<DT>(qd[e], rp);
-            d[e] = dequant<DT>(q, rp);
-            qi[e] = (uint32_t)q;
-          }
-          if (emit_pk) pack_store<W>(pk + c * W, qi, aligned);
-          store_chunk_nt<DT>(reinterpret_cast<Chunk<DT>*>(orow + out_off[k]), f32_to_chunk<DT>(d));
-        } else {
-#pragma unroll
-          for (int e = 0; e < 8; ++e) {
-            float qd;
-            if constexpr (FASTDIV) {
-              const float q0 = x[e] * rp.rcp;
-              qd = __builtin_fmaf(__builtin_fmaf(-q0, rp.scale, x[e]), rp.rcp, q0);
-            } else {
-              qd = x[e] / rp.scale;
-            }
-            const float t = __builtin_rintf(Dt<DT>::rnd(Dt<DT>::rnd(qd) + rp.zp));
-            uint32_t u;
-            asm("v_cvt_u32_f32 %0, %1" : "=v"(u) : "v"(t));
-            qi[e] = u < qmaxU ? u : qmaxU;
-          }
-          if (emit_pk) pack_store<W>(pk + c * W, qi, aligned);
-        }
-      }
-    };
-    auto by_width = [&](auto ftag) {
-      auto go = [&](auto wtag) {
-        if (emit_deq) process(wtag, ftag, std::true_type{});
-        else process(wtag, ftag, std::false_type{});
-      };
-      switch (w) {
-        case 2: go(std::integral_constant<int, 2>{}); break;
-        case 4: go(std::integral_constant<int, 4>{}); break;
-        case 8: go(std::integral_constant<int, 8>{}); break;
-        default: go(std::integral_constant<int, 16>{}); break;  // launcher guarantees w in {2,4,8,16}
-      }
-    };
-    if constexpr (DT == RTKV_F16) {
-      if (__builtin_amdgcn_readfirstlane((int)(rp.fast && !row_nan))) {
-        const _Float16 zph = (_Float16)rp.zp, sh = (_Float16)rp.scale, qmh = (_Float16)rp.qmaxT;
-        const h2_t zp2 = {zph, zph}, s2 = {sh, sh};
-        auto native = [&](auto wtag, auto dtag) {
-          constexpr int W = decltype(wtag)::value;
-          constexpr bool DEQ = decltype(dtag)::value;
-          const bool aligned = FULL || (((uintptr_t)pk & 15) == 0 && (nch * W) % 16 == 0);
-#pragma unroll
-          for (int k = 0; k < NCH; ++k) {
-            const int c = k * 64 + lane;
-            __builtin_amdgcn_sched_barrier(0);  // keep one chunk's temporaries live at a time
-            if (!valid(k)) continue;
-            uint32_t qi[8], dq[4];
-            f16_chunk_codes<DEQ>(raw[k].a, rp.scale, rp.rcp, zp2, s2, qmh, qi, dq);
-            if (emit_pk) pack_store<W>(pk + c * W, qi, aligned);
-            if constexpr (DEQ) nt_store16(orow + out_off[k], dq[0], dq[1], dq[2], dq[3]);
-          }
-        };
-        auto by_w = [&](auto dtag) {
-          switch (w) {
-            case 2: native(std::integral_constant<int, 2>{}, dtag); break;
-            case 4: native(std::integral_constant<int, 4>{}, dtag); break;
-            case 8: native(std::integral_constant<int, 8>{}, dtag); break;
-            default: native(std::integral_constant<int, 16>{}, dtag); break;
-          }
-        };
-        if (emit_deq) by_w(std::true_type{});
-        else by_w(std::false_type{});
-        continue;
-      }
-    }
-    if (__builtin_amdgcn_readfirstlane((int)rp.fast)) by_width(std::true_type{});
-    else by_width(std::false_type{});
+    emit_row<DT, NCH, CONTIG, FULL>(raw, rp, row_nan, w, orow, out_off, pk, nch, lane, emit_deq, emit_pk);
   }
 }
 

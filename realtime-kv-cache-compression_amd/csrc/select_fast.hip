@@ -1,955 +1,8 @@
-// select_fast.hip — K2 for one batch row (B = 1, S <= 32768: every reference configuration that
-// fits one GPU) in ONE launch instead of select.hip's four, with every per-token pass spread over
-// the whole grid.  Same outputs, bit for bit (scores, classes, mask, kept_index, row_offset,
-// row_label, counts; the double statistics to 1e-12 relative).
-//
-// Reference (per batch row), as in select.hip:
-//   scores      token_importance.py:134-176   s = α·N·w_l + β·log(i+1)/log(S) + γ·min(1, P/S)
-//   min-max     token_importance.py:49-85     (global min/max of A: K1 per-block partials)
-//   classes     dynamic_quantization.py:21-60
-//   selection   selective_propagation.py:68-161  greedy in closed form: top n_g of each class
-//   fallback    selective_propagation.py:205-211  topk(max(1, int(0.1·S))) if nothing selected
-//   compaction  selective_propagation.py:214-232  kept rows in ascending original index
-//
-// G = ceil(S/1024) workgroups of 1024 threads, one token per thread, three phases:
-// 1 scores  Scores and classes; per-workgroup class counts and score sums; a 4096-bin histogram per
-//           class over a FIXED linear binning of the score range (any monotone map of the score
-//           works: the histogram only has to tell which bin holds each class's threshold), and every
-//           token's (key, index) appended to a 64-entry slot list of its bin (slot = the histogram
-//           atomic's return value, one atomic per bin and wave).
-// 2 select  Workgroup G−1 (dispatched last): once every workgroup's counts are published, the quotas
-//           n_g from the class counts (the greedy in closed form), per partially kept class the bin
-//           where the count from the top reaches n_g, and the exact threshold from that bin's slot
-//           list (≤ 64 entries, one wave): key T and the number of tokens at T to take in index
-//           order.  A bin with more than 64 tokens (heavy ties) takes the exact rescan path: all S
-//           keys in registers, ≤ 3 LDS-histogram rounds.
-// 3 compact Every workgroup, its token still in registers: keep decisions from (mode, T, ties) per
-//           group; per-workgroup aggregates (surely kept tokens per class, ties per group); each
-//           workgroup sums its predecessors' aggregates (decoupled look-back: every aggregate is
-//           published before any is awaited, and all G <= 32 workgroups are resident at once), then
-//           ranks its tokens with block scans: mask, kept_index, row_label, row_offset; its
-//           kept-token statistics are added atomically.
-//
-// Hand-offs between workgroups are TAGGED 8-byte words (bit 63 set on a zeroed word: the region is
-// cleared before every launch), written with sc1 stores and polled with sc1 loads, so a consumer sees
-// data and flag in one round trip and producers need no drain between them (MI355X_MICROARCH.md
-// hand-off rows: each separate flag or drain costs a memory round trip, ≈1–2 µs).  The one drain
-// left is phase 1's: a workgroup's slot-list entries and score sums are complete (s_waitcnt
-// vmcnt(0)) before its tagged counts word, which is what the selecting workgroup polls.
-#include "common.h"
-
-#ifdef RTKV_SELECT_PROBE  // diagnostic build (tools/k2_probe.hip): phase timestamps (s_memrealtime, 100 MHz)
-__device__ unsigned long long g_k2_probe[16];   // the selecting workgroup's phases
-__device__ unsigned long long g_k2_clock[16];
-__device__ unsigned long long g_k2_wg[32][10];  // per workgroup phase timestamps
-__device__ int g_k2_rep;  // the probe's second pass over phase 2 (warm instruction cache) records at k + 8
-#define K2_PROBE(k) do { if (threadIdx.x == 0) { g_k2_probe[(k) + 8 * g_k2_rep] = __builtin_amdgcn_s_memrealtime(); g_k2_clock[(k) + 8 * g_k2_rep] = __builtin_amdgcn_s_memtime(); } } while (0)
-#define K2_WG(k) do { if (threadIdx.x == 0) g_k2_wg[blockIdx.x][k] = __builtin_amdgcn_s_memrealtime(); } while (0)
-__device__ int g_k2_twice;  // set by the probe: run phase 2 twice (the first pass cold)
-#else
-#define K2_PROBE(k) do { } while (0)
-#define K2_WG(k) do { } while (0)
-#endif
+// select_fast.hip — host side of the one-launch K2 (device code: select_fast.h) and of the fused
+// K2 + K4 launch (fused.h; per-dtype instantiations in fused_{f32,f16,bf16}.hip).
+#include "select_fast.h"
 
 namespace rtkv {
-
-namespace {
-
-constexpr int kST = 1024;          // threads per workgroup
-constexpr int kSW = kST / kWave;   // waves
-constexpr int kBinBits = 12;
-constexpr int kNBin = 1 << kBinBits;
-constexpr int kGrp = 4;            // classes LOW, MEDIUM, HIGH + "all tokens" (fallback)
-constexpr int kCap = 64;           // slot list entries per bin (one per lane of a wave)
-constexpr int kMaxS = 32 * kST;    // 32 tokens per thread in the rescan path
-constexpr int kMaxG = kMaxS / kST; // workgroups
-constexpr uint64_t kTag = 1ull << 63;
-enum { M_NONE = 0, M_ALL = 1, M_PART = 2 };
-
-struct FastHead {                  // zeroed before the launch (K1 or a memset): tagged hand-off words
-  uint64_t part[kMaxG];            // phase 1, per workgroup: kTag | class counts (3 x 11 bits)
-  uint64_t sel[8];                 // phase 2: [q] kTag | fallback<<50 | mode<<48 | ties<<32 | T; [4], [5] the mean
-  uint64_t agg[kMaxG][2];          // phase 3, per workgroup: kTag | sure (3 x 11 bits), kTag | ties (4 x 11 bits)
-};
-struct FastPartial {               // phase 1, per workgroup (complete before its counts word)
-  double ssum;
-  uint32_t kmn, kmx;               // score key range
-};
-struct FastLayout {
-  FastHead* head;                  // zeroed
-  uint32_t* hist;                  // [kGrp][kNBin] (zeroed)
-  FastPartial* part;               // [G]
-  uint64_t* slots;                 // [kGrp][kNBin][kCap] of (key << 32 | index)
-};
-
-struct FastArgs {
-  FinalizeArgs f;
-  FastLayout L;
-  float bin_lo[kGrp];              // bin(s) = clamp(floor((s - lo) * inv), 0, kNBin - 1): monotone in s
-  float bin_inv[kGrp];
-  int hist_fb;                     // histogram the fallback group too (fallback possible)
-  rtkv_early_stats* early;         // host-mapped stats mirror (nullable), published by the selecting workgroup
-  uint64_t early_seq;
-  uint32_t spin_limit;             // polls before a hand-off wait gives up (poll_tagged)
-  int withhold;                    // RTKV_TEST_WITHHOLD_SELECTION: never publish the selection words
-};
-
-__device__ __forceinline__ float key_score(uint32_t k) {
-  const uint32_t u = (k & 0x80000000u) ? (k & 0x7fffffffu) : ~k;
-  return __builtin_bit_cast(float, u);
-}
-
-// Monotone non-decreasing in the order-preserving key of s (NaNs: sign-bit ones below every
-// number, the others above, as in score_key).
-__device__ __forceinline__ int bin_of(float s, float lo, float inv) {
-  const float x = floorf((s - lo) * inv);
-  if (x != x) return (__builtin_bit_cast(uint32_t, s) >> 31) ? 0 : kNBin - 1;
-  return x <= 0.f ? 0 : (x >= (float)(kNBin - 1) ? kNBin - 1 : (int)x);
-}
-
-// Hide a value's provenance from the optimiser at a phase boundary, so that per-token values derived
-// from it (the 2-bit groups) are recomputed in each phase instead of being kept live across phases.
-template <typename T> __device__ __forceinline__ void opaque(T& v) { asm volatile("" : "+v"(v)); }
-
-__device__ __forceinline__ uint32_t fld(uint64_t v, int g) { return (uint32_t)(v >> (16 * g)) & 0xffffu; }
-
-// Exclusive block scan of a uint32 (block total < 2^32); *total = the block total.  `sh` is a [kSW]
-// LDS array private to this call site.
-// Inclusive wave scan on DPP lane moves (row_shr within rows of 16, then row_bcast:15 / :31 across
-// rows): register-to-register, no LDS round trips as __shfl's ds_bpermute takes.
-__device__ __forceinline__ uint32_t wave_scan_dpp(uint32_t v) {
-  int x = (int)v;
-  x += __builtin_amdgcn_update_dpp(0, x, 0x111, 0xf, 0xf, false);  // row_shr:1
-  x += __builtin_amdgcn_update_dpp(0, x, 0x112, 0xf, 0xf, false);  // row_shr:2
-  x += __builtin_amdgcn_update_dpp(0, x, 0x114, 0xf, 0xf, false);  // row_shr:4
-  x += __builtin_amdgcn_update_dpp(0, x, 0x118, 0xf, 0xf, false);  // row_shr:8
-  x += __builtin_amdgcn_update_dpp(0, x, 0x142, 0xa, 0xf, false);  // row_bcast:15 into rows 1, 3
-  x += __builtin_amdgcn_update_dpp(0, x, 0x143, 0xc, 0xf, false);  // row_bcast:31 into rows 2, 3
-  return (uint32_t)x;
-}
-
-__device__ __forceinline__ uint32_t block_excl_scan32(uint32_t v, uint32_t* sh, uint32_t* total) {
-  const int lane = threadIdx.x & (kWave - 1), wid = threadIdx.x / kWave;
-  const uint32_t inc = wave_scan_dpp(v);
-  if (lane == kWave - 1) sh[wid] = inc;
-  __syncthreads();
-  uint32_t ws = sh[lane & (kSW - 1)];
-#pragma unroll
-  for (int o = 1; o < kSW; o <<= 1) {
-    const uint32_t n = __shfl_up(ws, o, kWave);
-    if ((lane & (kSW - 1)) >= o) ws += n;
-  }
-  *total = __shfl(ws, kSW - 1, kWave);
-  const uint32_t base = wid > 0 ? __shfl(ws, wid - 1, kWave) : 0u;
-  return base + inc - v;
-}
-
-// Ranks in thread order of NF one-bit flags per thread, and their workgroup totals, from wave
-// ballots (the popcount below the lane plus the counts of the preceding waves): one barrier, no
-// shuffles.  `sh` is an [NF][kSW] LDS array private to the call site.
-template <int NF>
-__device__ __forceinline__ void block_flag_ranks(const bool (&f)[NF], uint32_t (&rank)[NF], uint32_t (&total)[NF],
-                                                 uint32_t (*sh)[kSW]) {
-  const int lane = threadIdx.x & (kWave - 1), wid = threadIdx.x / kWave;
-  const uint64_t lt = (1ull << lane) - 1ull;
-  uint64_t b[NF];
-#pragma unroll
-  for (int q = 0; q < NF; ++q) {
-    b[q] = __ballot(f[q]);
-    if (lane == 0) sh[q][wid] = (uint32_t)__popcll(b[q]);
-  }
-  __syncthreads();
-#pragma unroll
-  for (int q = 0; q < NF; ++q) {
-    uint32_t before = 0, tot = 0;
-#pragma unroll
-    for (int w = 0; w < kSW; ++w) {
-      const uint32_t v = sh[q][w];
-      tot += v;
-      before += w < wid ? v : 0u;
-    }
-    rank[q] = before + (uint32_t)__popcll(b[q] & lt);
-    total[q] = tot;
-  }
-}
-
-// Exclusive block scan of a packed uint64 (independent 16-bit fields whose block totals stay
-// < 65536); *total = the block total.  `sh` is a [kSW] LDS array private to this call site.
-__device__ __forceinline__ uint64_t block_excl_scan(uint64_t v, uint64_t* sh, uint64_t* total) {
-  const int lane = threadIdx.x & (kWave - 1), wid = threadIdx.x / kWave;
-  const uint64_t inc = wave_inclusive_scan(v);
-  if (lane == kWave - 1) sh[wid] = inc;
-  __syncthreads();
-  // lanes 0..15 scan the 16 wave totals; lane wid-1 holds the base of this wave, lane 15 the total
-  uint64_t ws = sh[lane & (kSW - 1)];
-#pragma unroll
-  for (int o = 1; o < kSW; o <<= 1) {
-    const uint64_t n = __shfl_up(ws, o, kWave);
-    if ((lane & (kSW - 1)) >= o) ws += n;
-  }
-  *total = __shfl(ws, kSW - 1, kWave);
-  const uint64_t base = wid > 0 ? __shfl(ws, wid - 1, kWave) : 0ull;
-  return base + inc - v;
-}
-
-__device__ __forceinline__ int64_t row_bytes(const FinalizeArgs& a, int lab) {
-  return (a.F * field_width(a.kv_dtype < 0 ? RTKV_F32 : a.kv_dtype, a.p.bits[lab]) + 7) / 8;
-}
-
-__device__ __forceinline__ float bin_lo_of(const FastArgs& g, int q) {
-  return q == 3 ? g.bin_lo[3] : (q == 2 ? g.bin_lo[2] : (q == 1 ? g.bin_lo[1] : g.bin_lo[0]));
-}
-__device__ __forceinline__ float bin_inv_of(const FastArgs& g, int q) {
-  return q == 3 ? g.bin_inv[3] : (q == 2 ? g.bin_inv[2] : (q == 1 ? g.bin_inv[1] : g.bin_inv[0]));
-}
-
-__device__ __forceinline__ int class_of(float s, const rtkv_layer_params& p) {
-  return (s >= p.theta_h) ? 2 : ((s >= p.theta_m && s < p.theta_h) ? 1 : 0);  // dynamic_quantization.py:41-45
-}
-
-
-// 16-bit packed fields <-> 11-bit packed fields (per-workgroup counts are <= 1024)
-__device__ __forceinline__ uint64_t to11(uint64_t v16, int n) {
-  uint64_t r = 0;
-#pragma unroll
-  for (int q = 0; q < 4; ++q)
-    if (q < n) r |= (uint64_t)fld(v16, q) << (11 * q);
-  return r;
-}
-__device__ __forceinline__ uint64_t from11(uint64_t v11, int n) {
-  uint64_t r = 0;
-#pragma unroll
-  for (int q = 0; q < 4; ++q)
-    if (q < n) r |= ((v11 >> (11 * q)) & 0x7ffull) << (16 * q);
-  return r;
-}
-
-// A histogram increment whose return value is the token's slot, aggregated over the wave: lanes with
-// the same bin id v (< 2^14) share one atomic by the lowest of them, and each takes base + its rank
-// among those peers (the slot order within a bin is arbitrary anyway: slot lists are ranked by
-// (key, index)).  Attention-like importance piles thousands of tokens into a few bins, where one
-// returning atomic per token serialises on the address (~11 ns each).
-__device__ __forceinline__ uint32_t hist_slot(uint32_t* addr, uint32_t v, bool part) {
-  uint64_t peers = __ballot(part);
-#pragma unroll
-  for (int k = 0; k < 14; ++k) {
-    const uint64_t bk = __ballot((v >> k) & 1u);
-    peers &= ((v >> k) & 1u) ? bk : ~bk;
-  }
-  const int lane = threadIdx.x & (kWave - 1);
-  const uint64_t below = peers & ((1ull << lane) - 1ull);
-  const int leader = peers ? __ffsll((unsigned long long)peers) - 1 : 0;
-  uint32_t base = 0u;
-  if (part && below == 0ull) base = atomicAdd(addr, (uint32_t)__popcll(peers));
-  base = (uint32_t)__shfl((int)base, leader, kWave);
-  return base + (uint32_t)__popcll(below);
-}
-
-// A 16-byte coherent load (global_load_dwordx4 ... sc1, as ld_sc1 for one word).  The compiler does not
-// track inline-asm loads: the caller waits (s_waitcnt vmcnt(0)) before the first use.
-__device__ __forceinline__ rtkv_u32x4 ld16_sc1(const uint32_t* p) {
-  rtkv_u32x4 v;
-  asm volatile("global_load_dwordx4 %0, %1, off sc1" : "=v"(v) : "v"(p) : "memory");
-  return v;
-}
-
-// Poll tagged words: lanes l < n of the calling wave wait for words[l * stride] to carry kTag and
-// return it (0 for the other lanes).  Bounded: after `limit` polls (≈1 µs each: a coherent load round
-// trip plus s_sleep) a lane gives up with an untagged 0 and RTKV_FLAG_SPIN_TIMEOUT is raised in the
-// layer statistics, so a hand-off that never comes ends the kernel instead of hanging the GPU.
-__device__ __forceinline__ uint64_t poll_tagged(const uint64_t* words, int stride, int n, uint32_t limit,
-                                                rtkv_layer_stats* stats) {
-  const int lane = threadIdx.x & (kWave - 1);
-  uint64_t w = 0;
-  if (lane < n) {
-    w = ld_sc1(words + (size_t)lane * stride);
-    for (uint32_t it = 0; !(w & kTag); ++it) {
-      if (it >= limit) {
-        atomicOr(&stats->error_flags, (int)RTKV_FLAG_SPIN_TIMEOUT);
-        w = 0;
-        break;
-      }
-      __builtin_amdgcn_s_sleep(1);
-      w = ld_sc1(words + (size_t)lane * stride);
-    }
-  }
-  return w;
-}
-
-// ------------------------------------------------------------------------------------ rescan path
-// Exact threshold of every group in `heavy` (a threshold bin with more than kCap tokens: heavy
-// ties) from all S keys held in registers: candidates = the group's tokens in its threshold bin,
-// then ≤ 3 rounds of key-range LDS histograms (span −12 bits per round).  need[q]: tokens to take
-// from the candidates on entry, tokens at the threshold key on exit.
-template <int TPT>
-__device__ __forceinline__ void rescan_thresholds(const FastArgs& g, uint32_t* hist_lds, int heavy, bool fallback,
-                                                  const int (&bstar)[kGrp], int (&need)[kGrp], uint32_t (&thr)[kGrp]) {
-  const FinalizeArgs& a = g.f;
-  __shared__ uint64_t s_scan[4][kSW];
-  __shared__ uint32_t s_key[2 * kGrp][kSW];
-  __shared__ uint32_t s_pick[2][kGrp][2];
-  const int t = threadIdx.x, lane = t & (kWave - 1), wid = t / kWave;
-  const int S = (int)a.S;
-  const int i0 = t * TPT;
-  const int nv = S - i0 < 0 ? 0 : (S - i0 > TPT ? TPT : S - i0);
-  float sv[TPT];
-#pragma unroll
-  for (int k = 0; k < TPT; ++k) sv[k] = ld_sc1(a.scores + (i0 + k < S ? i0 + k : S - 1));
-  uint32_t key[TPT];
-  uint64_t grp = 0;  // 2 bits per token: its group
-  uint32_t cand = 0;
-  uint32_t kmn[kGrp], kmx[kGrp];
-#pragma unroll
-  for (int q = 0; q < kGrp; ++q) { kmn[q] = 0xffffffffu; kmx[q] = 0u; }
-#pragma unroll
-  for (int k = 0; k < TPT; ++k) {
-    const float s = sv[k];
-    const int e = fallback ? 3 : class_of(s, a.p);
-    grp |= (uint64_t)e << (2 * k);
-    key[k] = score_key(s);
-    bool c = false;
-#pragma unroll
-    for (int q = 0; q < kGrp; ++q) {
-      const bool cq = (k < nv) & (e == q) & (((heavy >> q) & 1) != 0) & (bin_of(s, g.bin_lo[q], g.bin_inv[q]) == bstar[q]);
-      kmn[q] = cq ? min(kmn[q], key[k]) : kmn[q];
-      kmx[q] = cq ? max(kmx[q], key[k]) : kmx[q];
-      c |= cq;
-    }
-    cand |= (uint32_t)c << k;
-  }
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1)
-#pragma unroll
-    for (int q = 0; q < kGrp; ++q) {
-      kmn[q] = min(kmn[q], (uint32_t)__shfl_xor((int)kmn[q], o, kWave));
-      kmx[q] = max(kmx[q], (uint32_t)__shfl_xor((int)kmx[q], o, kWave));
-    }
-  if (lane == 0) {
-#pragma unroll
-    for (int q = 0; q < kGrp; ++q) { s_key[q][wid] = kmn[q]; s_key[kGrp + q][wid] = kmx[q]; }
-  }
-  __syncthreads();
-  uint32_t lo[kGrp], hi[kGrp];
-  {
-    const int src = lane & (kSW - 1);
-#pragma unroll
-    for (int q = 0; q < kGrp; ++q) { kmn[q] = s_key[q][src]; kmx[q] = s_key[kGrp + q][src]; }
-#pragma unroll
-    for (int o = kSW / 2; o > 0; o >>= 1)
-#pragma unroll
-      for (int q = 0; q < kGrp; ++q) {
-        kmn[q] = min(kmn[q], (uint32_t)__shfl_xor((int)kmn[q], o, kWave));
-        kmx[q] = max(kmx[q], (uint32_t)__shfl_xor((int)kmx[q], o, kWave));
-      }
-#pragma unroll
-    for (int q = 0; q < kGrp; ++q) { lo[q] = kmn[q]; hi[q] = kmx[q]; }
-  }
-#pragma unroll 1
-  for (int round = 0; round < 4; ++round) {
-    int act = 0, sh[kGrp];
-#pragma unroll
-    for (int q = 0; q < kGrp; ++q) {
-      if (((heavy >> q) & 1) && lo[q] != hi[q]) act |= 1 << q;
-      const int bl = 32 - __clz((int)(hi[q] - lo[q]));
-      sh[q] = bl > kBinBits ? bl - kBinBits : 0;
-    }
-    if (!act) break;
-    opaque(grp);
-    for (int w = t; w < kGrp * kNBin / 4; w += kST) reinterpret_cast<uint4*>(hist_lds)[w] = make_uint4(0u, 0u, 0u, 0u);
-    if (t < kGrp) { s_pick[round & 1][t][0] = 0u; s_pick[round & 1][t][1] = 0u; }
-    __syncthreads();
-#pragma unroll
-    for (int k = 0; k < TPT; ++k) {
-      const int e = (int)((grp >> (2 * k)) & 3u);
-      bool in = false;
-      uint32_t off = 0u;
-#pragma unroll
-      for (int q = 0; q < kGrp; ++q) {  // per-group compares combined by masks: no per-token indexing
-        const bool iq = (((cand >> k) & 1u) != 0) & (e == q) & (((act >> q) & 1) != 0) & (key[k] >= lo[q]) &
-                        (key[k] <= hi[q]);
-        in |= iq;
-        off = iq ? (uint32_t)(q * kNBin) + ((key[k] - lo[q]) >> sh[q]) : off;
-      }
-      if (in) atomicAdd(&hist_lds[off], 1u);
-    }
-    __syncthreads();
-    uint32_t c[kGrp][4];
-    uint64_t pk = 0;
-#pragma unroll
-    for (int q = 0; q < kGrp; ++q) {
-      const uint4 h4 = (act >> q) & 1 ? reinterpret_cast<const uint4*>(hist_lds + q * kNBin)[kNBin / 4 - 1 - t]
-                                      : make_uint4(0u, 0u, 0u, 0u);
-      c[q][0] = h4.w; c[q][1] = h4.z; c[q][2] = h4.y; c[q][3] = h4.x;
-      pk |= (uint64_t)(c[q][0] + c[q][1] + c[q][2] + c[q][3]) << (16 * q);
-    }
-    uint64_t tot;
-    const uint64_t ex = block_excl_scan(pk, s_scan[round], &tot);
-#pragma unroll
-    for (int q = 0; q < kGrp; ++q) {
-      if (!((act >> q) & 1)) continue;
-      int run = (int)fld(ex, q);
-      if (run < need[q] && need[q] <= run + (int)fld(pk, q)) {
-        bool found = false;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          if (!found && run + (int)c[q][j] >= need[q]) {
-            s_pick[round & 1][q][0] = (uint32_t)(kNBin - 1 - 4 * t - j);
-            s_pick[round & 1][q][1] = (uint32_t)run;
-            found = true;
-          }
-          run += c[q][j];
-        }
-      }
-    }
-    __syncthreads();
-#pragma unroll
-    for (int q = 0; q < kGrp; ++q) {
-      if (!((act >> q) & 1)) continue;
-      const uint64_t nlo = (uint64_t)lo[q] + ((uint64_t)s_pick[round & 1][q][0] << sh[q]);
-      const uint64_t nhi = nlo + ((1ull << sh[q]) - 1ull);
-      need[q] -= (int)s_pick[round & 1][q][1];
-      lo[q] = (uint32_t)nlo;
-      hi[q] = nhi < (uint64_t)hi[q] ? (uint32_t)nhi : hi[q];
-    }
-  }
-#pragma unroll
-  for (int q = 0; q < kGrp; ++q)
-    if ((heavy >> q) & 1) thr[q] = lo[q];
-}
-
-// ------------------------------------------------------------------------------------ phase 2
-// Workgroup G−1, after its own phase 1: quotas, threshold bins, exact thresholds; publishes the
-// selection words and the statistics.  s_selw receives the selection words (thread 0 writes them;
-// the caller's barrier publishes them to the workgroup).
-template <int TPT>
-__device__ __forceinline__ void select_thresholds(const FastArgs& g, uint32_t* hist_lds, uint64_t* s_selw) {
-  const FinalizeArgs& a = g.f;
-  __shared__ uint32_t s_scan32[kGrp][kSW];
-  __shared__ uint64_t s_part[kMaxG];
-  __shared__ uint32_t s_pick[kGrp][3];
-  __shared__ uint32_t s_thr[kGrp];
-  __shared__ int s_tie[kGrp];
-  __shared__ double s_ssum;
-  __shared__ uint32_t s_kr[2];
-  const int t = threadIdx.x, lane = t & (kWave - 1), wid = t / kWave;
-  const int S = (int)a.S;
-  const int G = (S + kST - 1) / kST;
-  K2_PROBE(0);
-  // ---- every workgroup's class counts (tagged words; their slot lists and sums are complete)
-  if (wid == 0) {
-    const uint64_t w = poll_tagged(g.L.head->part, 1, G, g.spin_limit, a.stats);
-    if (lane < G) s_part[lane] = w;
-  }
-  __syncthreads();
-  K2_PROBE(1);
-  // ---- issue every histogram load the thresholds may need (thread t owns descending bins 4t..4t+3)
-  // before the quotas are known, and wave 0 the score sums and ranges, in one round trip
-  const int ngrp = g.hist_fb ? 4 : 3;
-  double p_ss = 0.0;
-  uint32_t p_kmn = 0xffffffffu, p_kmx = 0u;
-  if (wid == 0 && lane < G) {
-    const FastPartial* pp = g.L.part + lane;
-    p_ss = ld_sc1(&pp->ssum);
-    p_kmn = ld_sc1(&pp->kmn);
-    p_kmx = ld_sc1(&pp->kmx);
-  }
-  uint32_t c[kGrp][4];
-  {
-    rtkv_u32x4 h[kGrp];
-#pragma unroll
-    for (int q = 0; q < kGrp; ++q) {
-      h[q] = rtkv_u32x4{0u, 0u, 0u, 0u};
-      if (q < ngrp) h[q] = ld16_sc1(g.L.hist + q * kNBin + (kNBin - 4 - 4 * t));
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#pragma unroll
-    for (int q = 0; q < kGrp; ++q) { c[q][0] = h[q].w; c[q][1] = h[q].z; c[q][2] = h[q].y; c[q][3] = h[q].x; }
-  }
-  if (wid == 0) {
-#pragma unroll
-    for (int o = kWave / 2; o > 0; o >>= 1) {  // lanes >= G hold the neutral values
-      p_ss += __shfl_xor(p_ss, o, kWave);
-      p_kmn = min(p_kmn, (uint32_t)__shfl_xor((int)p_kmn, o, kWave));
-      p_kmx = max(p_kmx, (uint32_t)__shfl_xor((int)p_kmx, o, kWave));
-    }
-    if (lane == 0) { s_ssum = p_ss; s_kr[0] = p_kmn; s_kr[1] = p_kmx; }
-  }
-#ifdef RTKV_SELECT_PROBE
-  {
-    uint32_t z = 0;
-#pragma unroll
-    for (int q = 0; q < kGrp; ++q) z += c[q][0] + c[q][1] + c[q][2] + c[q][3];
-    if (z == 0xffffffffu) g_k2_probe[15] = z;  // waits for the histogram loads
-    K2_PROBE(4);
-  }
-#endif
-  // ---- class counts and quotas in wave 0 (the other waves wait at the barrier, their histogram
-  // loads in flight): lane l reads workgroup l (G <= 32); the greedy in closed form
-  // (selective_propagation.py:93-131)
-  __shared__ int s_q[2 * kGrp];
-  __shared__ int64_t s_cc[3], s_quota[3];
-  if (wid == 0) {
-    uint64_t cnt = lane < G ? from11(s_part[lane] & ~kTag, 3) : 0ull;
-#pragma unroll
-    for (int o = kWave / 2; o > 0; o >>= 1) cnt += __shfl_xor(cnt, o, kWave);
-    if (lane == 0) {
-      // In 32-bit integers: N <= S <= 2^15 and bits <= 32, so every product and quotient that can
-      // decide n fits; the budget U = floor(8·S·ratio) (int64 in the reference) is compared as a
-      // double, exact below 2^53 (beyond, every class fits whole).
-      const double u8 = 8.0 * ((double)S * a.p.propagation_ratio);
-      const double Ud = u8 >= 9.0e18 ? 9.0e18 : floor(u8);
-      int used = 0, kept = 0;
-      for (int k = 2; k >= 0; --k) {
-        const int N = (int)fld(cnt, k), bb = a.p.bits[k];
-        int n;
-        if (a.mode_select == 2) n = N;
-        else if (!(u8 >= 0.0)) n = 0;  // U = -1 (selective_propagation.py: nothing fits)
-        else if (bb <= 0) n = N;
-        else {
-          const double x = Ud - (double)used;  // U - used >= 0
-          n = x >= (double)bb * (double)N ? N : (int)((uint32_t)x / (uint32_t)bb);
-        }
-        used += n * (bb > 0 ? bb : 0);
-        kept += n;
-        s_q[kGrp + k] = n;
-        s_quota[k] = n;
-        s_cc[k] = N;
-        s_q[k] = (n == 0) ? M_NONE : (n == N ? M_ALL : M_PART);
-      }
-      int64_t kf = (int64_t)((double)S * 0.1);
-      if (kf < 1) kf = 1;
-      const bool fb = a.mode_select == 1 && !(a.p.flags & RTKV_NO_FALLBACK) && kept == 0;
-      s_q[kGrp + 3] = (int)kf;
-      s_q[3] = !fb ? M_NONE : (kf >= S ? M_ALL : M_PART);
-    }
-  }
-  __syncthreads();
-  int mode[kGrp], need[kGrp];
-#pragma unroll
-  for (int q = 0; q < kGrp; ++q) { mode[q] = s_q[q]; need[q] = s_q[kGrp + q]; }
-  const bool fallback = mode[3] != M_NONE;
-  int part = 0;
-#pragma unroll
-  for (int q = 0; q < kGrp; ++q) part |= (mode[q] == M_PART) << q;
-  uint32_t thr[kGrp] = {0u, 0u, 0u, 0u};
-  K2_PROBE(5);
-  if (part) {
-    // ---- the bin holding each partial group's threshold: one 32-bit scan per partial group
-    if (t < kGrp) { s_pick[t][0] = 0u; s_pick[t][1] = 0u; s_pick[t][2] = 0u; }
-#pragma unroll
-    for (int q = 0; q < kGrp; ++q) {
-      if (!((part >> q) & 1)) continue;
-      const uint32_t sum = c[q][0] + c[q][1] + c[q][2] + c[q][3];
-      uint32_t tot;
-      int run = (int)block_excl_scan32(sum, s_scan32[q], &tot);
-      K2_PROBE(6);
-      if (run < need[q] && need[q] <= run + (int)sum) {
-        bool found = false;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          if (!found && run + (int)c[q][j] >= need[q]) {
-            s_pick[q][0] = (uint32_t)(kNBin - 1 - 4 * t - j);
-            s_pick[q][1] = (uint32_t)run;          // tokens of the group in higher bins
-            s_pick[q][2] = c[q][j];                // tokens in the bin
-            found = true;
-          }
-          run += c[q][j];
-        }
-      }
-    }
-    K2_PROBE(7);
-    __syncthreads();
-    int bstar[kGrp] = {0, 0, 0, 0};
-    int heavy = 0;
-#pragma unroll
-    for (int q = 0; q < kGrp; ++q) {
-      if (!((part >> q) & 1)) continue;
-      bstar[q] = (int)s_pick[q][0];
-      need[q] -= (int)s_pick[q][1];
-      if ((int)s_pick[q][2] > kCap) heavy |= 1 << q;
-    }
-    K2_PROBE(2);
-    // ---- light bins: wave q ranks its group's slot list (≤ 64 entries, one per lane)
-    if (wid < kGrp && ((part >> wid) & 1) && !((heavy >> wid) & 1)) {
-      const int q = wid;
-      const int n = (int)s_pick[q][2];
-      const uint64_t* sl = g.L.slots + ((size_t)q * kNBin + (size_t)bstar[q]) * kCap;
-      const uint64_t e = lane < n ? ld_sc1(sl + lane) : 0ull;
-      const uint32_t k = (uint32_t)(e >> 32), idx = (uint32_t)e;
-      // rank = entries ahead of this one in (key desc, index asc) order
-      int rank = 0;
-      for (int j = 0; j < n; ++j) {
-        const uint64_t o = __shfl(e, j, kWave);
-        const uint32_t ok = (uint32_t)(o >> 32), oi = (uint32_t)o;
-        rank += (ok > k) | ((ok == k) & (oi < idx));
-      }
-      const int r = need[q];  // 1 <= r <= n
-      const uint64_t hit = __ballot(lane < n && rank == r - 1);
-      const int src = hit ? (__ffsll((unsigned long long)hit) - 1) : 0;
-      const uint32_t T = (uint32_t)__shfl((int)k, src, kWave);
-      const uint64_t above = __ballot(lane < n && k > T);
-      if (lane == 0) { s_thr[q] = T; s_tie[q] = r - __popcll(above); }
-    }
-    if (heavy) rescan_thresholds<TPT>(g, hist_lds, heavy, fallback, bstar, need, thr);
-    __syncthreads();
-#pragma unroll
-    for (int q = 0; q < kGrp; ++q) {
-      if (!((part >> q) & 1) || ((heavy >> q) & 1)) continue;
-      thr[q] = s_thr[q];
-      need[q] = s_tie[q];
-    }
-  } else {
-    __syncthreads();  // s_ssum / s_kr
-  }
-  K2_PROBE(3);
-  if (t != 0) return;
-  // ---- the selection words first (the other workgroups wait on them), then the statistics
-  const double ssum = s_ssum;
-  const double mean = ssum / (double)S;
-  const uint64_t mb = __builtin_bit_cast(uint64_t, mean);
-  for (int q = 0; q < kGrp; ++q) {
-    const uint64_t w = kTag | ((uint64_t)(fallback ? 1 : 0) << 50) | ((uint64_t)mode[q] << 48) |
-                       ((uint64_t)(need[q] & 0xffff) << 32) | thr[q];
-    if (!g.withhold) st_sc1(&g.L.head->sel[q], w);
-    s_selw[q] = w;
-  }
-  const uint64_t m_lo = kTag | (mb & 0xffffffffu), m_hi = kTag | (mb >> 32);
-  if (!g.withhold) {
-    st_sc1(&g.L.head->sel[4], m_lo);
-    st_sc1(&g.L.head->sel[5], m_hi);
-  }
-  s_selw[4] = m_lo;
-  s_selw[5] = m_hi;
-  // statistics known here; phase 3 adds the kept-token sums (stats zeroed before the launch)
-  const int64_t ccount[3] = {s_cc[0], s_cc[1], s_cc[2]};
-  const int64_t quota[3] = {s_quota[0], s_quota[1], s_quota[2]};
-  rtkv_layer_stats* hs = a.stats;
-  rtkv_batch_stats* bs = reinterpret_cast<rtkv_batch_stats*>(hs + 1);
-  for (int q = 0; q < 3; ++q) bs->class_count[q] = ccount[q];
-  bs->fallback = fallback ? 1 : 0;
-  hs->score_sum = ssum;
-  hs->score_min = key_score(s_kr[0]);
-  hs->score_max = key_score(s_kr[1]);
-  int flags = 0;
-  if (a.kv_dtype == RTKV_F16)
-    for (int q = 0; q < 3; ++q)
-      if (ccount[q] > 0 && a.p.bits[q] >= 16) flags |= RTKV_FLAG_F16_QMAX_OVERFLOW;
-  if (flags) atomicOr(&hs->error_flags, flags);  // a spin timeout may have been flagged already
-  hs->B = 1;
-  if (!fallback) {  // the kept counts are the quotas: final here (phase 3 adds only the score sums)
-    int64_t n = 0, units = 0, bytes = 0;
-    for (int q = 0; q < 3; ++q) {
-      bs->kept_class[q] = quota[q];
-      n += quota[q];
-      units += quota[q] * (int64_t)a.p.bits[q];
-      bytes += quota[q] * row_bytes(a, q);
-    }
-    bs->kept = n;
-    bs->cost_units = units;
-    bs->packed_bytes = bytes;
-    hs->max_kept = n;
-    hs->total_packed_bytes = bytes;
-  }
-  if (g.early) {  // host-mapped mirror for the caller's early return (rtkv_compress_layer_early)
-    rtkv_early_stats* e = g.early;
-    auto put64 = [](void* dst, uint64_t v) {
-      __hip_atomic_store(reinterpret_cast<uint64_t*>(dst), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    };
-    auto put32 = [](void* dst, uint32_t v) {
-      __hip_atomic_store(reinterpret_cast<uint32_t*>(dst), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    };
-    const bool complete = !fallback && !g.withhold;  // withheld: the host takes the synchronised statistics
-    put32(&e->complete, complete ? 1u : 0u);
-    if (complete) {
-      put64(&e->stats.max_kept, (uint64_t)bs->kept);
-      put64(&e->stats.total_packed_bytes, (uint64_t)bs->packed_bytes);
-      put64(&e->stats.score_sum, __builtin_bit_cast(uint64_t, ssum));
-      put32(&e->stats.score_min, __builtin_bit_cast(uint32_t, hs->score_min));
-      put32(&e->stats.score_max, __builtin_bit_cast(uint32_t, hs->score_max));
-      put32(&e->stats.error_flags, (uint32_t)(flags | ld_sc1(&hs->error_flags)));
-      put32(&e->stats.B, 1u);
-      for (int q = 0; q < 3; ++q) {
-        put64(&e->batch.class_count[q], (uint64_t)ccount[q]);
-        put64(&e->batch.kept_class[q], (uint64_t)quota[q]);
-      }
-      put64(&e->batch.kept, (uint64_t)bs->kept);
-      put64(&e->batch.cost_units, (uint64_t)bs->cost_units);
-      put64(&e->batch.packed_bytes, (uint64_t)bs->packed_bytes);
-      put32(&e->batch.fallback, 0u);
-    }
-    __hip_atomic_store(&e->seq, g.early_seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-  }
-}
-
-// ------------------------------------------------------------------------------------ phase 3
-// Every workgroup: keep decisions for its token (s, l) still in registers, ranked across the row.
-// selw: the selection words in LDS.
-__device__ __forceinline__ void compact_phase(const FastArgs& g, float s, int l, int i, bool valid,
-                                              const uint64_t* selw) {
-  const FinalizeArgs& a = g.f;
-  __shared__ uint32_t s_f7[7][kSW];
-  __shared__ uint32_t s_f3[3][kSW];
-  __shared__ double s_d[2][kSW];
-  __shared__ uint64_t s_base[2];
-  const int t = threadIdx.x, lane = t & (kWave - 1), wid = t / kWave;
-  const int blk = blockIdx.x;
-  int mode[kGrp], tq[kGrp];
-  uint32_t thr[kGrp];
-#pragma unroll
-  for (int q = 0; q < kGrp; ++q) {
-    const uint64_t w = selw[q];
-    mode[q] = (int)((w >> 48) & 3u);
-    tq[q] = (int)((w >> 32) & 0xffffu);
-    thr[q] = (uint32_t)w;
-  }
-  const bool fallback = ((selw[0] >> 50) & 1u) != 0;
-  const double mean = __builtin_bit_cast(double, (selw[4] & 0xffffffffull) | ((selw[5] & 0xffffffffull) << 32));
-  // the class of group q's tokens at its threshold: q for a class; for the fallback group, the class
-  // of the threshold score (equal scores have equal classes)
-  const int tcls3 = class_of(key_score(thr[3]), a.p);
-  const uint32_t key = score_key(s);
-  const int e = valid ? (fallback ? 3 : l) : 4;
-  // ---- flags: surely kept (per class) and ties at T (per group); their in-workgroup ranks and
-  // totals (the aggregates, published before any wait)
-  bool f7[7] = {false, false, false, false, false, false, false};
-  bool sure = false;  // kept regardless of the tie order
-#pragma unroll
-  for (int q = 0; q < kGrp; ++q) {
-    const bool mine = e == q;
-    sure |= mine & ((mode[q] == M_ALL) | ((mode[q] == M_PART) & (key > thr[q])));
-    f7[3 + q] = mine & (mode[q] == M_PART) & (key == thr[q]);
-  }
-#pragma unroll
-  for (int c = 0; c < 3; ++c) f7[c] = sure & (l == c);  // under the token's class (also in the fallback group)
-  uint32_t r7[7], t7[7];
-  block_flag_ranks<7>(f7, r7, t7, s_f7);
-  if (wid == 0) {
-    if (lane == 0) {
-      const uint64_t x = (uint64_t)t7[0] | ((uint64_t)t7[1] << 16) | ((uint64_t)t7[2] << 32);
-      const uint64_t y = (uint64_t)t7[3] | ((uint64_t)t7[4] << 16) | ((uint64_t)t7[5] << 32) | ((uint64_t)t7[6] << 48);
-      st_sc1(&g.L.head->agg[blk][0], kTag | to11(x, 3));
-      st_sc1(&g.L.head->agg[blk][1], kTag | to11(y, 4));
-    }
-    K2_WG(6);
-    // look-back: lane p < blk waits for workgroup p's aggregate
-    const uint64_t w0 = poll_tagged(&g.L.head->agg[0][0], 2, blk, g.spin_limit, a.stats);
-    const uint64_t w1 = poll_tagged(&g.L.head->agg[0][1], 2, blk, g.spin_limit, a.stats);
-    uint64_t ps = lane < blk ? from11(w0 & ~kTag, 3) : 0ull;
-    uint64_t pt = lane < blk ? from11(w1 & ~kTag, 4) : 0ull;
-    // ties that predecessor p takes: those of its ties whose row-wide rank is below the quota
-    const uint64_t before = wave_inclusive_scan(pt) - pt;
-    uint64_t taken = 0;  // per class
-#pragma unroll
-    for (int q = 0; q < kGrp; ++q) {
-      const int b4 = (int)fld(before, q), mine_t = (int)fld(pt, q);
-      int take = tq[q] - b4;
-      take = take < 0 ? 0 : (take > mine_t ? mine_t : take);
-      taken += (uint64_t)take << (16 * (q < 3 ? q : tcls3));
-    }
-    ps = wave_sum(ps);
-    taken = wave_sum(taken);
-    pt = wave_sum(pt);
-    if (lane == 0) { s_base[0] = ps + taken; s_base[1] = pt; }
-  }
-  __syncthreads();
-  K2_WG(7);
-  const uint64_t kept_before = s_base[0], ties_before = s_base[1];
-  // ---- keep decisions (ties by their row-wide rank), then kept-row ranks per class in index order
-  bool take = false;
-#pragma unroll
-  for (int q = 0; q < kGrp; ++q) take |= f7[3 + q] & ((int)(r7[3 + q] + fld(ties_before, q)) < tq[q]);
-  const bool kept = valid & (f7[0] | f7[1] | f7[2] | take);
-  bool f3[3];
-#pragma unroll
-  for (int c = 0; c < 3; ++c) f3[c] = kept & (l == c);
-  uint32_t r3[3], t3[3];
-  block_flag_ranks<3>(f3, r3, t3, s_f3);
-  const uint64_t kept_tot = (uint64_t)t3[0] | ((uint64_t)t3[1] << 16) | ((uint64_t)t3[2] << 32);
-  K2_WG(9);
-  int64_t rb[3];
-#pragma unroll
-  for (int q = 0; q < 3; ++q) rb[q] = row_bytes(a, q);
-  if (valid) {
-    a.mask[i] = kept ? 1 : 0;
-    if (kept) {
-      const int64_t k0 = (int64_t)r3[0] + fld(kept_before, 0), k1 = (int64_t)r3[1] + fld(kept_before, 1),
-                    k2 = (int64_t)r3[2] + fld(kept_before, 2);
-      const int64_t row = k0 + k1 + k2;
-      if (row < a.row_capacity) {
-        a.kept_index[row] = i;
-        if (a.row_label) a.row_label[row] = (uint8_t)l;
-        if (a.row_offset) a.row_offset[row] = k0 * rb[0] + k1 * rb[1] + k2 * rb[2];
-      }
-    }
-  }
-  // ---- statistics: Σ kept scores, Σ (s - mean)^2 and the kept-token counts, added per workgroup
-  const double d = (double)s - mean;
-  const double ks = wave_sum(kept ? (double)s : 0.0), m2 = wave_sum(valid ? d * d : 0.0);
-  if (lane == 0) { s_d[0][wid] = ks; s_d[1][wid] = m2; }
-  __syncthreads();
-  if (wid == 0) {
-    double x = s_d[0][lane & (kSW - 1)], y = s_d[1][lane & (kSW - 1)];
-#pragma unroll
-    for (int o = kSW / 2; o > 0; o >>= 1) { x += __shfl_xor(x, o, kWave); y += __shfl_xor(y, o, kWave); }
-    if (lane == 0) {
-      rtkv_layer_stats* hs = a.stats;
-      rtkv_batch_stats* bs = reinterpret_cast<rtkv_batch_stats*>(hs + 1);
-      unsigned long long n = 0, units = 0, bytes = 0;
-      for (int q = 0; q < 3; ++q) {
-        const unsigned long long nq = fld(kept_tot, q);
-        if (nq && fallback) atomicAdd((unsigned long long*)&bs->kept_class[q], nq);
-        n += nq;
-        units += nq * (unsigned long long)a.p.bits[q];
-        bytes += nq * (unsigned long long)rb[q];
-      }
-      if (n) {
-        if (fallback) {  // otherwise phase 2 wrote the final counts (the quotas)
-          atomicAdd((unsigned long long*)&bs->kept, n);
-          atomicAdd((unsigned long long*)&bs->cost_units, units);
-          atomicAdd((unsigned long long*)&bs->packed_bytes, bytes);
-          atomicAdd((unsigned long long*)&hs->max_kept, n);
-          atomicAdd((unsigned long long*)&hs->total_packed_bytes, bytes);
-        }
-        atomicAdd(&bs->kept_score_sum, x);
-      }
-      atomicAdd(&hs->score_m2, y);
-    }
-  }
-}
-
-// ------------------------------------------------------------------------------------ kernel
-template <int TPT, bool HAS_T2, int DT>
-__global__ __launch_bounds__(kST) void fsel_kernel(FastArgs g) {
-  const FinalizeArgs& a = g.f;
-  extern __shared__ uint32_t hist_lds[];   // [kGrp][kNBin] (the rescan path's rounds)
-  __shared__ float s_mm[2][kSW];
-  __shared__ double s_sum[kSW];
-  __shared__ uint32_t s_c[5][kSW];
-  __shared__ uint64_t s_selw[8];
-  const int t = threadIdx.x, lane = t & (kWave - 1), wid = t / kWave;
-  const int S = (int)a.S;
-  K2_WG(0);
-  // ---- global min/max of A (token_importance.py:71-83): K1's per-block partials, or the row
-  float mn = INFINITY, mx = -INFINITY;
-  if (a.A_part) {
-    for (int k = t; k < a.A_nparts; k += kST) { mn = fminf(mn, a.A_part[2 * k]); mx = fmaxf(mx, a.A_part[2 * k + 1]); }
-  } else {
-    for (int k = t; k < S; k += kST) { mn = fminf(mn, a.A[k]); mx = fmaxf(mx, a.A[k]); }
-  }
-  mn = wave_min(mn);
-  mx = wave_max(mx);
-  if (lane == 0) { s_mm[0][wid] = mn; s_mm[1][wid] = mx; }
-  __syncthreads();
-  mn = s_mm[0][lane & (kSW - 1)];
-  mx = s_mm[1][lane & (kSW - 1)];
-#pragma unroll
-  for (int o = kSW / 2; o > 0; o >>= 1) { mn = fminf(mn, __shfl_xor(mn, o, kWave)); mx = fmaxf(mx, __shfl_xor(mx, o, kWave)); }
-  K2_WG(1);
-  const float den = Dt<DT>::rnd(mx - mn), eps = Dt<DT>::rnd(1e-8f);
-  // ---- phase 1: this thread's token: score, class, histogram bin + slot
-  const int i = blockIdx.x * kST + t;
-  const bool valid = i < S;
-  float s = 0.f;
-  int l = 0;
-  if (valid) {
-    const float Ai = a.A[i];
-    // Every op is an fp32 op rounded to the dtype (PyTorch CPU).  The barriers keep it so for f16:
-    // without them LLVM narrows fptrunc(fdiv(fpext h, fpext h)) to an f16 division (not correctly
-    // rounded on gfx950) and fptrunc(fmul(fpext h, f32)) to v_fma_mix (one rounding instead of two).
-    float qn = Dt<DT>::rnd(Ai - mn) / den;
-    opaque(qn);
-    const float N = (den > eps) ? Dt<DT>::rnd(qn) : 0.f;
-    float p1 = N * a.p.alpha;
-    opaque(p1);
-    float p2 = Dt<DT>::rnd(p1) * a.p.layer_weight;
-    opaque(p2);
-    const float t1 = Dt<DT>::rnd(p2);
-    const float t2 = HAS_T2 ? a.T2[i] : a.p.beta * ((S > 1) ? torch_logf((uint32_t)(i + 1)) / a.logS : 0.f);
-    s = t1 + t2;
-    s = s + a.p.gamma * a.ctx;
-    l = class_of(s, a.p);
-    st_sc1(a.scores + i, s);
-    a.labels[i] = (uint8_t)l;
-  }
-  K2_WG(2);
-  if (a.mode_select == 1) {  // wave-uniform: every lane takes part in the peer matching
-    const uint64_t entry = ((uint64_t)score_key(s) << 32) | (uint32_t)i;
-    const int b = l * kNBin + bin_of(s, bin_lo_of(g, l), bin_inv_of(g, l));
-    const uint32_t slot = hist_slot(&g.L.hist[b], (uint32_t)b, valid);
-    if (valid && slot < kCap) st_sc1(g.L.slots + (size_t)b * kCap + slot, entry);
-    if (g.hist_fb) {
-      const int b3 = 3 * kNBin + bin_of(s, g.bin_lo[3], g.bin_inv[3]);
-      const uint32_t slot3 = hist_slot(&g.L.hist[b3], (uint32_t)b3, valid);
-      if (valid && slot3 < kCap) st_sc1(g.L.slots + (size_t)b3 * kCap + slot3, entry);
-    }
-  }
-  K2_WG(3);
-  // ---- workgroup partials: class counts, score sum, score key range
-  const uint64_t b0 = __ballot(valid && l == 0), b1 = __ballot(valid && l == 1), b2 = __ballot(valid && l == 2);
-  const double sw = wave_sum(valid ? (double)s : 0.0);
-  uint32_t kmn = valid ? score_key(s) : 0xffffffffu, kmx = valid ? score_key(s) : 0u;
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    kmn = min(kmn, (uint32_t)__shfl_xor((int)kmn, o, kWave));
-    kmx = max(kmx, (uint32_t)__shfl_xor((int)kmx, o, kWave));
-  }
-  if (lane == 0) {
-    s_c[0][wid] = __popcll(b0); s_c[1][wid] = __popcll(b1); s_c[2][wid] = __popcll(b2);
-    s_c[3][wid] = kmn; s_c[4][wid] = kmx;
-    s_sum[wid] = sw;
-  }
-  __syncthreads();
-  uint64_t cw = 0;
-  if (wid == 0) {
-    const int src = lane & (kSW - 1);
-    uint32_t c0 = s_c[0][src], c1 = s_c[1][src], c2 = s_c[2][src], m0 = s_c[3][src], m1 = s_c[4][src];
-    double ss = s_sum[src];
-#pragma unroll
-    for (int o = kSW / 2; o > 0; o >>= 1) {
-      c0 += __shfl_xor(c0, o, kWave);
-      c1 += __shfl_xor(c1, o, kWave);
-      c2 += __shfl_xor(c2, o, kWave);
-      m0 = min(m0, (uint32_t)__shfl_xor((int)m0, o, kWave));
-      m1 = max(m1, (uint32_t)__shfl_xor((int)m1, o, kWave));
-      ss += __shfl_xor(ss, o, kWave);
-    }
-    cw = kTag | (uint64_t)c0 | ((uint64_t)c1 << 11) | ((uint64_t)c2 << 22);
-    if (lane == 0) {
-      FastPartial* pp = g.L.part + blockIdx.x;
-      st_sc1(&pp->ssum, ss);
-      st_sc1(&pp->kmn, m0);
-      st_sc1(&pp->kmx, m1);
-    }
-  }
-  K2_WG(4);
-  // ---- publish the counts once this workgroup's slot entries and partials are complete
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (t == 0) st_sc1(&g.L.head->part[blockIdx.x], cw);
-  // ---- phase 2 in workgroup G−1; the others wait for the selection words
-  if (blockIdx.x == gridDim.x - 1) {
-#ifdef RTKV_SELECT_PROBE
-    if (g_k2_twice) {
-      if (t == 0) g_k2_rep = 1;
-      __syncthreads();
-      select_thresholds<TPT>(g, hist_lds, s_selw);
-      __syncthreads();
-      if (t == 0) g_k2_rep = 0;
-      __syncthreads();
-    }
-#endif
-    select_thresholds<TPT>(g, hist_lds, s_selw);
-  } else if (wid == 0) {
-    const uint64_t w = poll_tagged(g.L.head->sel, 1, 6, g.spin_limit, a.stats);
-    if (lane < 6) s_selw[lane] = w;
-  }
-  __syncthreads();
-  K2_WG(5);
-  compact_phase(g, s, l, i, valid, s_selw);
-  K2_WG(8);
-}
-
-}  // namespace
 
 // ------------------------------------------------------------------------------------ host
 bool select_fast_shape(int64_t B, int64_t S) { return B == 1 && S >= 1 && S <= kMaxS; }
@@ -989,45 +42,7 @@ template <int TPT, bool HAS_T2> static int launch_fsel_dt(const FastArgs& g, int
 
 int launch_select_fast(const FinalizeArgs& f, void* ws, bool zeroed, hipStream_t st) {
   RTKV_REQUIRE(select_fast_eligible(f), "select_fast: not eligible");
-  FastArgs g;
-  g.f = f;
-  g.early = f.early;
-  g.early_seq = f.early_seq;
-  g.withhold = (f.p.flags & RTKV_TEST_WITHHOLD_SELECTION) ? 1 : 0;
-  static const uint32_t spin_limit = [] {  // RTKV_SPIN_LIMIT: polls per hand-off wait (default ≈ 2 s)
-    const char* e = getenv("RTKV_SPIN_LIMIT");
-    return e ? (uint32_t)strtoul(e, nullptr, 10) : (1u << 21);
-  }();
-  g.spin_limit = spin_limit;
-  char* p = static_cast<char*>(ws);
-  g.L.head = reinterpret_cast<FastHead*>(p);
-  p += sizeof(FastHead);
-  g.L.hist = reinterpret_cast<uint32_t*>(p);
-  p += (size_t)kGrp * kNBin * 4;
-  g.L.part = reinterpret_cast<FastPartial*>(p);
-  p += kMaxG * sizeof(FastPartial) + 256;
-  g.L.slots = reinterpret_cast<uint64_t*>((reinterpret_cast<uintptr_t>(p) + 255) & ~(uintptr_t)255);
-  // Fixed score binning.  s = t1 + t2 + t3 with t1 = α·w·N (N in [0, 1]), t2 = β·pos (pos in
-  // [0, 1]), t3 = γ·ctx: any range works for correctness (bins are clamped, the map stays
-  // monotone); this one spreads the scores over the bins.
-  const double aw = (double)f.p.alpha * (double)f.p.layer_weight, be = f.p.beta, t3 = (double)f.p.gamma * f.ctx;
-  double smin = (aw < 0 ? aw : 0.0) + (be < 0 ? be : 0.0) + t3, smax = (aw > 0 ? aw : 0.0) + (be > 0 ? be : 0.0) + t3;
-  const double pad = 1e-3 * (smax - smin) + 1e-6;
-  smin -= pad;
-  smax += pad;
-  const double th = f.p.theta_h, tm = f.p.theta_m;
-  const double lo[kGrp] = {smin, tm > smin ? tm : smin, th > smin ? th : smin, smin};
-  const double hi[kGrp] = {tm < smax ? tm : smax, th < smax ? th : smax, smax, smax};
-  for (int q = 0; q < kGrp; ++q) {
-    g.bin_lo[q] = (float)lo[q];
-    g.bin_inv[q] = hi[q] > lo[q] ? (float)(kNBin / (hi[q] - lo[q])) : 0.f;
-  }
-  {
-    const double u8 = 8.0 * ((double)f.S * f.p.propagation_ratio);
-    int wmax = 0;
-    for (int k = 0; k < 3; ++k) wmax = f.p.bits[k] > wmax ? f.p.bits[k] : wmax;
-    g.hist_fb = (f.mode_select == 1 && !(f.p.flags & RTKV_NO_FALLBACK) && !(u8 >= (double)wmax)) ? 1 : 0;
-  }
+  FastArgs g = make_fast_args(f, ws);
   if (!zeroed) {  // else K1 cleared them
     RTKV_HIP_CHECK(hipMemsetAsync(ws, 0, select_fast_zero_bytes(), st));
     RTKV_HIP_CHECK(hipMemsetAsync(f.stats, 0, rtkv_stats_bytes(f.B), st));
@@ -1037,6 +52,46 @@ int launch_select_fast(const FinalizeArgs& f, void* ws, bool zeroed, hipStream_t
   const int G = (int)((f.S + kST - 1) / kST);
   if (f.S <= 16 * kST) return f.T2 ? launch_fsel_dt<16, true>(g, G, st) : launch_fsel_dt<16, false>(g, G, st);
   return f.T2 ? launch_fsel_dt<32, true>(g, G, st) : launch_fsel_dt<32, false>(g, G, st);
+}
+
+// ------------------------------------------------------------------------------------ fused K2 + K4
+int launch_fused_f32(const FinalizeArgs& f, void* sel_ws, const QuantArgs& q, hipStream_t st);
+int launch_fused_f16(const FinalizeArgs& f, void* sel_ws, const QuantArgs& q, hipStream_t st);
+int launch_fused_bf16(const FinalizeArgs& f, void* sel_ws, const QuantArgs& q, hipStream_t st);
+
+bool fused_eligible(const FinalizeArgs& f, const QuantArgs& q) {
+  if (!select_fast_eligible(f) || !f.T2 || !f.row_label || (f.p.flags & RTKV_SEPARATE_QUANT)) return false;
+  const rtkv_kv_desc& kv = q.kv;
+  if (kv.B != 1 || kv.S != f.S || q.S_glob != 0 || q.shard_ranges || q.kept_index != f.kept_index) return false;
+  const int64_t F = kv.H * kv.D;
+  if (F != f.F || !(F == 4096 || (F == 5120 && kv.dtype != RTKV_F32))) return false;
+  if (!(kv.dtype == f.a_dtype || f.a_dtype == RTKV_F32)) return false;
+  const int esz = kv.dtype == RTKV_F32 ? 4 : 2;
+  auto al16 = [](const void* p) { return p == nullptr || ((uintptr_t)p % 16) == 0; };
+  // contiguous rows: element e of a row at e (input and dequantized output), 16-byte aligned
+  if (!(kv.H == 1 || kv.stride_h == kv.D) || (kv.stride_s * esz) % 16 != 0 || !al16(kv.k_dev) || !al16(kv.v_dev))
+    return false;
+  if (q.out.k_out_dev && (!(kv.H == 1 || q.out.o_stride_h == kv.D) || (q.out.o_stride_s * esz) % 16 != 0 ||
+                          !al16(q.out.k_out_dev) || !al16(q.out.v_out_dev)))
+    return false;
+  if (q.out.packed_k_dev) {
+    if (!al16(q.out.packed_k_dev) || !al16(q.out.packed_v_dev) || !q.out.row_offset_dev) return false;
+    for (int g = 0; g < 3; ++g) {
+      const int w = field_width(kv.dtype, q.bits[g]);
+      if (!(w == 2 || w == 4 || w == 8 || w == 16)) return false;
+    }
+  }
+  return q.out.row_capacity >= f.S;
+}
+
+int launch_select_quant_fused(const FinalizeArgs& f, void* sel_ws, const QuantArgs& q, hipStream_t st) {
+  RTKV_REQUIRE(fused_eligible(f, q), "fused selection + quantization: not eligible");
+  switch (q.kv.dtype) {
+    case RTKV_F32: return launch_fused_f32(f, sel_ws, q, st);
+    case RTKV_F16: return launch_fused_f16(f, sel_ws, q, st);
+    case RTKV_BF16: return launch_fused_bf16(f, sel_ws, q, st);
+  }
+  RTKV_REQUIRE(false, "fused selection + quantization: bad dtype");
 }
 
 }  // namespace rtkv

@@ -16,7 +16,8 @@ step() {  # step NAME SECONDS CMD...
 for s in ${STEPS:-smoke pytest bench}; do
   case $s in
     smoke)  step smoke 300 python -c "import __graft_entry__ as g; g.build(); g.smoke()" ;;
-    pytest) step pytest_gpu 1200 python -m pytest tests -m gpu -q -x -p no:cacheprovider ;;
+    pytest) step pytest_gpu 1200 python -u -m pytest tests -m gpu -q -x -p no:cacheprovider --timeout 120 --timeout-method thread ;;
+    fused)  step fused 600 python -u -m pytest tests/test_gpu_fused.py tests/test_gpu_early.py -q -x -p no:cacheprovider --timeout 120 --timeout-method thread ;;
     pytestall) step pytest_gpu 1200 python -m pytest tests -m gpu -q -p no:cacheprovider ;;
     bench)  step bench 600 python bench.py ${BENCH_ARGS:-} ;;
     prof)   step rocprof 900 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python3 bench.py --steps 5 --warmup 1 --legs none --cpu-baseline-seconds 0 ;;
