@@ -71,9 +71,9 @@ def parse():
     ap.add_argument("--cpu-baseline-seconds", type=float, default=12.0,
                     help="CPU work budget of the oracle sample (layers are added until it is spent; 0 = skip)")
     ap.add_argument("--cpu-baseline-layers", type=int, default=32, help="at most this many layers in the sample")
-    ap.add_argument("--separate-quant", action="store_true",
-                    help="run the selection and the quantization as two launches (RTKV_SEPARATE_QUANT) instead of "
-                         "the fused selection + quantization launch")
+    ap.add_argument("--fused-quant", action="store_true",
+                    help="run the selection and the quantization as ONE launch (RTKV_FUSED_QUANT, csrc/fused.h) "
+                         "instead of two")
     ap.add_argument("--quiet", action="store_true")
     ap.add_argument("--importance", default="w", choices=["w", "qk"],
                     help="w: the reference's attention-weights input (prompt slice); qk: fused mode "
@@ -151,10 +151,11 @@ class Job:
         if not (self.emit_packed or self.emit_dequant):
             raise SystemExit("--no-packed and --no-dequant together leave nothing to compute")
         flags = (L.EMIT_DEQUANT if self.emit_dequant else 0) | (L.EMIT_PACKED if self.emit_packed else 0) | \
-            (L.NO_SELECTION if quant_only else 0) | (L.SEPARATE_QUANT if args.separate_quant else 0)
-        # rtkv_compress_layer runs K2 + K4 as one launch for one batch row of <= 32768 tokens with 4096-element
-        # rows (5120 in fp16/bf16): then the K2 event interval is empty and the fused kernel is the K4 interval
-        self.fused = (not args.separate_quant and self.S <= 32768 and
+            (L.NO_SELECTION if quant_only else 0) | (L.FUSED_QUANT if args.fused_quant else 0)
+        # with --fused-quant, rtkv_compress_layer runs K2 + K4 as one launch for one batch row of <= 32768 tokens
+        # with 4096-element rows (5120 in fp16/bf16): the K2 event interval is then empty and the fused kernel
+        # is the K4 interval
+        self.fused = (args.fused_quant and self.S <= 32768 and
                       (self.F == 4096 or (self.F == 5120 and self.dtype != torch.float32)))
         prop = rtkv.SelectiveTokenPropagator(self.cfg)
         gen = torch.Generator(device=device)

@@ -67,8 +67,10 @@ enum rtkv_layer_flag {
   RTKV_NO_FALLBACK = 8,    /* skip the top-10% emergency fallback (select_tokens_with_budget alone) */
   RTKV_SELECT_PIPELINE = 16, /* use the multi-workgroup selection pipeline even where the one-workgroup
                               selection applies (B = 1, S <= 32768); same results, for cross-checks */
-  RTKV_SEPARATE_QUANT = 32, /* run the quantization as its own launch after the selection instead of the
-                              fused selection + quantization launch; same results, for cross-checks */
+  RTKV_FUSED_QUANT = 32,   /* run the selection and the quantization as ONE launch (csrc/fused.h: the
+                              quantization workgroups start on the selection's early hand-offs) where it
+                              applies (B = 1, S <= 32768, contiguous 4096/5120-element rows); same results.
+                              Off by default: measured slower than the two launches on MI355X */
   RTKV_TEST_WITHHOLD_SELECTION = 1 << 16 /* test only: the one-launch selection never publishes its
                               thresholds, so every waiting workgroup runs into its poll bound and the
                               layer reports RTKV_FLAG_SPIN_TIMEOUT instead of hanging */

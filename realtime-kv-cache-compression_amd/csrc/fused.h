@@ -9,12 +9,11 @@
 // Why: the reference caller compresses one layer at a time (modified_llama.py:113-157), so K2's ~20 µs
 // chain of cross-workgroup round trips is fully exposed between K1 and K4, with 240 of 256 CUs idle.
 // Here the quantization waves are resident from the start of the launch and
-//   1. wait for the MODE word (sel[6], sel[7]: per group ALL / PART / NONE, the fallback flag and
-//      min/max of A), which the selecting workgroup publishes as soon as the class counts give the
-//      quotas — before any histogram or threshold work;
-//   2. take tasks (token i, tensor K or V) in token order from an atomic counter, recompute the
-//      token's score with the very code phase 1 runs (token_score: bit-identical), and skip dropped
-//      tokens without reading their row: NONE → dropped, ALL → kept, PART → compare with the group's
+//   1. wait for the MODE word (sel[6]: per group ALL / PART / NONE and the fallback flag), which the
+//      selecting workgroup publishes as soon as the class counts give the quotas — before any
+//      histogram or threshold work;
+//   2. take one task each (token i, tensor K or V) in token order, read the token's score and class
+//      (tokinfo[i], a tagged word phase 1 stores), and skip dropped tokens without reading their row: NONE → dropped, ALL → kept, PART → compare with the group's
 //      threshold key (sel[q], published at the end of phase 2); ties at the threshold are decided by
 //      phase 3;
 //   3. load the row, reduce min/max and the row parameters, and only then wait for the token's output
@@ -38,6 +37,11 @@ struct FusedArgs {
   QuantArgs q;
 };
 
+__device__ __forceinline__ uint64_t uni64(uint64_t w) {  // wave-uniform copy (every lane loaded the same word)
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)w), hi = __builtin_amdgcn_readfirstlane((uint32_t)(w >> 32));
+  return ((uint64_t)hi << 32) | lo;
+}
+
 // Wave-uniform bounded wait for a tagged word (every lane loads the same address).  `broken`: a wait
 // of this wave already timed out (or another wave's did), so the layer is lost: return at once.
 __device__ __forceinline__ uint64_t wait_word(const uint64_t* p, uint32_t limit, rtkv_layer_stats* stats, bool& broken) {
@@ -52,8 +56,7 @@ __device__ __forceinline__ uint64_t wait_word(const uint64_t* p, uint32_t limit,
     __builtin_amdgcn_s_sleep(1);
     w = ld_sc1(p);
   }
-  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)w), hi = __builtin_amdgcn_readfirstlane((uint32_t)(w >> 32));
-  return ((uint64_t)hi << 32) | lo;
+  return uni64(w);
 }
 
 template <typename T> __device__ __forceinline__ T pick3(int k, T a0, T a1, T a2) { return k == 0 ? a0 : (k == 1 ? a1 : a2); }
@@ -74,17 +77,6 @@ __device__ __forceinline__ void k4_tasks(const FusedArgs& x) {
   const uint32_t ntask = 2u * (uint32_t)S;
   FastHead* head = g.L.head;
   bool broken = false;
-  // ---- the modes and the range of A (published with the quotas)
-  const uint64_t m6 = wait_word(&head->sel[6], g.spin_limit, a.stats, broken);
-  const uint64_t m7 = wait_word(&head->sel[7], g.spin_limit, a.stats, broken);
-  const float amin = __builtin_bit_cast(float, (uint32_t)(m6 >> 16)), amax = __builtin_bit_cast(float, (uint32_t)m7);
-  const bool fallback = ((m6 >> 8) & 1u) != 0;
-  int mode[kGrp];
-#pragma unroll
-  for (int k = 0; k < kGrp; ++k) mode[k] = broken ? (int)M_NONE : (int)((m6 >> (2 * k)) & 3u);
-  const float den = Dt<ADT>::rnd(amax - amin), eps = Dt<ADT>::rnd(1e-8f);
-  uint32_t thr[kGrp] = {0u, 0u, 0u, 0u};
-  bool have_thr = false;
   // ---- per-class packed widths and row bytes (selective_propagation.py byte offsets of the codes)
   int wid3[3];
   int64_t rb[3];
@@ -96,35 +88,30 @@ __device__ __forceinline__ void k4_tasks(const FusedArgs& x) {
   const bool emit_deq = q.out.k_out_dev != nullptr;
   const bool emit_pk = q.out.packed_k_dev != nullptr;
   const int nch = NCH * 64;
-  auto grab = [&]() -> uint32_t {
-    uint32_t v = 0;
-    if (lane == 0) v = atomicAdd(&head->task, 1u);
-    return __builtin_amdgcn_readfirstlane(v);
-  };
-  uint32_t t = broken ? ntask : grab();
-  while (t < ntask) {
-    const uint32_t tn = grab();  // the next task, in flight under this one
-    const int i = (int)(t >> 1), which = (int)(t & 1u);
-    t = tn;
-    // ---- keep decision from the modes (and the threshold of a partially kept group)
-    const float s = token_score<ADT, true>(a, i, a.A[i], amin, den, eps);
-    const int l = class_of(s, a.p);
-    const int e = fallback ? 3 : l;
-    const int md = pick4(e, mode);
-    if (md == M_NONE) continue;
-    if (md == M_PART) {
-      if (!have_thr) {
-#pragma unroll
-        for (int k = 0; k < kGrp; ++k) thr[k] = (uint32_t)wait_word(&head->sel[k], g.spin_limit, a.stats, broken);
-        have_thr = true;
-      }
-      if (broken || score_key(s) < pick4(e, thr)) continue;  // below the threshold: dropped, never read
-    }
+  // One task (token*2 + tensor) per wave, in token order over the quantization workgroups.  Not a
+  // persistent loop: on gfx9 one counter (vmcnt) tracks loads and stores in order, so a wave that went
+  // on to its next task would wait for its previous task's stores before its next loads could be used;
+  // a wave that ends after its stores lets them drain while a new wave starts.
+  const uint32_t t = (uint32_t)(blockIdx.x - (a.S + kST - 1) / kST) * (kST / kWave) + (uint32_t)(threadIdx.x / kWave);
+  if (t >= ntask) return;
+  {
+    const int r = (int)(t >> 1), which = (int)(t & 1u);
+    // ---- the kept row count (published with the quotas): rows beyond it end here, long before the
+    // selection is done; then this row's token, class and packed offset (phase 3)
+    const uint64_t m6 = wait_word(&head->sel[6], g.spin_limit, a.stats, broken);
+    if (broken || r >= (int)((m6 >> 16) & 0xffffffu)) return;
+    uint64_t w0 = uni64(ld_sc1(&head->rowinfo[r][0]));
+    uint64_t w1 = uni64(ld_sc1(&head->rowinfo[r][1]));
+    if (!(w0 & kTag)) w0 = wait_word(&head->rowinfo[r][0], g.spin_limit, a.stats, broken);
+    if (!(w1 & kTag)) w1 = wait_word(&head->rowinfo[r][1], g.spin_limit, a.stats, broken);
+    if (broken) return;
+    const int i = (int)(uint32_t)w0, l = (int)((w0 >> 32) & 3u);
+    if ((unsigned)i >= (unsigned)S) return;
+    const int64_t k0 = (int64_t)(w1 & 0xffffu), k1 = (int64_t)((w1 >> 16) & 0xffffu), k2 = (int64_t)((w1 >> 32) & 0xffffu);
     // ---- the row: loads in flight, min/max and the row parameters before its position is known.
-    // The lane index is made opaque per task so that the per-lane offsets of every pack width are
-    // recomputed here (a few shifts) instead of being hoisted out of the task loop as 64-bit
-    // invariants, which overflowed the 128 registers into scratch reloads (each followed by a full
-    // vmcnt wait inside the store loop).
+    // The lane index is made opaque here so that the per-lane offsets of every pack width are computed
+    // where they are used instead of early (as 64-bit values that overflowed the 128 registers into
+    // scratch, each reload followed by a full vmcnt wait inside the store loop).
     int ln = lane;
     asm volatile("" : "+v"(ln));
     int off[NCH];
@@ -139,11 +126,6 @@ __device__ __forceinline__ void k4_tasks(const FusedArgs& x) {
     row_minmax<KDT, NCH, true>(raw, nch, ln, mn, mx, anz, row_nan);
     const int bits = pick3(l, a.p.bits[0], a.p.bits[1], a.p.bits[2]);
     const RowParams rp = row_params<KDT>(mn, mx, bits, anz);
-    // ---- its output position (phase 3): kept rows of each class before it
-    const uint64_t tr = wait_word(&head->tokrow[i], g.spin_limit, a.stats, broken);
-    if (!((tr >> 48) & 1u)) continue;  // a tie at the threshold that phase 3 did not take (or broken)
-    const int64_t k0 = (int64_t)(tr & 0xffffu), k1 = (int64_t)((tr >> 16) & 0xffffu), k2 = (int64_t)((tr >> 32) & 0xffffu);
-    const int64_t r = k0 + k1 + k2;
     if (q.out.scale_zp_dev && lane < 2) q.out.scale_zp_dev[r * 4 + which * 2 + lane] = lane == 0 ? rp.scale : rp.zp;
     S_* orow = emit_deq ? static_cast<S_*>(which ? q.out.v_out_dev : q.out.k_out_dev) + r * q.out.o_stride_s : nullptr;
     uint8_t* pk = emit_pk ? (which ? q.out.packed_v_dev : q.out.packed_k_dev) + (k0 * rb[0] + k1 * rb[1] + k2 * rb[2])
@@ -167,18 +149,13 @@ __global__ __launch_bounds__(kST) void fused_kernel(FusedArgs x) {
 template <int ADT, int KDT, int NCH> int launch_fused_inst(const FusedArgs& x, hipStream_t st) {
   const size_t lds = (size_t)kGrp * kNBin * sizeof(uint32_t);
   const void* fn = (const void*)fused_kernel<ADT, KDT, NCH>;
-  static int per_cu = 0, cus = 0;  // per instantiation (one device type per process)
-  if (!per_cu) {
+  static bool attr = false;  // per instantiation
+  if (!attr) {
     RTKV_HIP_CHECK(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-    int dev = 0;
-    RTKV_HIP_CHECK(hipGetDevice(&dev));
-    RTKV_HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
-    RTKV_HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, kST, lds));
-    if (per_cu < 1) per_cu = 1;
+    attr = true;
   }
   const int G = (int)((x.g.f.S + kST - 1) / kST);
-  // enough quantization workgroups to fill the rest of the chip once; each drains the task queue
-  const int nq = cus * per_cu - G > 16 ? cus * per_cu - G : 16;
+  const int nq = (int)((2 * x.g.f.S + kST / kWave - 1) / (kST / kWave));  // one wave per (token, tensor)
   hipLaunchKernelGGL((fused_kernel<ADT, KDT, NCH>), dim3(G + nq), dim3(kST), lds, st, x);
   RTKV_HIP_CHECK(hipGetLastError());
   return RTKV_OK;

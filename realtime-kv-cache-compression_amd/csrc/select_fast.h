@@ -72,12 +72,10 @@ struct FastHead {                  // zeroed before the launch (K1 or a memset):
   uint64_t ready[kMaxG];           // phase 1, per workgroup: kTag once its slot entries, partials, scores and
                                    // classes are complete (drained)
   uint64_t sel[8];                 // phase 2: [q] kTag | fallback<<50 | mode<<48 | ties<<32 | T; [4], [5] the mean;
-                                   // [6] kTag | min(A)<<16 | fallback<<8 | mode[q]<<2q, [7] kTag | max(A) (fused)
+                                   // [6] kTag | kept rows<<16 | fallback<<8 (fused)
   uint64_t agg[kMaxG][2];          // phase 3, per workgroup: kTag | sure (3 x 11 bits), kTag | ties (4 x 11 bits)
-  uint32_t task;                   // fused: the next quantization task (token*2 + tensor), atomically taken
-  uint32_t pad[63];
-  uint64_t tokrow[kMaxS];          // fused, phase 3, per token: kTag | kept<<48 | k2<<32 | k1<<16 | k0, k_c = kept
-                                   // rows of class c before the token (its output row is k0+k1+k2)
+  uint64_t rowinfo[kMaxS][2];      // fused, phase 3, per kept row r: {kTag | class<<32 | token, kTag | k2<<32 |
+                                   // k1<<16 | k0}, k_c = kept rows of class c before it (its packed offset)
 };
 struct FastPartial {               // phase 1, per workgroup (complete before its counts word)
   double ssum;
@@ -431,8 +429,7 @@ __device__ __forceinline__ void rescan_thresholds(const FastArgs& g, uint32_t* h
 // selection words and the statistics.  s_selw receives the selection words (thread 0 writes them;
 // the caller's barrier publishes them to the workgroup).
 template <int TPT>
-__device__ __forceinline__ void select_thresholds(const FastArgs& g, uint32_t* hist_lds, uint64_t* s_selw, float amin,
-                                                  float amax) {
+__device__ __forceinline__ void select_thresholds(const FastArgs& g, uint32_t* hist_lds, uint64_t* s_selw) {
   const FinalizeArgs& a = g.f;
   __shared__ uint32_t s_scan32[kGrp][kSW];
   __shared__ uint32_t s_pick[kGrp][3];
@@ -485,11 +482,9 @@ __device__ __forceinline__ void select_thresholds(const FastArgs& g, uint32_t* h
       s_q[kGrp + 3] = (int)kf;
       md[3] = !fb ? M_NONE : (kf >= S ? M_ALL : M_PART);
       s_q[3] = md[3];
-      if (g.fused && !g.withhold) {  // the modes: the quantization waves start on ALL-mode rows now
-        uint64_t m = (uint64_t)(fb ? 1 : 0) << 8;
-        for (int q = 0; q < kGrp; ++q) m |= (uint64_t)md[q] << (2 * q);
-        st_sc1(&g.L.head->sel[7], kTag | (uint64_t)__builtin_bit_cast(uint32_t, amax));
-        st_sc1(&g.L.head->sel[6], kTag | ((uint64_t)__builtin_bit_cast(uint32_t, amin) << 16) | m);
+      if (g.fused && !g.withhold) {  // the kept row count: quantization waves of rows beyond it end now
+        const int64_t nkept = fb ? (kf < S ? kf : S) : kept;
+        st_sc1(&g.L.head->sel[6], kTag | ((uint64_t)nkept << 16) | ((uint64_t)(fb ? 1 : 0) << 8));
       }
     }
   } else if (wid == 1) {
@@ -787,7 +782,6 @@ __device__ __forceinline__ void compact_phase(const FastArgs& g, float s, int l,
   for (int q = 0; q < 3; ++q) rb[q] = row_bytes(a, q);
   if (valid) {
     a.mask[i] = kept ? 1 : 0;
-    uint64_t tr = kTag;
     if (kept) {
       const int64_t k0 = (int64_t)r3[0] + fld(kept_before, 0), k1 = (int64_t)r3[1] + fld(kept_before, 1),
                     k2 = (int64_t)r3[2] + fld(kept_before, 2);
@@ -796,10 +790,12 @@ __device__ __forceinline__ void compact_phase(const FastArgs& g, float s, int l,
         a.kept_index[row] = i;
         if (a.row_label) a.row_label[row] = (uint8_t)l;
         if (a.row_offset) a.row_offset[row] = k0 * rb[0] + k1 * rb[1] + k2 * rb[2];
+        if (g.fused) {  // the fused quantization waves of row `row` wait on it
+          st_sc1(&g.L.head->rowinfo[row][0], kTag | ((uint64_t)l << 32) | (uint32_t)i);
+          st_sc1(&g.L.head->rowinfo[row][1], kTag | ((uint64_t)k2 << 32) | ((uint64_t)k1 << 16) | (uint64_t)k0);
+        }
       }
-      tr |= (1ull << 48) | ((uint64_t)k2 << 32) | ((uint64_t)k1 << 16) | (uint64_t)k0;
     }
-    if (g.fused) st_sc1(&g.L.head->tokrow[i], tr);  // the fused quantization wave of token i waits on it
   }
   // ---- statistics: Σ kept scores, Σ (s - mean)^2 and the kept-token counts, added per workgroup
   const double d = (double)s - mean;
@@ -911,7 +907,8 @@ __device__ __forceinline__ void amin_amax(const FinalizeArgs& a, float& mn, floa
 // fptrunc(fmul(fpext h, f32)) to v_fma_mix (one rounding instead of two).  The fused kernel's
 // quantization waves recompute it with this same code: bit-identical to the score phase 1 stores.
 template <int DT, bool HAS_T2>
-__device__ __forceinline__ float token_score(const FinalizeArgs& a, int i, float Ai, float mn, float den, float eps) {
+__device__ __forceinline__ float token_score(const FinalizeArgs& a, int i, float Ai, float T2i, float mn, float den,
+                                             float eps) {
   float qn = Dt<DT>::rnd(Ai - mn) / den;
   opaque(qn);
   const float N = (den > eps) ? Dt<DT>::rnd(qn) : 0.f;
@@ -920,7 +917,7 @@ __device__ __forceinline__ float token_score(const FinalizeArgs& a, int i, float
   float p2 = Dt<DT>::rnd(p1) * a.p.layer_weight;
   opaque(p2);
   const float t1 = Dt<DT>::rnd(p2);
-  const float t2 = HAS_T2 ? a.T2[i] : a.p.beta * ((a.S > 1) ? torch_logf((uint32_t)(i + 1)) / a.logS : 0.f);
+  const float t2 = HAS_T2 ? T2i : a.p.beta * ((a.S > 1) ? torch_logf((uint32_t)(i + 1)) / a.logS : 0.f);
   float s = t1 + t2;
   s = s + a.p.gamma * a.ctx;
   return s;
@@ -948,7 +945,7 @@ __device__ __forceinline__ void k2_body(const FastArgs& g, uint32_t* hist_lds) {
   float s = 0.f;
   int l = 0;
   if (valid) {
-    s = token_score<DT, HAS_T2>(a, i, a.A[i], mn, den, eps);
+    s = token_score<DT, HAS_T2>(a, i, a.A[i], HAS_T2 ? a.T2[i] : 0.f, mn, den, eps);
     l = class_of(s, a.p);
     st_sc1(a.scores + i, s);
     a.labels[i] = (uint8_t)l;
@@ -1020,13 +1017,13 @@ __device__ __forceinline__ void k2_body(const FastArgs& g, uint32_t* hist_lds) {
     if (g_k2_twice) {
       if (t == 0) g_k2_rep = 1;
       __syncthreads();
-      select_thresholds<TPT>(g, hist_lds, s_selw, mn, mx);
+      select_thresholds<TPT>(g, hist_lds, s_selw);
       __syncthreads();
       if (t == 0) g_k2_rep = 0;
       __syncthreads();
     }
 #endif
-    select_thresholds<TPT>(g, hist_lds, s_selw, mn, mx);
+    select_thresholds<TPT>(g, hist_lds, s_selw);
   } else if (wid == 0) {
     const uint64_t w = poll_tagged(g.L.head->sel, 1, 6, g.spin_limit, a.stats);
     if (lane < 6) s_selw[lane] = w;

@@ -60,7 +60,7 @@ int launch_fused_f16(const FinalizeArgs& f, void* sel_ws, const QuantArgs& q, hi
 int launch_fused_bf16(const FinalizeArgs& f, void* sel_ws, const QuantArgs& q, hipStream_t st);
 
 bool fused_eligible(const FinalizeArgs& f, const QuantArgs& q) {
-  if (!select_fast_eligible(f) || !f.T2 || !f.row_label || (f.p.flags & RTKV_SEPARATE_QUANT)) return false;
+  if (!(f.p.flags & RTKV_FUSED_QUANT) || !select_fast_eligible(f) || !f.T2 || !f.row_label) return false;
   const rtkv_kv_desc& kv = q.kv;
   if (kv.B != 1 || kv.S != f.S || q.S_glob != 0 || q.shard_ranges || q.kept_index != f.kept_index) return false;
   const int64_t F = kv.H * kv.D;

@@ -18,7 +18,7 @@ LIB_PATH = os.environ.get("RTKV_LIB", os.path.join(ROOT, "librtkv.so"))
 
 F32, F16, BF16 = 0, 1, 2
 EMIT_DEQUANT, EMIT_PACKED, NO_SELECTION, NO_FALLBACK, SELECT_PIPELINE = 1, 2, 4, 8, 16
-SEPARATE_QUANT = 32
+FUSED_QUANT = 32
 TEST_WITHHOLD_SELECTION = 1 << 16
 FLAG_F16_QMAX_OVERFLOW, FLAG_SPIN_TIMEOUT = 1, 2
 ERR_NAMES = {-1: "RTKV_ERR_INVALID", -2: "RTKV_ERR_UNSUPPORTED", -3: "RTKV_ERR_HIP", -4: "RTKV_ERR_WORKSPACE",

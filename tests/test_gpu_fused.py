@@ -1,6 +1,6 @@
-"""GPU: the fused selection + quantization launch (csrc/fused.h), taken by rtkv_compress_layer for one
-batch row of S <= 32768 tokens with contiguous 4096- or 5120-element rows, against the same layer run
-as two launches (RTKV_SEPARATE_QUANT: select_fast.hip's K2, then quant_rows_kernel) and, at sizes the
+"""GPU: the fused selection + quantization launch (csrc/fused.h, opt-in with RTKV_FUSED_QUANT; taken
+for one batch row of S <= 32768 tokens with contiguous 4096- or 5120-element rows), against the same
+layer run as two launches (the default: select_fast.hip's K2, then quant_rows_kernel) and, at sizes the
 oracle finishes quickly, against the C oracle.
 
 Every output must agree byte for byte: scores, classes, mask, kept indices, row offsets, packed codes,
@@ -101,7 +101,9 @@ CASES = [
     (4096, 4096, "float32", 0.6, {}, "rand"),
     (4096, 4096, "float16", 1.0, {}, "rand"),          # everything fits: every class ALL
     (4097, 5120, "bfloat16", 0.8, {}, "rand"),
-    (3000, 5120, "float16", 0.5, dict(low_precision_bits=4, medium_precision_bits=8, high_precision_bits=16), "rand"),
+    (3000, 5120, "float16", 0.5, {}, "rand"),
+    (3000, 5120, "bfloat16", 0.5, dict(low_precision_bits=4, medium_precision_bits=8, high_precision_bits=16),
+     "rand"),                                           # bf16 16-bit codes are 17 bits wide: two launches
     (4000, 4096, "float32", 0.5, dict(low_precision_bits=4, medium_precision_bits=8, high_precision_bits=16), "rand"),
     (3000, 4096, "float16", 0.0004, {}, "rand"),       # budget below one row: the top-10% fallback
     (4096, 4096, "float16", 0.5, dict(beta=0.0), "tie"),  # threshold inside a block of equal scores
@@ -124,8 +126,8 @@ def test_fused_matches_two_launches_and_oracle(S, F, dtype, ratio, over, kind):
     (Kd, Vd, Wd), host = gen(900 + S, S, F, H, P, dtype, kind)
     kw = dict(COV, **over)
     base = L.EMIT_DEQUANT | L.EMIT_PACKED
-    a, sa = run(Kd, Vd, Wd, S, F, dtype, kw, 1, ratio, base)
-    b, sb = run(Kd, Vd, Wd, S, F, dtype, kw, 1, ratio, base | L.SEPARATE_QUANT)
+    a, sa = run(Kd, Vd, Wd, S, F, dtype, kw, 1, ratio, base | L.FUSED_QUANT)
+    b, sb = run(Kd, Vd, Wd, S, F, dtype, kw, 1, ratio, base)
     same(a, b)
     assert (sa.max_kept, sa.total_packed_bytes, sa.error_flags) == (sb.max_kept, sb.total_packed_bytes, sb.error_flags)
     assert sa.error_flags == 0 and sa.max_kept >= 1
@@ -157,8 +159,8 @@ def test_fused_single_output_modes(outputs, dtype):
     (Kd, Vd, Wd), _ = gen(55, S, F, 32, 128, dtype, "big")
     fl = L.EMIT_PACKED if outputs == "packed" else L.EMIT_DEQUANT
     for extra in (0, L.NO_SELECTION):
-        a, sa = run(Kd, Vd, Wd, S, F, dtype, COV, 2, 0.5, fl | extra)
-        b, sb = run(Kd, Vd, Wd, S, F, dtype, COV, 2, 0.5, fl | extra | L.SEPARATE_QUANT)
+        a, sa = run(Kd, Vd, Wd, S, F, dtype, COV, 2, 0.5, fl | extra | L.FUSED_QUANT)
+        b, sb = run(Kd, Vd, Wd, S, F, dtype, COV, 2, 0.5, fl | extra)
         same(a, b)
         assert sa.max_kept == sb.max_kept and (sa.max_kept == S) == bool(extra)
 
@@ -176,7 +178,7 @@ def test_fused_qk_mode_matches_two_launches():
     lse = rtkv.attention_lse(Q, K, k_layout="bsf")
     cfg = rtkv.CompressionConfig(num_hidden_layers=1, layer_weights=[1.0], **COV)
     outs = []
-    for extra in (0, L.SEPARATE_QUANT):
+    for extra in (L.FUSED_QUANT, 0):
         p = rtkv.params_from_config(cfg, 0, rtkv.prompt_length(S), 0.6, L.EMIT_DEQUANT | L.EMIT_PACKED | extra)
         bufs = rtkv.LayerBuffers(1, S, H * D, torch.float16, "cuda", (2, 4, 8))
         st = rtkv.compress_layer_qk(K, V, Q, lse, p, bufs, rtkv.Workspace("cuda")).final_stats()
