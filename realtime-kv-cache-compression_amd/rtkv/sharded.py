@@ -167,12 +167,15 @@ class ShardedPrefillCompressor:
         if self.overlap:
             ranks = dist.get_process_group_ranks(self.group) if self.group is not None else list(range(self.world))
             self.xgroup = dist.new_group(ranks=ranks)
-        # collectives: "torch" (torch.distributed on the group) or "rtkv" (the C ABI's RCCL
-        # communicators: rtkv_allgather_rows for A, rtkv_allgather_packed for the exchange on its own
-        # stream), the path a host binding of include/rtkv.h takes
-        if collectives not in ("torch", "rtkv"):
-            raise ValueError("collectives: 'torch' or 'rtkv'")
+        # collectives: "torch" (torch.distributed on the group), "rtkv" (the C ABI's RCCL communicators:
+        # rtkv_allgather_rows for A, rtkv_allgather_packed for the exchange on its own stream, the path a
+        # host binding of include/rtkv.h takes) or "host" (the same exchanges staged through host memory,
+        # for a group whose backend does not take device tensors, e.g. gloo: ranks sharing one GPU, or a
+        # node without RCCL)
+        if collectives not in ("torch", "rtkv", "host"):
+            raise ValueError("collectives: 'torch', 'rtkv' or 'host'")
         self.collectives = collectives
+        self._host = collectives == "host" and self.device.type == "cuda"
         self.comm = self.xcomm = self._xstream = None
         if collectives == "rtkv":
             if self.device.type != "cuda":
@@ -247,7 +250,12 @@ class ShardedPrefillCompressor:
             kp = self._prompt_keys[(B, P, F, K.dtype)] = torch.empty(B, P, F, dtype=K.dtype, device=self.device)
         if self.rank == 0:
             kp.copy_(K[:, :P])
-        dist.broadcast(kp, src=self._peer_rank(0), group=self.group)
+        if self._host:
+            kh = kp.cpu()
+            dist.broadcast(kh, src=self._peer_rank(0), group=self.group)
+            kp.copy_(kh)
+        else:
+            dist.broadcast(kp, src=self._peer_rank(0), group=self.group)
         self.stages.aggregate_qk(Q, kp, lse, P, row0, causal, A_local)
         return self._select_and_quantize(K, V, layout, layer_idx, p, bufs, L.F32)
 
@@ -271,7 +279,12 @@ class ShardedPrefillCompressor:
             self.comm.allgather_rows(A_local, A)  # straight into token order, any B
             A_glob = A
         else:
-            dist.all_gather_into_tensor(A_parts.view(-1), A_local.view(-1), group=self.group)
+            if self._host:
+                parts = torch.empty(A_parts.numel(), dtype=A_parts.dtype)
+                dist.all_gather_into_tensor(parts, A_local.reshape(-1).cpu(), group=self.group)
+                A_parts.view(-1).copy_(parts)
+            else:
+                dist.all_gather_into_tensor(A_parts.view(-1), A_local.view(-1), group=self.group)
             if B == 1:
                 A_glob = A_parts.view(1, S_total)  # rank-major = token order
             else:
@@ -338,6 +351,19 @@ class ShardedPrefillCompressor:
                 for (lo, hi), buf in ((spans[j][0], g.packed_k), (spans[j][0], g.packed_v), (spans[j][1], sz)):
                     if hi > lo:
                         ops.append(dist.P2POp(dist.irecv, buf[lo:hi], peer, group))
+        if self._host and ops:  # stage the byte ranges through host memory
+            staged, back = [], []
+            for op in ops:
+                h = op.tensor.cpu() if op.op is dist.isend else torch.empty(op.tensor.shape, dtype=op.tensor.dtype)
+                staged.append(dist.P2POp(op.op, h, op.peer, op.group))
+                if op.op is not dist.isend:
+                    back.append((op.tensor, h))
+            works = dist.batch_isend_irecv(staged)
+            for w in works:
+                w.wait()
+            for dst, h in back:
+                dst.copy_(h)
+            return []
         return dist.batch_isend_irecv(ops) if ops else []
 
     def _rtkv_exchange(self, sl: ShardLayer):

@@ -219,3 +219,74 @@ def test_rtkv_collectives_single_rank():
                 assert torch.equal(x, y)
     finally:
         dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("name,dtype,S_total,world,H,D,ratio", [
+    ("cfg4", "float32", 65536, 8, 32, 128, 0.6),    # BASELINE configs[3]: 7B, S = 65536 over 8 ranks
+    ("cfg4", "float16", 65536, 8, 32, 128, 0.4),
+    ("cfg5", "float32", 32768, 8, 40, 128, 0.8),    # configs[4]: 13B shape (40 heads, F = 5120) over 8 ranks
+    ("cfg5", "bfloat16", 32768, 8, 40, 128, 0.4),
+])
+def test_shards_union_equals_single_gpu_at_config_size(name, dtype, S_total, world, H, D, ratio):
+    """The 8-way sequence-shard split at BASELINE's multi-GPU sizes (inputs generated on the device):
+    S_total = 65536 takes the pipeline selection in rtkv_finalize_select (S > 32768) on every rank, and
+    rtkv_shard_ranges / rtkv_quantize_rows_shard split it 8 ways; the union equals the single-GPU
+    rtkv_compress_layer byte for byte."""
+    import rtkv
+    from rtkv import _lib as L
+    from rtkv.sharded import HipShardStages, ShardBuffers
+    F = H * D
+    P = rtkv.prompt_length(S_total)
+    td = getattr(torch, dtype)
+    g = torch.Generator(device="cuda").manual_seed(S_total + H)
+    Kd = torch.randn(1, S_total, F, device="cuda", generator=g).to(td)
+    Vd = torch.randn(1, S_total, F, device="cuda", generator=g).to(td)
+    u = torch.rand(1, H, S_total, P, device="cuda", generator=g)
+    Wd = (u * u) ** 2 + 1e-6
+    Wd = Wd * (torch.arange(P, device="cuda")[None, :] <= torch.arange(S_total, device="cuda")[:, None])
+    Wd = (Wd / Wd.sum(-1, keepdim=True) * torch.rand(1, H, S_total, 1, device="cuda", generator=g)).to(td)
+    del u
+    cfg = rtkv.CompressionConfig(alpha=0.8, beta=0.1, gamma=0.1, theta_h=0.4, theta_m=0.25, num_hidden_layers=1,
+                                 layer_weights=[1.0], high_precision_bits=8, medium_precision_bits=4,
+                                 low_precision_bits=2)
+    params = rtkv.params_from_config(cfg, 0, P, ratio, L.EMIT_DEQUANT | L.EMIT_PACKED)
+    bits = (2, 4, 8)
+    ref = rtkv.LayerBuffers(1, S_total, F, td, "cuda", bits)
+    res = rtkv.compress_layer(Kd, Vd, Wd, params, ref, rtkv.Workspace("cuda"))
+    st = res.final_stats()
+    k_ref, v_ref = res.kv()
+    n, tot = st.max_kept, st.total_packed_bytes
+    assert 0 < n < S_total
+    S_local = S_total // world
+    stages = HipShardStages("cuda")
+    A = torch.empty(1, S_total, dtype=torch.float32, device="cuda")
+    for j in range(world):
+        sl = slice(j * S_local, (j + 1) * S_local)
+        stages.aggregate(Wd[:, :, sl].contiguous(), P, j * S_local, S_total, A[:, sl])
+    pk = torch.zeros_like(ref.packed_k)
+    pv = torch.zeros_like(ref.packed_v)
+    sz = torch.zeros_like(ref.scale_zp)
+    bufs = ShardBuffers(1, S_local, world, F, td, "cuda", bits)  # one rank's buffers, reused rank after rank
+    for j in range(world):
+        stages.finalize(A, L.TORCH_DTYPE_CODE[td], params, bufs)
+        stages.ranges(bufs, world)
+        sl = slice(j * S_local, (j + 1) * S_local)
+        stages.quantize(Kd[:, sl].contiguous(), Vd[:, sl].contiguous(), "bsf", j * S_local, j, world, params, bufs)
+        torch.cuda.synchronize()
+        gb = bufs.g
+        assert torch.equal(gb.scores, ref.scores) and torch.equal(gb.mask, ref.mask)
+        assert torch.equal(gb.kept_index[:, :n], ref.kept_index[:, :n])
+        assert torch.equal(gb.row_offset[:, :n], ref.row_offset[:, :n])
+        rg = bufs.ranges.cpu()
+        assert int(rg[0, -1, 0]) == n and int(rg[0, -1, 1]) == tot
+        r0, r1 = int(rg[0, j, 0]), int(rg[0, j + 1, 0])
+        b0, b1 = int(rg[0, j, 1]), int(rg[0, j + 1, 1])
+        assert r1 > r0, f"rank {j} keeps no row"
+        pk[b0:b1] = gb.packed_k[b0:b1]
+        pv[b0:b1] = gb.packed_v[b0:b1]
+        sz[:, r0:r1] = gb.scale_zp[:, r0:r1]
+        assert torch.equal(bufs.k_local[:, : r1 - r0], k_ref[:, r0:r1]), f"rank {j} local K'"
+        assert torch.equal(bufs.v_local[:, : r1 - r0], v_ref[:, r0:r1]), f"rank {j} local V'"
+    assert torch.equal(pk[:tot], ref.packed_k[:tot])
+    assert torch.equal(pv[:tot], ref.packed_v[:tot])
+    assert torch.equal(sz[:, :n], ref.scale_zp[:, :n])
