@@ -60,9 +60,14 @@ def parse():
                     help="K/V/attention dtype (default: the reference model's fp32)")
     ap.add_argument("--no-packed", action="store_true", help="skip the packed-code output")
     ap.add_argument("--no-dequant", action="store_true", help="skip the dequantized K'/V' output (packed only)")
-    ap.add_argument("--legs", default="f16,packed_only,drop_in,s4096,cfg2_s4096_quant,s65536,independent_layers",
+    ap.add_argument("--legs", default="f16,packed_only,drop_in,s4096,cfg2_s4096_quant,s65536,independent_layers,"
+                                      "prefill_7b",
                     help="extra single-GPU legs after the main line: comma list of f16, packed_only, drop_in, "
-                         "s4096, cfg2_s4096_quant, s65536, independent_layers (or 'none')")
+                         "s4096, cfg2_s4096_quant, s65536, independent_layers, prefill_7b (or 'none')")
+    ap.add_argument("--prefill-dtype", default="float16", choices=["float16", "bfloat16", "float32"],
+                    help="dtype of the prefill_7b leg's random-init model")
+    ap.add_argument("--prefill-modes", default="none,fused,eager",
+                    help="prefill_7b attention variants (tools/prefill_model.py): none, fused, eager")
     ap.add_argument("--streams", type=int, default=1,
                     help="single GPU: consecutive layers go to this many streams (layer l on stream l %% n, one "
                          "workspace each).  Default 1: strictly sequential, the reference caller's order "
@@ -523,9 +528,6 @@ def kernel_us(job, kus):
 
 def main():
     args = parse()
-    if args.importance == "qk" and args.dtype == "float32":
-        raise SystemExit("bench.py: --importance qk runs the MFMA kernels, which take float16 or bfloat16 "
-                         "states: add --dtype float16 (or bfloat16)")
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -655,6 +657,13 @@ def main():
                     if leg.slots < args.layers:
                         legs[name]["inputs"] = f"{leg.slots} distinct layer inputs cycled over {args.layers} layers"
                     del leg
+                elif name == "prefill_7b":
+                    # sync'd prefill wall time of a random-init 7B-shaped model at S (TTFT as
+                    # benchmark runner.py:202-212 measures it), with / without compression
+                    sys.path.insert(0, os.path.join(REPO, "tools"))
+                    from prefill_model import prefill_leg
+                    legs["prefill_7b"] = prefill_leg(device, S=job.S, dtype=getattr(torch, args.prefill_dtype),
+                                                     modes=tuple(args.prefill_modes.split(",")))
                 elif name == "drop_in":
                     legs["drop_in"] = drop_in_leg(args, job, args.leg_steps, 2)
                     legs["drop_in"]["raw_driver_ms_per_layer"] = round(ms_per_step / args.layers, 4)

@@ -129,7 +129,7 @@ typedef struct rtkv_qk_desc {
   const void* q_dev;
   const void* k_dev;
   const float* lse_dev;
-  int32_t dtype;                       /* RTKV_F16 or RTKV_BF16 (MFMA operands) */
+  int32_t dtype;                       /* RTKV_F16, RTKV_BF16 (16x16x32 MFMA) or RTKV_F32 (16x16x4 f32 MFMA) */
   int32_t causal;
   int64_t B, H, Hkv, S, D;
   int64_t q_stride_b, q_stride_h, q_stride_s;
@@ -138,6 +138,14 @@ typedef struct rtkv_qk_desc {
   float scale;                         /* 1/sqrt(head_dim) in the reference (modified_llama.py:89) */
   int32_t reserved;
   int64_t row0;                        /* global position of query row 0 (sequence shards), else 0 */
+  /* Optional additive key bias kbias[b, j] (fp32, at kbias_dev + b*kbias_stride_b + j; null: none): the
+   * key-padding part of the model's attention_mask (modified_llama.py:90-91), 0 for a real key and
+   * -inf (or any value below -1e30, e.g. the mask's finfo.min) for a padding key.  A query row that
+   * sees no key at all (a padding row) gets lse = -inf, and its softmax is the uniform 1/S the
+   * reference's all-masked row has (every logit equal).  Supported by rtkv_attention_lse and the
+   * fused-mode K1' with head_dim 128. */
+  const float* kbias_dev;
+  int64_t kbias_stride_b;
 } rtkv_qk_desc;
 
 /* Per-batch-row statistics (device-resident; one entry per batch row after the header). */
@@ -309,6 +317,23 @@ int rtkv_compress_layer_qk_early(const rtkv_kv_desc* kv, const rtkv_qk_desc* q, 
                                  void* stream, rtkv_early_stats* early_host, uint64_t seq, int32_t* published);
 /* Spin until early_host->seq == seq (RTKV_OK) or timeout_us passes (RTKV_ERR_TIMEOUT). */
 int rtkv_wait_early(const rtkv_early_stats* early_host, uint64_t seq, int64_t timeout_us);
+
+/* The layer in two calls, for exactly-sized outputs (the drop-in: the reference returns K'/V' of S'
+ * rows, unified_compressor.py:170 / selective_propagation.py:214-232).  rtkv_compress_layer_begin runs
+ * K1 and K2 and publishes the early statistics as rtkv_compress_layer_early does; `out` needs only
+ * the per-token buffers (scores, labels, mask, kept_index, row_offset, scale_zp, stats; row_capacity
+ * >= S).  With S' and the packed byte count known (rtkv_wait_early, or stats_dev after a stream sync
+ * when *published = 0), the caller allocates K'/V' of [B, S', F] and packed buffers of exactly that
+ * many bytes and calls rtkv_compress_layer_finish (K4) with the same per-token buffers, the same
+ * row_capacity and workspace, o_stride_b = -1, on the same stream. */
+int rtkv_compress_layer_begin(const rtkv_kv_desc* kv, const rtkv_attn_desc* w, const rtkv_layer_params* p,
+                              const rtkv_layer_out* out, void* workspace_dev, size_t workspace_bytes, void* stream,
+                              rtkv_early_stats* early_host, uint64_t seq, int32_t* published);
+int rtkv_compress_layer_qk_begin(const rtkv_kv_desc* kv, const rtkv_qk_desc* q, const rtkv_layer_params* p,
+                                 const rtkv_layer_out* out, void* workspace_dev, size_t workspace_bytes, void* stream,
+                                 rtkv_early_stats* early_host, uint64_t seq, int32_t* published);
+int rtkv_compress_layer_finish(const rtkv_kv_desc* kv, const rtkv_layer_params* p, const rtkv_layer_out* out,
+                               void* workspace_dev, size_t workspace_bytes, void* stream);
 /* Pinned, device-coherent host memory for rtkv_early_stats (hipHostMalloc, coherent + mapped). */
 void* rtkv_host_alloc(size_t bytes);
 void rtkv_host_free(void* p);

@@ -203,12 +203,13 @@ int rtkv_quantize_rows(const rtkv_kv_desc* kv, const uint8_t* labels_dev, const 
   return quantize_rows_impl(kv, labels_dev, kept_index_dev, p, out, stream, nullptr);
 }
 
-// The fused layer: K1 (W aggregation, or K1' on MFMA when q != null) → K2 → K4.
+// The fused layer: K1 (W aggregation, or K1' on MFMA when q != null) → K2 → K4.  stop_after_select: the
+// first half of rtkv_compress_layer_begin / _finish (K1 and K2 only; the caller sizes the outputs).
 static int compress_layer_impl(const rtkv_kv_desc* kv, const rtkv_attn_desc* w, const rtkv_qk_desc* qk,
                                const rtkv_layer_params* p, const rtkv_layer_out* out, void* workspace_dev,
                                size_t workspace_bytes, void* stream, void* const events[4],
                                rtkv_early_stats* early = nullptr, uint64_t early_seq = 0,
-                               int32_t* published = nullptr) {
+                               int32_t* published = nullptr, bool stop_after_select = false) {
   if (published) *published = 0;
   int rc = check_params(p);
   if (rc) return rc;
@@ -219,15 +220,18 @@ static int compress_layer_impl(const rtkv_kv_desc* kv, const rtkv_attn_desc* w, 
                "compress_layer needs scores, labels, mask, kept_index and stats outputs");
   RTKV_REQUIRE(out->row_capacity >= kv->S, "row_capacity must be >= S (every token may be kept)");
   if (p->flags & RTKV_EMIT_PACKED) {
-    RTKV_REQUIRE(out->packed_k_dev && out->packed_v_dev && out->row_offset_dev && out->scale_zp_dev,
-                 "EMIT_PACKED needs packed_k, packed_v, row_offset and scale_zp outputs");
+    RTKV_REQUIRE(out->row_offset_dev && out->scale_zp_dev, "EMIT_PACKED needs row_offset and scale_zp outputs");
     for (int g = 0; g < 3; ++g)
       RTKV_REQUIRE(field_width(kv->dtype, p->bits[g]) > 0, "packed codes unsupported for this dtype/bits");
-    RTKV_REQUIRE(out->packed_capacity >= rtkv_packed_capacity(kv->B, out->row_capacity < kv->S ? out->row_capacity : kv->S,
-                                                             kv->H * kv->D, kv->dtype, p->bits),
-                 "packed_capacity too small");
+    if (!stop_after_select) {
+      RTKV_REQUIRE(out->packed_k_dev && out->packed_v_dev, "EMIT_PACKED needs packed_k and packed_v outputs");
+      RTKV_REQUIRE(out->packed_capacity >= rtkv_packed_capacity(kv->B, out->row_capacity < kv->S ? out->row_capacity : kv->S,
+                                                               kv->H * kv->D, kv->dtype, p->bits),
+                   "packed_capacity too small");
+    }
   }
-  if (p->flags & RTKV_EMIT_DEQUANT) RTKV_REQUIRE(out->k_out_dev && out->v_out_dev, "EMIT_DEQUANT needs k_out and v_out");
+  if ((p->flags & RTKV_EMIT_DEQUANT) && !stop_after_select)
+    RTKV_REQUIRE(out->k_out_dev && out->v_out_dev, "EMIT_DEQUANT needs k_out and v_out");
   Workspace ws;
   rc = carve(workspace_dev, workspace_bytes, kv->B, kv->S, ws);
   if (rc) return rc;
@@ -287,6 +291,11 @@ static int compress_layer_impl(const rtkv_kv_desc* kv, const rtkv_attn_desc* w, 
     a.early_seq = early_seq;
     if (published) *published = 1;
   }
+  if (stop_after_select) {
+    rc = launch_select(a, ws.sel, true, st);
+    if (rc) return rc;
+    return mark(2);
+  }
   const QuantArgs q = make_quant_args(kv, out->labels_dev, out->kept_index_dev, p, out, row_labels ? ws.labels : nullptr);
   if (fused_eligible(a, q)) {  // K2 + K4 in one launch (fused.h): events 1 and 2 mark the same point
     if ((rc = mark(2))) return rc;
@@ -328,6 +337,45 @@ int rtkv_compress_layer_qk_early(const rtkv_kv_desc* kv, const rtkv_qk_desc* q, 
   RTKV_REQUIRE(q != nullptr && early_host != nullptr, "null query descriptor or early-stats buffer");
   return compress_layer_impl(kv, nullptr, q, p, out, workspace_dev, workspace_bytes, stream, nullptr, early_host,
                              seq, published);
+}
+
+int rtkv_compress_layer_begin(const rtkv_kv_desc* kv, const rtkv_attn_desc* w, const rtkv_layer_params* p,
+                              const rtkv_layer_out* out, void* workspace_dev, size_t workspace_bytes, void* stream,
+                              rtkv_early_stats* early_host, uint64_t seq, int32_t* published) {
+  RTKV_REQUIRE(w != nullptr, "null attention descriptor");
+  return compress_layer_impl(kv, w, nullptr, p, out, workspace_dev, workspace_bytes, stream, nullptr, early_host, seq,
+                             published, true);
+}
+
+int rtkv_compress_layer_qk_begin(const rtkv_kv_desc* kv, const rtkv_qk_desc* q, const rtkv_layer_params* p,
+                                 const rtkv_layer_out* out, void* workspace_dev, size_t workspace_bytes, void* stream,
+                                 rtkv_early_stats* early_host, uint64_t seq, int32_t* published) {
+  RTKV_REQUIRE(q != nullptr, "null query descriptor");
+  return compress_layer_impl(kv, nullptr, q, p, out, workspace_dev, workspace_bytes, stream, nullptr, early_host, seq,
+                             published, true);
+}
+
+int rtkv_compress_layer_finish(const rtkv_kv_desc* kv, const rtkv_layer_params* p, const rtkv_layer_out* out,
+                               void* workspace_dev, size_t workspace_bytes, void* stream) {
+  int rc = check_params(p);
+  if (rc) return rc;
+  RTKV_REQUIRE(kv && out && out->labels_dev && out->kept_index_dev && out->stats_dev,
+               "compress_layer_finish needs the labels, kept_index and stats of rtkv_compress_layer_begin");
+  RTKV_REQUIRE(out->row_capacity >= kv->S, "row_capacity must be the capacity rtkv_compress_layer_begin used (>= S)");
+  if (p->flags & RTKV_EMIT_PACKED)
+    RTKV_REQUIRE(out->packed_k_dev && out->packed_v_dev && out->row_offset_dev && out->scale_zp_dev &&
+                     out->packed_capacity >= 1,
+                 "EMIT_PACKED needs packed_k, packed_v (>= the published packed bytes), row_offset and scale_zp");
+  if (p->flags & RTKV_EMIT_DEQUANT)
+    RTKV_REQUIRE(out->k_out_dev && out->v_out_dev && out->o_stride_b < 0,
+                 "EMIT_DEQUANT needs k_out / v_out of [B, S', F] rows packed at the kept count (o_stride_b = -1)");
+  Workspace ws;
+  rc = carve(workspace_dev, workspace_bytes, kv->B, kv->S, ws);
+  if (rc) return rc;
+  // the one-launch K2 (B = 1, S <= 32768) left each kept row's class in the workspace
+  const bool row_labels = select_fast_shape(kv->B, kv->S) && !(p->flags & RTKV_SELECT_PIPELINE);
+  return launch_quant(make_quant_args(kv, out->labels_dev, out->kept_index_dev, p, out, row_labels ? ws.labels : nullptr),
+                      (hipStream_t)stream);
 }
 
 int rtkv_wait_early(const rtkv_early_stats* early_host, uint64_t seq, int64_t timeout_us) {

@@ -1,0 +1,286 @@
+// attn_f32.hip — the model-side kernels of the fused importance mode for fp32 states, the reference
+// model's precision (modified_llama.py:368 builds CompressedLlamaForCausalLM with fp32 parameters):
+//
+//   lse[b,h,i] = log Σ_j exp(q·k_j·scale + kbias[b,j])             (j ≤ i when causal)   attn_lse_f32_kernel
+//   A[b,i]     = Σ_{p<P} (1/H) Σ_h exp(q·k_p·scale + kbias[b,p] − lse)                      qk_head_f32_kernel
+//
+// on gfx950's f32-input MFMA (v_mfma_f32_16x16x4_f32: exact fp32 products, fp32 accumulation; 155
+// TF/s, 1/16 of the bf16 rate, so these kernels are matrix-core bound where the f16/bf16 ones
+// (attn_lse.hip, qk_importance.hip) are not).  head_dim 128.
+//
+// Fragments (cdna_hip_programming.md, f32 16x16x4): lane l supplies A[row l&15][k = l>>4] and
+// B[k = l>>4][col l&15]; the accumulator holds col l&15, rows 4(l>>4) + reg.  The k order is permuted
+// so that every operand comes from 16-byte loads: k-step (j, e) covers head dims 16j + 4kg + e for
+// the lane group kg = l>>4 (a dot product's order of terms is the only thing that changes: parity is a
+// tolerance against the fp32 restatement, tests/test_gpu_model_side.py).  Key rows sit in LDS with
+// their 16-byte chunks XOR-swizzled by row (chunk c of row r at c ^ (r & 31)).
+#include "common.h"
+
+namespace rtkv {
+
+namespace {
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int kD = 128;            // head_dim
+constexpr int kRB = kD * 4;        // bytes per key row
+constexpr int kCH = kRB / 16;      // 16-byte chunks per row (32)
+constexpr int kKS = kD / 16;       // 16-dim groups per row (8): 4 k-steps each
+constexpr float kL2E = 1.4426950408889634f;
+
+__device__ __forceinline__ void dma16(const void* g, void* lds_base) {
+  __builtin_amdgcn_global_load_lds(g, (__attribute__((address_space(3))) void*)lds_base, 16, 0, 0);
+}
+
+// 16 rows × 16 keys of q·k (raw dot products) for key rows kr = 16t + (l & 15) of an LDS tile
+__device__ __forceinline__ f32x4 dot_tile(const f32x4 (&a)[kKS], const uint8_t* tile, int kr, int kg) {
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  const uint8_t* krow = tile + kr * kRB;
+#pragma unroll
+  for (int j = 0; j < kKS; ++j) {
+    const f32x4 b = *reinterpret_cast<const f32x4*>(krow + (((4 * j + kg) ^ (kr & (kCH - 1))) * 16));
+#pragma unroll
+    for (int e = 0; e < 4; ++e) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[j][e], b[e], acc, 0, 0, 0);
+  }
+  return acc;
+}
+
+__device__ __forceinline__ float kb_raw(const rtkv_qk_desc& q, int b, int64_t j, float inv_scale) {
+  return q.kbias_dev ? key_bias_raw(q, b, j, inv_scale) : 0.f;
+}
+
+struct LseF32Args {
+  rtkv_qk_desc q;
+  float* lse;
+  int nblk;
+};
+
+constexpr int kLKeysF = 64;  // keys per LDS tile (32 KiB)
+
+// One workgroup: 64 query rows (16 per wave) of one (b, h); key tiles double-buffered in LDS by
+// LDS-DMA, walked up to the causal diagonal; 4 column tiles per key tile = 4 independent accumulator
+// chains per wave (the f32 MFMA's 40-cycle dependent latency hides behind 32-cycle issue).
+__global__ __launch_bounds__(256) void attn_lse_f32_kernel(LseF32Args g) {
+  constexpr int TILE = kLKeysF * kRB;
+  constexpr int KI = TILE / 1024 / 4;  // DMA instructions per wave per tile
+  constexpr int RPI = 1024 / kRB;      // key rows per DMA instruction
+  extern __shared__ __attribute__((aligned(1024))) uint8_t lds[];  // 2 × TILE
+  const rtkv_qk_desc& q = g.q;
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int c16 = lane & 15, kg = lane >> 4;
+  const int qb = g.nblk - 1 - (int)blockIdx.x;  // longest-first
+  const int h = blockIdx.y, b = blockIdx.z;
+  const int S = (int)q.S, grp = (int)(q.H / q.Hkv);
+  const int i0 = qb * 64, wrow0 = i0 + wave * 16, crow0 = wrow0 + 4 * kg;
+  const float sc = q.scale * kL2E, inv_scale = 1.f / q.scale;
+  const float* Kh = static_cast<const float*>(q.k_dev) + b * q.k_stride_b + (int64_t)(h / grp) * q.k_stride_h;
+  int64_t kend = q.causal ? q.row0 + i0 + 64 : S;
+  if (kend > S) kend = S;
+  const int ntiles = (int)((kend + kLKeysF - 1) / kLKeysF);
+  const int lrow = lane / kCH, lpc = lane % kCH;
+  auto issue = [&](int kt) {
+    uint8_t* st = lds + (kt & 1) * TILE;
+#pragma unroll
+    for (int k = 0; k < KI; ++k) {
+      const int r = (wave * KI + k) * RPI + lrow;
+      const int c = lpc ^ (r & (kCH - 1));
+      int kr = kt * kLKeysF + r;
+      kr = kr < S ? kr : S - 1;
+      dma16(Kh + (int64_t)kr * q.k_stride_s + c * 4, st + (wave * KI + k) * 1024);
+    }
+  };
+  f32x4 a[kKS];
+  {
+    const int qr = wrow0 + c16 < S ? wrow0 + c16 : S - 1;
+    const float* qrow = static_cast<const float*>(q.q_dev) + b * q.q_stride_b + (int64_t)h * q.q_stride_h +
+                        (int64_t)qr * q.q_stride_s;
+#pragma unroll
+    for (int j = 0; j < kKS; ++j) a[j] = *reinterpret_cast<const f32x4*>(qrow + 16 * j + 4 * kg);
+  }
+  float m[4], l[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) { m[r] = -1e30f; l[r] = 0.f; }
+  issue(0);
+  for (int kt = 0; kt < ntiles; ++kt) {
+    if (kt + 1 < ntiles) {
+      issue(kt + 1);
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(KI) : "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __builtin_amdgcn_s_barrier();  // every wave's pieces of tile kt landed
+    const uint8_t* st = lds + (kt & 1) * TILE;
+    f32x4 acc[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) acc[t] = dot_tile(a, st, 16 * t + c16, kg);
+    __builtin_amdgcn_s_barrier();  // every wave has read tile kt: its slot is free for tile kt+2
+    const bool edge = (int64_t)(kt + 1) * kLKeysF > (q.causal ? q.row0 + wrow0 : (int64_t)S) || (kt + 1) * kLKeysF > S;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const int64_t j = (int64_t)kt * kLKeysF + 16 * t + c16;
+      const float kb = (q.kbias_dev && j < S) ? kb_raw(q, b, j, inv_scale) : 0.f;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const bool ok = !edge || (j < S && (!q.causal || j <= q.row0 + crow0 + r));
+        acc[t][r] = ok ? acc[t][r] + kb : -INFINITY;
+      }
+    }
+    bool up = false;
+    float mt[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      mt[r] = fmaxf(fmaxf(acc[0][r], acc[1][r]), fmaxf(acc[2][r], acc[3][r])) * sc;
+      up |= mt[r] > m[r] + 8.f;
+    }
+    if (__ballot(up)) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float mn = mt[r] > m[r] + 8.f ? mt[r] : m[r];
+        l[r] *= __builtin_amdgcn_exp2f(m[r] - mn);
+        m[r] = mn;
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+      for (int t = 0; t < 4; ++t) l[r] += __builtin_amdgcn_exp2f(__builtin_fmaf(acc[t][r], sc, -m[r]));
+  }
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    float M = m[r];
+#pragma unroll
+    for (int o = 1; o < 16; o <<= 1) M = fmaxf(M, __shfl_xor(M, o, 64));
+    float L = l[r] * __builtin_amdgcn_exp2f(m[r] - M);
+#pragma unroll
+    for (int o = 1; o < 16; o <<= 1) L += __shfl_xor(L, o, 64);
+    const int i = crow0 + r;
+    if (c16 == 0 && i < S)
+      g.lse[b * q.lse_stride_b + (int64_t)h * q.lse_stride_h + i] = L > 0.f ? (M + __log2f(L)) * 0.6931471805599453f : -INFINITY;
+  }
+}
+
+// Head-major K1' (as qk_head_kernel): a workgroup owns ONE head and 4·rpw query rows; the head's
+// P ≤ 128 prompt keys stay in LDS (64 KiB); each wave walks its rows in 16-row tiles and writes the
+// per-head prompt mass of each row to part[b][h][i] (qk_head_reduce_kernel sums the heads in order).
+__global__ __launch_bounds__(256) void qk_head_f32_kernel(rtkv_qk_desc q, int P, float* __restrict__ part, int rpw) {
+  constexpr int PT = 128;
+  constexpr int KEY_BYTES = PT * kRB;
+  constexpr int KI = KEY_BYTES / 1024 / 4;
+  constexpr int RPI = 1024 / kRB;
+  extern __shared__ __attribute__((aligned(1024))) uint8_t lds[];  // KEY_BYTES
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int c16 = lane & 15, kg = lane >> 4;
+  const int h = blockIdx.y, b = blockIdx.z;
+  const int S = (int)q.S, grp = (int)(q.H / q.Hkv);
+  const int wrow = (blockIdx.x * 4 + wave) * rpw;
+  const float sc = q.scale * kL2E, inv_scale = 1.f / q.scale;
+  const float* Qh = static_cast<const float*>(q.q_dev) + b * q.q_stride_b + (int64_t)h * q.q_stride_h;
+  const float* Lh = q.lse_dev + b * q.lse_stride_b + (int64_t)h * q.lse_stride_h;
+  float* Ph = part + ((int64_t)b * q.H + h) * S;
+  {
+    const float* kh = static_cast<const float*>(q.k_dev) + b * q.k_stride_b + (int64_t)(h / grp) * q.k_stride_h;
+    const int lrow = lane / kCH, lpc = lane % kCH;
+#pragma unroll
+    for (int k = 0; k < KI; ++k) {
+      const int r = (wave * KI + k) * RPI + lrow;
+      const int c = lpc ^ (r & (kCH - 1));
+      const int pr = r < P ? r : P - 1;
+      dma16(kh + (int64_t)pr * q.k_stride_s + c * 4, lds + (wave * KI + k) * 1024);
+    }
+  }
+  // the prompt columns' key bias (raw units), the same for every row
+  float kb[8];
+#pragma unroll
+  for (int t = 0; t < 8; ++t) kb[t] = (16 * t + c16 < P) ? kb_raw(q, b, 16 * t + c16, inv_scale) : 0.f;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  const int ntile = rpw / 16;
+  for (int k = 0; k < ntile; ++k) {
+    const int r0 = wrow + 16 * k;
+    if (r0 >= S) break;
+    const int crow0 = r0 + 4 * kg;
+    f32x4 a[kKS];
+    {
+      const int qr = r0 + c16 < S ? r0 + c16 : S - 1;
+      const float* qp = Qh + (int64_t)qr * q.q_stride_s;
+#pragma unroll
+      for (int j = 0; j < kKS; ++j) a[j] = *reinterpret_cast<const f32x4*>(qp + 16 * j + 4 * kg);
+    }
+    float lv[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) lv[r] = crow0 + r < S ? Lh[crow0 + r] : 0.f;
+    float v[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int t = 0; t < 8; ++t) {
+      if (16 * t >= P) break;
+      const f32x4 acc = dot_tile(a, lds, 16 * t + c16, kg);
+      const int p = 16 * t + c16;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int i = crow0 + r;
+        const bool ok = p < P && i < S && (!q.causal || (int64_t)p <= q.row0 + i);
+        const float w = __builtin_amdgcn_exp2f(__builtin_fmaf(acc[r] + kb[t], sc, -lv[r] * kL2E));
+        v[r] += ok ? w : 0.f;
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+#pragma unroll
+      for (int o = 1; o < 16; o <<= 1) v[r] += __shfl_xor(v[r], o, 64);
+      // a row that sees no key at all (lse = -inf): the reference's all-masked softmax row is uniform
+      if (lv[r] == -INFINITY) v[r] = (float)P / (float)S;
+    }
+    if (c16 == 0 && crow0 < S) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        if (crow0 + r < S) Ph[crow0 + r] = v[r];
+    }
+  }
+}
+
+}  // namespace
+
+int launch_attention_lse_f32(const rtkv_qk_desc& q, float* lse, hipStream_t st) {
+  RTKV_REQUIRE(q.D == kD, "attention_lse (fp32): head_dim must be 128");
+  RTKV_REQUIRE(q.q_stride_s % 4 == 0 && q.q_stride_h % 4 == 0 && q.q_stride_b % 4 == 0 && q.k_stride_s % 4 == 0 &&
+                   q.k_stride_h % 4 == 0 && q.k_stride_b % 4 == 0 && ((uintptr_t)q.q_dev % 16) == 0 &&
+                   ((uintptr_t)q.k_dev % 16) == 0,
+               "attention_lse (fp32): Q/K rows must be 16-byte aligned");
+  constexpr size_t lds = 2 * (size_t)kLKeysF * kRB;
+  static bool attr = false;
+  if (!attr) {
+    RTKV_HIP_CHECK(hipFuncSetAttribute((const void*)attn_lse_f32_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                       (int)lds));
+    attr = true;
+  }
+  LseF32Args a;
+  a.q = q;
+  a.lse = lse;
+  a.nblk = (int)((q.S + 63) / 64);
+  hipLaunchKernelGGL(attn_lse_f32_kernel, dim3((unsigned)a.nblk, (unsigned)q.H, (unsigned)q.B), dim3(256), lds, st, a);
+  RTKV_HIP_CHECK(hipGetLastError());
+  return RTKV_OK;
+}
+
+int launch_qk_head_f32(const rtkv_qk_desc& q, int P, float* part, hipStream_t st) {
+  RTKV_REQUIRE(q.D == kD, "importance_qk_lse (fp32): head_dim must be 128");
+  RTKV_REQUIRE(q.q_stride_s % 4 == 0 && q.q_stride_h % 4 == 0 && q.q_stride_b % 4 == 0 && q.k_stride_s % 4 == 0 &&
+                   q.k_stride_h % 4 == 0 && q.k_stride_b % 4 == 0 && ((uintptr_t)q.q_dev % 16) == 0 &&
+                   ((uintptr_t)q.k_dev % 16) == 0,
+               "importance_qk_lse (fp32): Q/K rows must be 16-byte aligned");
+  constexpr size_t lds = (size_t)128 * kRB;
+  static bool attr = false;
+  if (!attr) {
+    RTKV_HIP_CHECK(hipFuncSetAttribute((const void*)qk_head_f32_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                       (int)lds));
+    attr = true;
+  }
+  int rpw = 256;
+  while (rpw > 16 && (q.S + 4 * rpw - 1) / (4 * rpw) * q.H * q.B < 2048) rpw /= 2;
+  const dim3 grid((unsigned)((q.S + 4 * rpw - 1) / (4 * rpw)), (unsigned)q.H, (unsigned)q.B);
+  hipLaunchKernelGGL(qk_head_f32_kernel, grid, dim3(256), lds, st, q, P, part, rpw);
+  RTKV_HIP_CHECK(hipGetLastError());
+  return RTKV_OK;
+}
+
+}  // namespace rtkv

@@ -82,7 +82,7 @@ __global__ __launch_bounds__(256, RG == 1 ? LSE_WPE : 1) void attn_lse_kernel(Ls
   const int S = (int)q.S, grp = (int)(q.H / q.Hkv);
   const int i0 = qb * kLRows;
   const int wrow0 = i0 + wave * 16 * RG;     // the wave's rows: RG groups of 16 from here
-  const float sc = q.scale * 1.4426950408889634f;
+  const float sc = q.scale * 1.4426950408889634f, inv_scale = 1.f / q.scale;
   const S_* Kh = static_cast<const S_*>(q.k_dev) + b * q.k_stride_b + (int64_t)(h / grp) * q.k_stride_h;
   // key rows this block needs: causal → up to its last query row (global position row0 + i)
   int64_t kend = q.causal ? q.row0 + i0 + kLRows : S;
@@ -143,6 +143,17 @@ __global__ __launch_bounds__(256, RG == 1 ? LSE_WPE : 1) void attn_lse_kernel(Ls
   auto prepare = [&](f32x4 (&acc)[RG][4], int kt) {
     bool up = false;
     float mt[RG][4];
+    if (q.kbias_dev) {  // key padding: the bias of this tile's columns (raw units), -inf for a padding key
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const int j = kt * kLKeys + 16 * t + c16;
+        const float kb = j < S ? key_bias_raw(q, b, j, inv_scale) : 0.f;
+#pragma unroll
+        for (int rg = 0; rg < RG; ++rg)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) acc[rg][t][r] += kb;
+      }
+    }
 #pragma unroll
     for (int rg = 0; rg < RG; ++rg) {
       const int grow0 = wrow0 + 16 * rg;      // first row of the group
@@ -267,12 +278,14 @@ int launch_attention_lse(const rtkv_qk_desc& q, float* lse, hipStream_t st) {
   RTKV_REQUIRE(q.H % q.Hkv == 0, "attention_lse: H must be a multiple of Hkv");
   RTKV_REQUIRE(q.D == 64 || q.D == 128, "attention_lse: head_dim must be 64 or 128");
   RTKV_REQUIRE(q.scale > 0.f, "attention_lse: scale must be positive");
-  RTKV_REQUIRE(q.dtype == RTKV_F16 || q.dtype == RTKV_BF16, "attention_lse: Q/K must be float16 or bfloat16");
+  RTKV_REQUIRE(q.S < ((int64_t)1 << 31) && q.row0 == 0, "attention_lse: bad row range (row0 must be 0)");
+  RTKV_REQUIRE(q.dtype == RTKV_F16 || q.dtype == RTKV_BF16 || q.dtype == RTKV_F32,
+               "attention_lse: Q/K must be float16, bfloat16 or float32");
+  if (q.dtype == RTKV_F32) return launch_attention_lse_f32(q, lse, st);
   RTKV_REQUIRE(q.q_stride_s % 8 == 0 && q.q_stride_h % 8 == 0 && q.q_stride_b % 8 == 0 && q.k_stride_s % 8 == 0 &&
                    q.k_stride_h % 8 == 0 && q.k_stride_b % 8 == 0 && ((uintptr_t)q.q_dev % 16) == 0 &&
                    ((uintptr_t)q.k_dev % 16) == 0,
                "attention_lse: Q/K rows must be 16-byte aligned");
-  RTKV_REQUIRE(q.S < ((int64_t)1 << 31) && q.row0 == 0, "attention_lse: bad row range (row0 must be 0)");
   LseArgs a;
   a.q = q;
   a.lse = lse;

@@ -196,6 +196,14 @@ __device__ __forceinline__ void zero_regions(const AggExtras& x) {
 int launch_aggregation(const rtkv_attn_desc& w, int P, float* A, hipStream_t st, const AggExtras& x = AggExtras());
 // scratch: [B][H][S] fp32 (qk_scratch_bytes) for the head-major kernel, or null (head-walking kernel)
 size_t qk_scratch_bytes(int64_t B, int64_t H, int64_t S);
+// fp32 states on the f32 MFMA (attn_f32.hip): the row LSE and the head-major K1' per-head masses
+int launch_attention_lse_f32(const rtkv_qk_desc& q, float* lse, hipStream_t st);
+int launch_qk_head_f32(const rtkv_qk_desc& q, int P, float* part, hipStream_t st);
+// an additive key bias in raw dot-product units (bias / scale), -inf for a padding key (< -1e30)
+__device__ __forceinline__ float key_bias_raw(const rtkv_qk_desc& q, int64_t b, int64_t j, float inv_scale) {
+  const float v = q.kbias_dev[b * q.kbias_stride_b + j];
+  return v < -1e30f ? -INFINITY : v * inv_scale;
+}
 int launch_qk_importance(const rtkv_qk_desc& q, int P, float* A, hipStream_t st, const AggExtras& x, int* nparts,
                          float* scratch = nullptr, size_t scratch_bytes = 0);
 int launch_attention_lse(const rtkv_qk_desc& q, float* lse, hipStream_t st);

@@ -268,6 +268,11 @@ __global__ __launch_bounds__(256, QK_HEAD_WPE) void qk_head_kernel(QKArgs g, flo
       glds16(kh + (int64_t)pr * q.k_stride_s + c * 8, lds + (wave * KI + k) * 1024);
     }
   }
+  // the prompt columns' key bias (raw units; 0 without one), the same for every row
+  float kb[NT];
+#pragma unroll
+  for (int t = 0; t < NT; ++t)
+    kb[t] = (q.kbias_dev && 16 * t + c16 < P) ? key_bias_raw(q, b, 16 * t + c16, 1.f / q.scale) : 0.f;
   const int ntile = rpw / 16;
   auto load_tile = [&](int k, FT (&a)[KS], f32x4& l) {  // tile k of this wave (clamped rows)
     const int r0 = wrow + 16 * (k < ntile ? k : ntile - 1);
@@ -318,7 +323,7 @@ __global__ __launch_bounds__(256, QK_HEAD_WPE) void qk_head_kernel(QKArgs g, flo
 #pragma unroll
       for (int t = 0; t < NT; ++t)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) v[r] += __builtin_amdgcn_exp2f(__builtin_fmaf(acc[t][r], sc, nl2[r]));
+        for (int r = 0; r < 4; ++r) v[r] += __builtin_amdgcn_exp2f(__builtin_fmaf(acc[t][r] + kb[t], sc, nl2[r]));
     } else {
 #pragma unroll
       for (int t = 0; t < NT; ++t) {
@@ -327,15 +332,18 @@ __global__ __launch_bounds__(256, QK_HEAD_WPE) void qk_head_kernel(QKArgs g, flo
         for (int r = 0; r < 4; ++r) {
           const int i = crow0 + r;
           const bool ok = p < P && i < S && (!q.causal || (int64_t)p <= q.row0 + i);
-          const float w = __builtin_amdgcn_exp2f(__builtin_fmaf(acc[t][r], sc, nl2[r]));
+          const float w = __builtin_amdgcn_exp2f(__builtin_fmaf(acc[t][r] + kb[t], sc, nl2[r]));
           v[r] += ok ? w : 0.f;
         }
       }
     }
 #pragma unroll
-    for (int r = 0; r < 4; ++r)
+    for (int r = 0; r < 4; ++r) {
 #pragma unroll
       for (int o = 1; o < 16; o <<= 1) v[r] += __shfl_xor(v[r], o, 64);
+      // a row that sees no key (lse = -inf, padding): the reference's all-masked row is uniform over S
+      if (nl2[r] == INFINITY) v[r] = (float)P / (float)S;
+    }
     if (c16 == 0 && crow0 < S) *reinterpret_cast<f32x4*>(Ph + crow0) = f32x4{v[0], v[1], v[2], v[3]};
 #pragma unroll
     for (int s_ = 0; s_ < KS; ++s_) qa[s_] = qn[s_];
@@ -393,6 +401,15 @@ __global__ __launch_bounds__(256) void qk_head_reduce_kernel(const float* __rest
   }
 }
 
+// one wave per 64 tokens: every token's H loads in flight at once, over S/64 CUs
+static int launch_qk_head_reduce(const QKArgs& a, float* part, hipStream_t st, int* nparts) {
+  const dim3 rgrid((unsigned)((a.q.S + 63) / 64), (unsigned)a.q.B);
+  if (nparts) *nparts = (int)rgrid.x;
+  hipLaunchKernelGGL(qk_head_reduce_kernel, rgrid, dim3(64), 0, st, part, a.q.H, a.q.S, a.A, a.ex);
+  RTKV_HIP_CHECK(hipGetLastError());
+  return RTKV_OK;
+}
+
 template <int DT, int NT, int KS>
 static int launch_qk_head(const QKArgs& a, float* part, hipStream_t st, int* nparts) {
   constexpr size_t lds = (size_t)(16 * NT) * (64 * KS);
@@ -407,12 +424,7 @@ static int launch_qk_head(const QKArgs& a, float* part, hipStream_t st, int* npa
   const dim3 grid((unsigned)((S + 4 * rpw - 1) / (4 * rpw)), (unsigned)a.q.H, (unsigned)a.q.B);
   hipLaunchKernelGGL((qk_head_kernel<DT, NT, KS>), grid, dim3(256), lds, st, a, part, rpw);
   RTKV_HIP_CHECK(hipGetLastError());
-  // one wave per 64 tokens: every token's H loads in flight at once, over S/64 CUs
-  const dim3 rgrid((unsigned)((S + 63) / 64), (unsigned)a.q.B);
-  if (nparts) *nparts = (int)rgrid.x;
-  hipLaunchKernelGGL(qk_head_reduce_kernel, rgrid, dim3(64), 0, st, part, a.q.H, S, a.A, a.ex);
-  RTKV_HIP_CHECK(hipGetLastError());
-  return RTKV_OK;
+  return launch_qk_head_reduce(a, part, st, nparts);
 }
 
 template <int DT, int NT, int KS>
@@ -452,24 +464,37 @@ int launch_qk_importance(const rtkv_qk_desc& q, int P, float* A, hipStream_t st,
   RTKV_REQUIRE(q.H % q.Hkv == 0, "importance_qk_lse: H must be a multiple of Hkv");
   RTKV_REQUIRE(q.D == 32 || q.D == 64 || q.D == 128, "importance_qk_lse: head_dim must be 32, 64 or 128");
   RTKV_REQUIRE(P >= 1 && P <= 128, "importance_qk_lse: prompt_len must be in [1, 128]");
-  RTKV_REQUIRE(q.dtype == RTKV_F16 || q.dtype == RTKV_BF16, "importance_qk_lse: Q/K must be float16 or bfloat16");
-  RTKV_REQUIRE(q.q_stride_s % 8 == 0 && q.q_stride_h % 8 == 0 && q.q_stride_b % 8 == 0 && q.k_stride_s % 8 == 0 &&
-                   q.k_stride_h % 8 == 0 && q.k_stride_b % 8 == 0 && ((uintptr_t)q.q_dev % 16) == 0 &&
-                   ((uintptr_t)q.k_dev % 16) == 0,
-               "importance_qk_lse: Q/K rows must be 16-byte aligned");
+  RTKV_REQUIRE(q.dtype == RTKV_F16 || q.dtype == RTKV_BF16 || q.dtype == RTKV_F32,
+               "importance_qk_lse: Q/K must be float16, bfloat16 or float32");
   RTKV_REQUIRE(((uintptr_t)q.lse_dev % 16) == 0 && q.lse_stride_h % 4 == 0 && q.lse_stride_b % 4 == 0,
                "importance_qk_lse: lse rows must be 16-byte aligned");
   RTKV_REQUIRE(q.S < ((int64_t)1 << 31) && q.row0 >= 0, "importance_qk_lse: bad row range");
+  RTKV_REQUIRE(!q.kbias_dev || q.row0 == 0, "importance_qk_lse: key bias with row0 != 0");
   QKArgs a;
   a.q = q;
   a.P = P;
   a.A = A;
   a.ex = x;
+  const bool head_ok = scratch && scratch_bytes >= qk_scratch_bytes(q.B, q.H, q.S) && q.H <= 65535 && q.D == 128;
+  if (q.dtype == RTKV_F32) {  // fp32 states: the head-major kernel on the f32 MFMA (attn_f32.hip)
+    RTKV_REQUIRE(head_ok, "importance_qk_lse (fp32): needs head_dim 128 and the head-major scratch "
+                          "(rtkv_importance_qk_lse_ws / rtkv_workspace_size_qk)");
+    const int rc = launch_qk_head_f32(q, P, scratch, st);
+    if (rc) return rc;
+    return launch_qk_head_reduce(a, scratch, st, nparts);
+  }
+  RTKV_REQUIRE(q.q_stride_s % 8 == 0 && q.q_stride_h % 8 == 0 && q.q_stride_b % 8 == 0 && q.k_stride_s % 8 == 0 &&
+                   q.k_stride_h % 8 == 0 && q.k_stride_b % 8 == 0 && ((uintptr_t)q.q_dev % 16) == 0 &&
+                   ((uintptr_t)q.k_dev % 16) == 0,
+               "importance_qk_lse: Q/K rows must be 16-byte aligned");
   // head-major kernel when a scratch is given (the C ABI entries that take a workspace); RTKV_QK_RING
-  // forces the head-walking kernel (cross-check knob)
+  // forces the head-walking kernel (cross-check knob).  A key bias (padding) is applied by the
+  // head-major kernel only.
   static const bool ring = getenv("RTKV_QK_RING") != nullptr;
-  if (scratch && scratch_bytes >= qk_scratch_bytes(q.B, q.H, q.S) && q.S % 4 == 0 && !ring &&
-      q.H <= 65535 && P > 64 && q.D == 128) {
+  if (q.kbias_dev)
+    RTKV_REQUIRE(head_ok && q.S % 4 == 0, "importance_qk_lse: a key bias needs head_dim 128, S % 4 == 0 and the "
+                                          "head-major scratch");
+  if (head_ok && q.S % 4 == 0 && ((!ring && P > 64) || q.kbias_dev)) {
     if (q.dtype == RTKV_F16) return launch_qk_head<RTKV_F16, 8, 4>(a, scratch, st, nparts);
     return launch_qk_head<RTKV_BF16, 8, 4>(a, scratch, st, nparts);
   }

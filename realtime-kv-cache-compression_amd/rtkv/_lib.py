@@ -53,7 +53,7 @@ class QKDesc(ctypes.Structure):
                 ("q_stride_b", c_i64), ("q_stride_h", c_i64), ("q_stride_s", c_i64),
                 ("k_stride_b", c_i64), ("k_stride_h", c_i64), ("k_stride_s", c_i64),
                 ("lse_stride_b", c_i64), ("lse_stride_h", c_i64), ("scale", c_f), ("reserved", c_i32),
-                ("row0", c_i64)]
+                ("row0", c_i64), ("kbias_dev", c_p), ("kbias_stride_b", c_i64)]
 
 
 class BatchStats(ctypes.Structure):
@@ -119,6 +119,9 @@ _SIGS = {
     "rtkv_compress_layer_early": ([c_p, c_p, c_p, c_p, c_p, c_sz, c_p, c_p, ctypes.c_uint64, c_p], c_i32),
     "rtkv_compress_layer_qk_early": ([c_p, c_p, c_p, c_p, c_p, c_sz, c_p, c_p, ctypes.c_uint64, c_p], c_i32),
     "rtkv_wait_early": ([c_p, ctypes.c_uint64, c_i64], c_i32),
+    "rtkv_compress_layer_begin": ([c_p, c_p, c_p, c_p, c_p, c_sz, c_p, c_p, ctypes.c_uint64, c_p], c_i32),
+    "rtkv_compress_layer_qk_begin": ([c_p, c_p, c_p, c_p, c_p, c_sz, c_p, c_p, ctypes.c_uint64, c_p], c_i32),
+    "rtkv_compress_layer_finish": ([c_p, c_p, c_p, c_p, c_sz, c_p], c_i32),
     "rtkv_host_alloc": ([c_sz], c_p),
     "rtkv_host_free": ([c_p], None),
     "rtkv_comm_unique_id": ([c_p, c_sz], c_i32),

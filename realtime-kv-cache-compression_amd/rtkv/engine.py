@@ -77,10 +77,13 @@ def kv_desc(K: torch.Tensor, V: torch.Tensor, layout: str = "bsf", heads: Option
 
 
 def qk_desc(Q: torch.Tensor, K: torch.Tensor, lse: torch.Tensor, scale: Optional[float] = None,
-            causal: bool = True, k_layout: str = "bsf", kv_heads: Optional[int] = None, row0: int = 0) -> L.QKDesc:
+            causal: bool = True, k_layout: str = "bsf", kv_heads: Optional[int] = None, row0: int = 0,
+            key_bias: Optional[torch.Tensor] = None) -> L.QKDesc:
     """Fused importance input: Q [B,H,S,D] (model layout, unit d stride), keys whose first P rows are
     the prompt keys — K [B,S,Hkv*D] ('bsf', the reference's compress_layer_kv_cache input) or
-    [B,Hkv,S,D] ('bhsd') — and the row log-sum-exp lse [B,H,S] (fp32) of the model's softmax."""
+    [B,Hkv,S,D] ('bhsd') — and the row log-sum-exp lse [B,H,S] (fp32) of the model's softmax.
+    key_bias: optional fp32 [B, S] additive key-padding bias (0 real key, -inf padding key), the
+    padding part of the model's attention_mask (modified_llama.py:90-91)."""
     if Q.dim() != 4 or Q.stride(-1) != 1:
         raise ValueError("queries must be [B, H, S, D] with unit head_dim stride")
     B, H, S, D = Q.shape
@@ -109,6 +112,13 @@ def qk_desc(Q: torch.Tensor, K: torch.Tensor, lse: torch.Tensor, scale: Optional
     d.lse_stride_b, d.lse_stride_h = lse.stride(0), lse.stride(1)
     d.scale = float(scale) if scale is not None else 1.0 / float(D) ** 0.5
     d.row0 = int(row0)
+    if key_bias is not None:
+        if key_bias.dtype != torch.float32 or key_bias.dim() != 2 or tuple(key_bias.shape) != (B, S) \
+                or key_bias.stride(-1) != 1 or key_bias.device != Q.device:
+            raise ValueError(f"key_bias must be float32 [B, S] = {(B, S)} with unit stride on the queries' device")
+        if row0 != 0:
+            raise ValueError("key_bias is not supported for sequence shards (row0 != 0)")
+        d.kbias_dev, d.kbias_stride_b = key_bias.data_ptr(), key_bias.stride(0)
     return d
 
 
@@ -158,6 +168,7 @@ class EarlyStatsBuffer:
         self.ptr = self._lib.rtkv_host_alloc(ctypes.sizeof(L.EarlyStats))
         if not self.ptr:
             raise RuntimeError("rtkv: rtkv_host_alloc failed (pinned host memory for the early statistics)")
+        self._view = L.EarlyStats.from_address(self.ptr)  # the pinned block in place (read after the seq word)
         self.seq = 0
 
     def next_seq(self) -> int:
@@ -165,7 +176,7 @@ class EarlyStatsBuffer:
         return self.seq
 
     def _read(self) -> L.EarlyStats:
-        return L.EarlyStats.from_buffer_copy(ctypes.string_at(self.ptr, ctypes.sizeof(L.EarlyStats)))
+        return L.EarlyStats.from_buffer_copy(self._view)
 
     def wait(self, seq: int, device=None) -> L.EarlyStats:
         """The statistics of call `seq` once the device has published them.  A queue slower than the
@@ -208,21 +219,27 @@ class LayerBuffers:
     layer call, as the reference returns fresh tensors; one allocation instead of ten keeps that
     cheap).  Views are 256-byte aligned."""
 
-    def __init__(self, B: int, S: int, F: int, dtype: torch.dtype, device, bits, emit_dequant=True, emit_packed=True):
+    def __init__(self, B: int, S: int, F: int, dtype: torch.dtype, device, bits, emit_dequant=True, emit_packed=True,
+                 outputs: bool = True):
+        """outputs=False: only the per-token buffers (scores, classes, mask, kept indices, row offsets,
+        scale/zero-points, statistics); the caller supplies exactly-sized K'/V' and packed buffers to
+        finish() (rtkv_compress_layer_begin / _finish)."""
         self.B, self.S, self.F, self.dtype = B, S, F, dtype
+        self.emit_dequant, self.emit_packed = emit_dequant, emit_packed
         dev = self.device = torch.device(device)
         esz = torch.tensor([], dtype=dtype).element_size()
         cap = 0
-        if emit_packed:
+        if emit_packed and outputs:
             b3 = (ctypes.c_int32 * 3)(*bits)
             cap = int(L.lib().rtkv_packed_capacity(B, S, F, L.TORCH_DTYPE_CODE[dtype], b3))
         plan = [("scores", B * S * 4), ("labels", B * S), ("mask", B * S), ("kept_index", B * S * 4),
                 ("stats", L.stats_bytes(B))]
-        if emit_dequant:
+        if emit_dequant and outputs:
             plan += [("k_out", B * S * F * esz), ("v_out", B * S * F * esz)]
         if emit_packed:
-            plan += [("packed_k", max(cap, 1)), ("packed_v", max(cap, 1)), ("row_offset", B * S * 8),
-                     ("scale_zp", B * S * 16)]
+            if outputs:
+                plan += [("packed_k", max(cap, 1)), ("packed_v", max(cap, 1))]
+            plan += [("row_offset", B * S * 8), ("scale_zp", B * S * 16)]
         offs, total = {}, 0
         for name, n in plan:
             offs[name] = (total, n)
@@ -238,17 +255,17 @@ class LayerBuffers:
         self.mask = view("mask", torch.uint8, (B, S))
         self.kept_index = view("kept_index", torch.int32, (B, S))
         self.stats = view("stats", torch.uint8, (L.stats_bytes(B),))
-        self.k_out = view("k_out", dtype, (B * S * F,)) if emit_dequant else None
-        self.v_out = view("v_out", dtype, (B * S * F,)) if emit_dequant else None
+        self.k_out = view("k_out", dtype, (B * S * F,)) if emit_dequant and outputs else None
+        self.v_out = view("v_out", dtype, (B * S * F,)) if emit_dequant and outputs else None
+        self.packed_k = self.packed_v = self.row_offset = self.scale_zp = None
+        self.packed_capacity = 0
         if emit_packed:
-            self.packed_k = view("packed_k", torch.uint8, (max(cap, 1),))
-            self.packed_v = view("packed_v", torch.uint8, (max(cap, 1),))
-            self.packed_capacity = cap
+            if outputs:
+                self.packed_k = view("packed_k", torch.uint8, (max(cap, 1),))
+                self.packed_v = view("packed_v", torch.uint8, (max(cap, 1),))
+                self.packed_capacity = cap
             self.row_offset = view("row_offset", torch.int64, (B, S))
             self.scale_zp = view("scale_zp", torch.float32, (B, S, 4))
-        else:
-            self.packed_k = self.packed_v = self.row_offset = self.scale_zp = None
-            self.packed_capacity = 0
 
     def matches(self, B, S, F, dtype, emit_dequant, emit_packed) -> bool:
         return (self.B, self.S, self.F, self.dtype) == (B, S, F, dtype) and \
@@ -326,12 +343,13 @@ class LayerResult:
 
 def compress_layer_qk(K, V, Q, lse, params: L.LayerParams, bufs: LayerBuffers, workspace: Workspace,
                       layout: str = "bsf", causal: bool = True, scale: Optional[float] = None,
-                      stream: Optional[int] = None, early: Optional[EarlyStatsBuffer] = None) -> LayerResult:
+                      stream: Optional[int] = None, early: Optional[EarlyStatsBuffer] = None,
+                      key_bias: Optional[torch.Tensor] = None) -> LayerResult:
     """compress_layer in the fused importance mode: K1' computes A from Q, the prompt keys (the first
     P rows of K) and the row LSE on MFMA; K2 and K4 are unchanged."""
     L.require_device(K, V, Q, lse)
     kd = kv_desc(K, V, layout)
-    qd = qk_desc(Q, K, lse, scale=scale, causal=causal, k_layout=layout)
+    qd = qk_desc(Q, K, lse, scale=scale, causal=causal, k_layout=layout, key_bias=key_bias)
     if qd.B != kd.B or qd.S != kd.S:
         raise ValueError(f"queries {tuple(Q.shape)} do not match key states {tuple(K.shape)}")
     ws = workspace.get(kd.B, kd.S, H=qd.H)
@@ -352,10 +370,10 @@ def compress_layer_qk(K, V, Q, lse, params: L.LayerParams, bufs: LayerBuffers, w
 
 
 def importance_qk_lse(Q, K, lse, prompt_len: int, causal: bool = True, scale: Optional[float] = None,
-                      k_layout: str = "bsf") -> torch.Tensor:
+                      k_layout: str = "bsf", key_bias: Optional[torch.Tensor] = None) -> torch.Tensor:
     """A [B, S] (fp32) of the fused importance mode alone (rtkv_importance_qk_lse)."""
     L.require_device(Q, K, lse)
-    qd = qk_desc(Q, K, lse, scale=scale, causal=causal, k_layout=k_layout)
+    qd = qk_desc(Q, K, lse, scale=scale, causal=causal, k_layout=k_layout, key_bias=key_bias)
     A = torch.empty(qd.B, qd.S, dtype=torch.float32, device=Q.device)
     scratch = torch.empty(int(L.lib().rtkv_qk_scratch_size(qd.B, qd.H, qd.S)), dtype=torch.uint8, device=Q.device)
     L.check(L.lib().rtkv_importance_qk_lse_ws(ctypes.byref(qd), int(prompt_len), A.data_ptr(), scratch.data_ptr(),
@@ -363,13 +381,15 @@ def importance_qk_lse(Q, K, lse, prompt_len: int, causal: bool = True, scale: Op
     return A
 
 
-def attention_lse(Q, K, causal: bool = True, scale: Optional[float] = None, k_layout: str = "bhsd") -> torch.Tensor:
-    """Row log-sum-exp [B, H, S] (fp32) of softmax(Q·Kᵀ·scale + causal mask) (rtkv_attention_lse):
-    the lse the fused importance mode consumes, without the [B, H, S, S] matrix."""
+def attention_lse(Q, K, causal: bool = True, scale: Optional[float] = None, k_layout: str = "bhsd",
+                  key_bias: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Row log-sum-exp [B, H, S] (fp32) of softmax(Q·Kᵀ·scale + causal mask + key_bias) (rtkv_attention_lse):
+    the lse the fused importance mode consumes, without the [B, H, S, S] matrix.  A row that sees no
+    key (a padding row) gets -inf."""
     L.require_device(Q, K)
     B, H, S, _ = Q.shape
     lse = torch.empty(B, H, S, dtype=torch.float32, device=Q.device)
-    qd = qk_desc(Q, K, lse, scale=scale, causal=causal, k_layout=k_layout)
+    qd = qk_desc(Q, K, lse, scale=scale, causal=causal, k_layout=k_layout, key_bias=key_bias)
     L.check(L.lib().rtkv_attention_lse(ctypes.byref(qd), lse.data_ptr(), L.stream_ptr(Q.device)), "rtkv_attention_lse")
     return lse
 
@@ -398,3 +418,69 @@ def compress_layer(K, V, W, params: L.LayerParams, bufs: LayerBuffers, workspace
                                      ws.data_ptr(), ws.numel(), st)
     L.check(rc, "rtkv_compress_layer")
     return LayerResult(bufs, kd.B, stream=st)
+
+
+class PendingLayer(LayerResult):
+    """A layer whose K1 and K2 are enqueued (rtkv_compress_layer_begin): stats() gives S' and the packed
+    byte count (early publication, or a stream sync); finish() enqueues K4 into exactly-sized buffers."""
+
+    def __init__(self, bufs: LayerBuffers, kd: L.KVDesc, params: L.LayerParams, workspace: torch.Tensor, stream: int,
+                 early: Optional[EarlyStatsBuffer], seq: int, out: L.LayerOut):
+        super().__init__(bufs, kd.B, early, seq, stream=stream)
+        self._kd, self._params, self._ws, self._stream, self._out = kd, params, workspace, stream, out
+        self.k_out = self.v_out = self.packed_k = self.packed_v = None
+
+    def finish(self) -> "PendingLayer":
+        """Allocate K'/V' [B, S', F] and the packed codes at their exact sizes and enqueue K4 into them.
+        Between the early statistics and this launch the device only runs K2's tail, so this path is
+        kept short: one allocation for K'+V', one for both code planes, the begin call's LayerOut patched."""
+        st = self.stats()
+        b = self.bufs
+        dev, Sp, pb = b.device, st.max_kept, st.total_packed_bytes
+        out = self._out
+        if b.emit_dequant:
+            kv = torch.empty(2, self.B, Sp, b.F, dtype=b.dtype, device=dev)
+            self.k_out, self.v_out = kv[0], kv[1]
+            out.k_out_dev, out.v_out_dev = self.k_out.data_ptr(), self.v_out.data_ptr()
+        if b.emit_packed:
+            n = (max(pb, 1) + 255) // 256 * 256
+            codes = torch.empty(2, n, dtype=torch.uint8, device=dev)
+            self.packed_k, self.packed_v = codes[0], codes[1]
+            out.packed_k_dev, out.packed_v_dev = self.packed_k.data_ptr(), self.packed_v.data_ptr()
+            out.packed_capacity = n
+        L.check(L.lib().rtkv_compress_layer_finish(ctypes.byref(self._kd), ctypes.byref(self._params), ctypes.byref(out),
+                                                   self._ws.data_ptr(), self._ws.numel(), self._stream),
+                "rtkv_compress_layer_finish")
+        self.done.record(torch.cuda.ExternalStream(self._stream, device=dev)
+                         if self._stream != torch.cuda.current_stream(dev).cuda_stream else torch.cuda.current_stream(dev))
+        return self
+
+    def kv(self):
+        return self.k_out, self.v_out
+
+
+def compress_layer_begin(K, V, W, params: L.LayerParams, bufs: LayerBuffers, workspace: Workspace,
+                         early: Optional[EarlyStatsBuffer], layout: str = "bsf", Q=None, lse=None, causal: bool = True,
+                         stream: Optional[int] = None, key_bias: Optional[torch.Tensor] = None) -> PendingLayer:
+    """K1 + K2 of one layer (W, or Q + lse for the fused importance mode when W is None) into the
+    per-token buffers of `bufs` (LayerBuffers(..., outputs=False)); PendingLayer.finish() runs K4."""
+    L.require_device(K, V, *((Q, lse) if W is None else (W,)))
+    kd = kv_desc(K, V, layout)
+    if W is None:
+        xd = qk_desc(Q, K, lse, causal=causal, k_layout=layout, key_bias=key_bias)
+        ws = workspace.get(kd.B, kd.S, H=xd.H)
+        fn, name = L.lib().rtkv_compress_layer_qk_begin, "rtkv_compress_layer_qk_begin"
+    else:
+        xd = attn_desc(W)
+        ws = workspace.get(kd.B, kd.S)
+        fn, name = L.lib().rtkv_compress_layer_begin, "rtkv_compress_layer_begin"
+    if xd.B != kd.B or xd.S != kd.S:
+        raise ValueError("attention input and key states disagree on B or S")
+    out = bufs.out_struct()
+    out.o_stride_h = kd.D
+    st = L.stream_ptr(K.device) if stream is None else stream
+    seq, pub = (early.next_seq(), ctypes.c_int32(0)) if early is not None else (0, ctypes.c_int32(0))
+    L.check(fn(ctypes.byref(kd), ctypes.byref(xd), ctypes.byref(params), ctypes.byref(out), ws.data_ptr(), ws.numel(),
+               st, early.ptr if early is not None else None, seq, ctypes.byref(pub)), name)
+    return PendingLayer(bufs, kd, params, ws, st, early if pub.value else None, seq, out)
+

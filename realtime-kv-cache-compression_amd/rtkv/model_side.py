@@ -5,7 +5,8 @@ softmax(Q·Kᵀ/√d + mask) as a [B, H, S, S] tensor only to hand it to compres
 recomputes the attention over the compressed keys.  `CompressedPrefillAttention` keeps the same
 three steps without that tensor:
 
-1. the row log-sum-exp of the prefill softmax, on MFMA (rtkv_attention_lse, csrc/attn_lse.hip);
+1. the row log-sum-exp of the prefill softmax, on MFMA (rtkv_attention_lse, csrc/attn_lse.hip; fp32
+   states on the f32 MFMA, csrc/attn_f32.hip);
 2. the compression in the fused importance mode: Q, the prompt keys and the lse give the
    prompt-attention mass (rtkv_compress_layer_qk, K1' on MFMA), then the usual selection and
    quantization (K2, K4) — K', V' and the packed codes as in the reference layer;
@@ -19,10 +20,18 @@ three steps without that tensor:
 
 Inputs are the post-RoPE states the reference layer has at :64-75, in its [B, heads, S, D] layout.
 
-Limits at this boundary (checked, ValueError): the states are float16 or bfloat16 with head_dim 64 or
-128 (the MFMA LSE and K1' kernels), and the model's attention_mask, when given, must be the plain
-causal mask — a padded batch (padding columns in the mask, modified_llama.py:90-91) is rejected
-rather than silently scored as unpadded.
+Masks: the model's additive attention_mask [B, 1, S, S] (modified_llama.py:90-91) is accepted when it
+is the causal mask plus a key-padding mask (HF's left or right padding: every entry 0 or at most
+finfo.min/2, and a key masked for one query masked for all).  Its padding part becomes a per-key bias
+(0 / -inf) that the LSE and K1' kernels apply, and the attention after compression uses the model's
+own mask exactly as the reference does — its first S' columns (:131-134), or the whole mask when
+nothing was dropped.  A query row that sees no key at all (a padding row) has lse = -inf and the
+uniform 1/S softmax row the reference's all-masked row has (exact for an fp32 mask, whose finfo.min
+absorbs every logit).
+
+Limits (checked, ValueError): float32, float16 or bfloat16 states; head_dim 128 (or 64 for
+float16/bfloat16 without padding); S a multiple of 4 with a padding mask; any other mask is
+rejected rather than silently scored as something else.
 """
 from __future__ import annotations
 
@@ -51,29 +60,30 @@ class CompressedPrefillAttention:
                  attention_mask: Optional[torch.Tensor] = None) -> Tuple[torch.Tensor, Tuple[torch.Tensor, torch.Tensor], Dict]:
         """query [B,H,S,D], key/value [B,Hkv,S,D] (post-RoPE) → (attn_output [B,H,S,D] before o_proj,
         (K' [B,Hkv,S',D], V' [B,Hkv,S',D]) for the cache, compression_info).  attention_mask: the
-        model's additive [B, 1, S, S] mask (optional; only the causal mask is accepted)."""
+        model's additive [B, 1, S, S] mask (optional; causal, with or without key padding)."""
         B, H, S, D = query_states.shape
         Hkv = key_states.shape[1]
         if H != self.num_heads or Hkv != self.num_kv_heads or D != self.head_dim:
             raise ValueError("state shapes do not match the layer's head configuration")
-        if query_states.dtype not in (torch.float16, torch.bfloat16) or D not in (64, 128):
-            raise ValueError(f"CompressedPrefillAttention needs float16/bfloat16 states with head_dim 64 or 128 "
-                             f"(got {query_states.dtype}, head_dim {D}); fp32 models use the reference attention "
-                             f"with RealTimePrefillCompressor.compress_layer_kv_cache")
+        dt = query_states.dtype
+        if dt not in (torch.float32, torch.float16, torch.bfloat16) or D not in (64, 128) or \
+                (dt == torch.float32 and D != 128):
+            raise ValueError(f"CompressedPrefillAttention needs float32/float16/bfloat16 states with head_dim 128 "
+                             f"(64 for float16/bfloat16); got {dt}, head_dim {D}")
+        key_bias, valid_key = None, None
         if attention_mask is not None:
-            m = attention_mask[..., :S, :S]
-            causal = torch.ones(S, S, dtype=torch.bool, device=m.device).tril()
-            if m.dim() != 4 or not bool(torch.equal((m >= 0).expand(B, 1, S, S), causal.expand(B, 1, S, S))):
-                raise ValueError("attention_mask is not the plain causal mask (padded batches are not supported by "
-                                 "the fused importance mode)")
+            key_bias, valid_key = split_attention_mask(attention_mask, B, S)
+            if key_bias is not None and (D != 128 or S % 4):
+                raise ValueError("a padded attention_mask needs head_dim 128 and S % 4 == 0")
         Q = query_states.contiguous()
         # [B, S, Hkv·D] keys/values as the reference reshapes them for the compressor (:104-107)
         k_bsf = key_states.transpose(1, 2).reshape(B, S, Hkv * D).contiguous()
         v_bsf = value_states.transpose(1, 2).reshape(B, S, Hkv * D).contiguous()
-        lse = attention_lse(Q, k_bsf, causal=True, k_layout="bsf")
+        lse = attention_lse(Q, k_bsf, causal=True, k_layout="bsf", key_bias=key_bias)
         ids = input_ids if input_ids is not None else torch.zeros(B, S, dtype=torch.long, device=Q.device)
         k2, v2, info = self.compressor.compress_layer_kv_cache(k_bsf, v_bsf, None, ids, self.layer_idx,
-                                                               query_states=Q, attention_lse=lse)
+                                                               query_states=Q, attention_lse=lse,
+                                                               key_padding_bias=key_bias)
         Sp = k2.shape[1]
         ck = k2.view(B, Sp, Hkv, D).transpose(1, 2)
         cv = v2.view(B, Sp, Hkv, D).transpose(1, 2)
@@ -91,15 +101,21 @@ class CompressedPrefillAttention:
                 kp.scatter_(1, tgt, torch.arange(S, device=Q.device).expand(B, S))
                 kept_pos = kp[:, :Sp]
                 mask = kept_pos[:, None, None, :] <= torch.arange(S, device=Q.device)[None, None, :, None]
-                # a query before the first kept position sees no key: its output is zero
+                if valid_key is not None:  # kept padding tokens stay masked
+                    vk = torch.cat([valid_key, valid_key.new_zeros(B, 1)], 1).gather(1, kept_pos)
+                    mask = mask & vk[:, None, None, :]
+                # a query that sees no key (before the first kept position, or padding): zero output
                 empty = ~mask.any(dim=-1, keepdim=True)
                 mask = mask | empty
+            elif attention_mask is not None:
+                # the reference: the first S' columns of the model's mask (:131-134)
+                mask = attention_mask[..., :S, :Sp].to(Q.dtype)
             else:
-                # the reference: the first S' columns of the causal mask (:131-134)
+                # ... of the causal mask the model builds when it is given none
                 mask = torch.ones(S, S, dtype=torch.bool, device=Q.device).tril()[:, :Sp][None, None]
         else:
             keys, vals = key_states, cv  # original weights with the compressed values (:139-140)
-            mask = None
+            mask = None if attention_mask is None or key_bias is None else attention_mask[..., :S, :S].to(Q.dtype)
         if g > 1:
             keys = keys.repeat_interleave(g, dim=1)
             vals = vals.repeat_interleave(g, dim=1)
@@ -109,4 +125,36 @@ class CompressedPrefillAttention:
             out = Fn.scaled_dot_product_attention(Q, keys, vals, attn_mask=mask)
             if Sp != S and self.position_mask:
                 out = out.masked_fill(empty, 0.0)
+            elif mask.dtype != torch.bool:
+                # a query row the model's mask hides every key from (padding): the reference's softmax
+                # of equal logits is uniform, so its output is the mean of the values (SDPA kernels may
+                # return zeros for such rows)
+                blind = (mask <= torch.finfo(mask.dtype).min / 2).all(-1, keepdim=True)   # [B|1, 1, S, 1]
+                out = torch.where(blind, vals.mean(dim=2, keepdim=True).to(out.dtype), out)
         return out, (ck, cv), info
+
+
+def split_attention_mask(attention_mask: torch.Tensor, B: int, S: int):
+    """The model's additive mask [B or 1, 1, S, >=S] → (key_bias, valid_key): None, None for the plain
+    causal mask; else the fp32 [B, S] key bias (0 real key, -inf padding key) and the bool [B, S]
+    key validity, when the mask is exactly causal ∧ key-padding.  Anything else raises ValueError."""
+    if attention_mask.dim() != 4 or attention_mask.shape[1] != 1 or attention_mask.shape[0] not in (1, B) \
+            or attention_mask.shape[2] < S or attention_mask.shape[3] < S:
+        raise ValueError(f"attention_mask must be [B, 1, S, S] (got {tuple(attention_mask.shape)})")
+    m = attention_mask[..., :S, :S]
+    if not m.dtype.is_floating_point:
+        raise ValueError("attention_mask must be the model's additive (floating-point) mask")
+    masked = m <= torch.finfo(m.dtype).min / 2
+    if not bool(((m == 0) | masked).all()):
+        raise ValueError("attention_mask entries must be 0 or <= finfo.min/2 (an additive causal + padding mask)")
+    visible = ~masked[:, 0]                                   # [B|1, S, S]
+    valid_key = visible[:, S - 1, :]                          # the last query sees every unpadded key
+    causal = torch.ones(S, S, dtype=torch.bool, device=m.device).tril()
+    if not bool(torch.equal(visible, causal[None] & valid_key[:, None, :])):
+        raise ValueError("attention_mask is not a causal mask with key padding (unsupported by the fused "
+                         "importance mode)")
+    valid_key = valid_key.expand(B, S)
+    if bool(valid_key.all()):
+        return None, None
+    bias = torch.zeros(B, S, dtype=torch.float32, device=m.device).masked_fill_(~valid_key, float("-inf"))
+    return bias.contiguous(), valid_key.contiguous()

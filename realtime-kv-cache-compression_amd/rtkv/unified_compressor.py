@@ -16,7 +16,7 @@ import torch
 
 from . import _lib as L
 from .dynamic_quantization import F16_OVERFLOW_MSG, DynamicPrecisionQuantizer
-from .engine import (EarlyStatsBuffer, LayerBuffers, Workspace, compress_layer, compress_layer_qk, params_from_config,
+from .engine import (EarlyStatsBuffer, LayerBuffers, Workspace, compress_layer_begin, params_from_config,
                      prompt_length)
 from .selective_propagation import SelectiveTokenPropagator
 from .token_importance import LayerWiseImportanceTracker
@@ -72,6 +72,11 @@ class _LazyDict(dict):
         return repr(self.copy())
 
 
+def _synced(ev):
+    ev.synchronize()
+    return ev
+
+
 class RealTimePrefillCompressor:
     """Prompt-guided importance → dynamic precision → selective propagation, per layer."""
 
@@ -101,7 +106,8 @@ class RealTimePrefillCompressor:
                                 attention_weights: Optional[torch.Tensor], input_ids: torch.Tensor,
                                 layer_idx: int, query_states: Optional[torch.Tensor] = None,
                                 attention_lse: Optional[torch.Tensor] = None,
-                                causal: bool = True) -> Tuple[torch.Tensor, torch.Tensor, Dict]:
+                                causal: bool = True,
+                                key_padding_bias: Optional[torch.Tensor] = None) -> Tuple[torch.Tensor, torch.Tensor, Dict]:
         """K, V [B,S,F] + attention [B,H,S,S] (or its [B,H,S,P] prompt columns) → (K', V', info).
 
         K', V' are the dequantized kept rows in ascending token order, zero-padded across the batch,
@@ -110,11 +116,16 @@ class RealTimePrefillCompressor:
         Fused importance mode (extension): pass attention_weights=None with
         query_states [B,H,S,D] and attention_lse [B,H,S] (fp32 row log-sum-exp of the model's
         softmax); the prompt-attention mass is then computed on MFMA from Q, the first P keys and the
-        LSE (rtkv_compress_layer_qk) — within tolerance of the W path, not bit-exact."""
+        LSE (rtkv_compress_layer_qk) — within tolerance of the W path, not bit-exact.
+        key_padding_bias [B,S] (fp32, 0 real key / -inf padding key): the key-padding part of the
+        model's attention_mask in that mode (the same bias the lse was computed with)."""
         start_time = time.time()
         fused = attention_weights is None
         if fused and (query_states is None or attention_lse is None):
             raise ValueError("attention_weights=None needs query_states and attention_lse (fused importance mode)")
+        if key_padding_bias is not None and not fused:
+            raise ValueError("key_padding_bias applies to the fused importance mode (attention_weights=None); "
+                             "attention weights already carry the model's mask")
         L.require_device(key_states, value_states, *((query_states, attention_lse) if fused else (attention_weights,)))
         K = key_states if key_states.stride(-1) == 1 else key_states.contiguous()
         V = value_states if value_states.stride() == K.stride() else value_states.contiguous()
@@ -131,23 +142,31 @@ class RealTimePrefillCompressor:
             emit_packed = False
         flags = L.EMIT_DEQUANT | (L.EMIT_PACKED if emit_packed else 0)
         params = params_from_config(self.config, layer_idx, P, ratio, flags)
-        bufs = LayerBuffers(B, S, F, K.dtype, K.device, bits, emit_dequant=True, emit_packed=emit_packed)
+        # per-token buffers only: K'/V' and the packed codes are allocated at their exact sizes once S' is
+        # known (rtkv_compress_layer_begin / _finish), so a layer retains 2·S'·F elements + its codes
+        bufs = LayerBuffers(B, S, F, K.dtype, K.device, bits, emit_dequant=True, emit_packed=emit_packed, outputs=False)
         ws = self._workspaces.get(K.device)
         if ws is None:
             ws = self._workspaces[K.device] = Workspace(K.device)
         early = self._early.get(K.device)
         if early is None:
             early = self._early[K.device] = EarlyStatsBuffer()
+        t_start = torch.cuda.Event(enable_timing=True)
+        t_start.record()
         if fused:
             Q = query_states if query_states.stride(-1) == 1 else query_states.contiguous()
-            res = compress_layer_qk(K, V, Q, attention_lse.contiguous(), params, bufs, ws, causal=causal, early=early)
+            res = compress_layer_begin(K, V, None, params, bufs, ws, early, Q=Q, lse=attention_lse.contiguous(),
+                                       causal=causal, key_bias=key_padding_bias)
         else:
-            res = compress_layer(K, V, W, params, bufs, ws, early=early)
+            res = compress_layer_begin(K, V, W, params, bufs, ws, early)
         # the one host wait of the layer: the device publishes S' and the counts as soon as K2 has its
-        # thresholds, so the views below are built while K2's tail and K4 still run (stream-ordered)
+        # thresholds; the exactly-sized outputs are allocated then and K4 is enqueued into them
         st = res.stats()
         if st.error_flags & L.FLAG_F16_QMAX_OVERFLOW:
             raise RuntimeError(F16_OVERFLOW_MSG)
+        res.finish()
+        t_end = torch.cuda.Event(enable_timing=True)
+        t_end.record()
         selected_keys, selected_values = res.kv()
         Sp = st.max_kept
         scores = bufs.scores
@@ -176,10 +195,13 @@ class RealTimePrefillCompressor:
         def std_score():
             m2 = res.final_stats().score_m2
             return (m2 / (n - 1)) ** 0.5 if n > 1 else float("nan")
-        processing_time = time.time() - start_time
-        compression_info = {
+        host_time = time.time() - start_time
+        # processing_time: the layer's device time, K1 start to K4 end (HIP events on the stream; read,
+        # with its wait, on first access).  host_return_time: when this call returned (K4 still running).
+        compression_info = _LazyDict({
             "layer_idx": layer_idx,
-            "processing_time": processing_time,
+            "processing_time": _Lazy(lambda: t_start.elapsed_time(_synced(t_end)) / 1e3),
+            "host_return_time": host_time,
             "original_shape": key_states.shape,
             "compressed_shape": selected_keys.shape,
             "compression_ratio": compression_ratio,
@@ -189,11 +211,11 @@ class RealTimePrefillCompressor:
             "precision_stats": precision_stats,
             "quantization_info": quant_info,
             "propagation_info": propagation_info,
-        }
+        })
         if emit_packed:
             compression_info["packed"] = {
-                "codes_k": bufs.packed_k[: st.total_packed_bytes],
-                "codes_v": bufs.packed_v[: st.total_packed_bytes],
+                "codes_k": res.packed_k[: st.total_packed_bytes],
+                "codes_v": res.packed_v[: st.total_packed_bytes],
                 "row_offset": bufs.row_offset[:, :Sp],
                 "scale_zp": bufs.scale_zp[:, :Sp],
                 "kept_index": bufs.kept_index[:, :Sp],
@@ -203,6 +225,7 @@ class RealTimePrefillCompressor:
                 "dtype": K.dtype,
                 "feature_dim": F,
             }
+        res.k_out = res.v_out = None  # the caller owns K'/V'; nothing kept here pins them
         self.layer_states[layer_idx] = compression_info
         return selected_keys, selected_values, compression_info
 

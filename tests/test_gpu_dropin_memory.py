@@ -1,0 +1,78 @@
+"""GPU: what the drop-in (RealTimePrefillCompressor.compress_layer_kv_cache) allocates and retains.
+
+The reference returns K'/V' of exactly S' rows (selective_propagation.py:214-232,
+unified_compressor.py:170).  rtkv sizes them from the early statistics (rtkv_compress_layer_begin /
+_finish), so a layer's K'/V' hold 2·B·S'·F elements, its packed codes exactly their bytes, and the
+compressor's layer_states keep only per-token buffers and the packed codes: once the caller drops K'/V'
+nothing pins them, and reset_compression_state() releases the rest."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module", autouse=True)
+def gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no ROCm device")
+
+
+def _round(n):  # the caching allocator's granule (memory_allocated counts rounded block sizes)
+    return (n + 511) // 512 * 512
+
+
+# A block the caching allocator hands out may exceed the request by up to 1 MiB (it does not split off
+# a remainder of <= 1 MiB from a cached segment); two large allocations per layer (K'+V', the codes).
+SLACK = 2 * (1 << 20) + 256 * 1024
+
+
+@pytest.mark.parametrize("dtype", ["float16", "float32"])
+def test_dropin_retains_exactly_the_kept_rows(dtype):
+    import rtkv
+    S, H, D, layers = 8192, 32, 128, 6
+    F = H * D
+    td = getattr(torch, dtype)
+    esz = torch.tensor([], dtype=td).element_size()
+    cfg = rtkv.CompressionConfig(alpha=0.8, beta=0.1, gamma=0.1, theta_h=0.4, theta_m=0.25, num_hidden_layers=layers,
+                                 high_precision_bits=8, medium_precision_bits=4, low_precision_bits=2,
+                                 early_layer_ratio=0.8, middle_layer_ratio=0.6, later_layer_ratio=0.4)
+    g = torch.Generator(device="cuda").manual_seed(5)
+    P = rtkv.prompt_length(S)
+    ins = []
+    for _ in range(layers):
+        K = torch.randn(1, S, F, device="cuda", generator=g).to(td)
+        V = torch.randn(1, S, F, device="cuda", generator=g).to(td)
+        u = torch.rand(1, H, S, P, device="cuda", generator=g)
+        W = ((u * u) ** 2 + 1e-6)
+        W = (W / W.sum(-1, keepdim=True) * torch.rand(1, H, S, 1, device="cuda", generator=g)).to(td)
+        ins.append((K, V, W))
+    ids = torch.zeros(1, S, dtype=torch.long, device="cuda")
+    comp = rtkv.RealTimePrefillCompressor(cfg)
+    comp.compress_layer_kv_cache(*ins[0], ids, 0)  # workspace + early-stats buffer exist from here on
+    comp.reset_compression_state()
+    torch.cuda.synchronize()
+    base = torch.cuda.memory_allocated()
+    kept = []
+    for l, (K, V, W) in enumerate(ins):
+        kept.append(comp.compress_layer_kv_cache(K, V, W, ids, l)[:2])
+    torch.cuda.synchronize()
+    grown = torch.cuda.memory_allocated() - base
+    rows = [k.shape[1] for k, _ in kept]
+    packed = [int(comp.layer_states[l]["packed"]["codes_k"].numel()) for l in range(layers)]
+    meta = 34 * S + 4096  # per layer: scores, classes, mask, kept index, row offset, scale/zero-point, stats
+    exact = sum(_round(2 * r * F * esz) + _round(2 * ((pb + 255) // 256 * 256)) + meta for r, pb in zip(rows, packed))
+    assert all(0 < r < S for r in rows)
+    assert grown <= exact + SLACK * layers, (grown, exact)
+    # capacity-sized outputs (S rows of K'/V' and S rows of 8-bit codes per tensor) would not fit that bound
+    assert exact + SLACK * layers < layers * (2 * S * F * esz + 2 * S * F)
+    # the caller drops K'/V': nothing the compressor keeps pins them
+    del kept
+    torch.cuda.synchronize()
+    held = torch.cuda.memory_allocated() - base
+    assert held <= sum(_round(2 * ((pb + 255) // 256 * 256)) + meta for pb in packed) + SLACK * layers, held
+    info = comp.layer_states[layers - 1]
+    assert info["packed"]["codes_k"].numel() == packed[-1] and info["processing_time"] > 0
+    del info  # (it references the layer's codes)
+    comp.reset_compression_state()
+    torch.cuda.synchronize()
+    assert torch.cuda.memory_allocated() - base <= 256 * 1024

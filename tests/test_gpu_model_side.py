@@ -91,8 +91,8 @@ def test_compressed_prefill_attention(B, H, Hkv, S, dtype, ratio, pmask):
 
 
 def test_attention_mask_and_dtype_limits():
-    """The plain causal mask is accepted (same output as no mask); a padded mask and fp32 states are
-    rejected at the boundary instead of being scored as unpadded / run on the wrong kernels."""
+    """The plain causal mask is accepted (same output as no mask); masks that are not causal + key
+    padding, a padded mask at head_dim 64 and fp32 states at head_dim 64 are rejected at the boundary."""
     from rtkv.model_side import CompressedPrefillAttention
     B, H, S, D = 2, 8, 256, 64
     g = torch.Generator(device="cuda").manual_seed(5)
@@ -106,7 +106,15 @@ def test_attention_mask_and_dtype_limits():
     assert torch.equal(out0, out1)
     padded = mask.clone()
     padded[1, :, :, :7] = neg  # left padding of batch row 1
-    with pytest.raises(ValueError, match="causal"):
+    with pytest.raises(ValueError, match="head_dim 128"):
         layer(Q, K, V, attention_mask=padded)
-    with pytest.raises(ValueError, match="float16/bfloat16"):
+    window = mask.clone()
+    window[:, :, 100:, :3] = neg  # a sliding-window-like mask: not causal + key padding
+    with pytest.raises(ValueError, match="causal"):
+        layer(Q, K, V, attention_mask=window)
+    odd = mask.clone()
+    odd[0, 0, 5, 0] = -3.0  # an additive bias that is neither 0 nor a mask value
+    with pytest.raises(ValueError, match="0 or"):
+        layer(Q, K, V, attention_mask=odd)
+    with pytest.raises(ValueError, match="head_dim 128"):
         layer(Q.float(), K.float(), V.float())
