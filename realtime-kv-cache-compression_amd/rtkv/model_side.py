@@ -107,19 +107,21 @@ class CompressedPrefillAttention:
                 # a query that sees no key (before the first kept position, or padding): zero output
                 empty = ~mask.any(dim=-1, keepdim=True)
                 mask = mask | empty
-            elif attention_mask is not None:
-                # the reference: the first S' columns of the model's mask (:131-134)
+            elif key_bias is not None:
+                # the reference: the first S' columns of the model's (padded) mask (:131-134)
                 mask = attention_mask[..., :S, :Sp].to(Q.dtype)
             else:
-                # ... of the causal mask the model builds when it is given none
-                mask = torch.ones(S, S, dtype=torch.bool, device=Q.device).tril()[:, :Sp][None, None]
+                # the first S' columns of the causal mask: tril(ones(S, S'))[i, j] = j <= i, which is
+                # SDPA's is_causal for S queries over S' < S keys (upper-left aligned), so the fused
+                # causal kernels run instead of a masked one
+                mask = None
         else:
             keys, vals = key_states, cv  # original weights with the compressed values (:139-140)
             mask = None if attention_mask is None or key_bias is None else attention_mask[..., :S, :S].to(Q.dtype)
         if g > 1:
             keys = keys.repeat_interleave(g, dim=1)
             vals = vals.repeat_interleave(g, dim=1)
-        if mask is None:
+        if mask is None:  # causal: over S keys, or upper-left over the S' kept keys (see above)
             out = Fn.scaled_dot_product_attention(Q, keys, vals, is_causal=True)
         else:
             out = Fn.scaled_dot_product_attention(Q, keys, vals, attn_mask=mask)

@@ -20,6 +20,7 @@ for s in ${STEPS:-smoke pytest bench}; do
     shardp) step shardp 900 python -u -m pytest tests/test_gpu_shard_procs.py tests/test_gpu_shard.py -q -x -p no:cacheprovider --timeout 300 --timeout-method thread ;;
     fused)  step fused 600 python -u -m pytest tests/test_gpu_fused.py tests/test_gpu_early.py -q -x -p no:cacheprovider --timeout 120 --timeout-method thread ;;
     targ)   step targ 900 python -u -m pytest ${TESTS:-tests/test_gpu_f32_masks.py} -q -x -p no:cacheprovider --timeout 120 --timeout-method thread ;;
+    profprefill) step profprefill 900 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/profprefill -o run -- python3 bench.py --steps 1 --warmup 1 --legs prefill_7b --prefill-modes ${PREFILL_MODES:-none,fused} --cpu-baseline-seconds 0 ;;
     pytestall) step pytest_gpu 1200 python -m pytest tests -m gpu -q -p no:cacheprovider ;;
     bench)  step bench 600 python bench.py ${BENCH_ARGS:-} ;;
     prof)   step rocprof 900 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python3 bench.py --steps 5 --warmup 1 --legs none --cpu-baseline-seconds 0 ;;
