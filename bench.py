@@ -450,7 +450,8 @@ def cpu_baseline(args, job):
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     import numpy as np
     import rtkv_oracle as orc
-    threads = os.cpu_count() or 1
+    affinity = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    threads = affinity
     if os.environ.get("OMP_NUM_THREADS", "").isdigit():   # the host-core share of this job (16 on the GPU box)
         threads = max(1, min(threads, int(os.environ["OMP_NUM_THREADS"])))
     code = {torch.float32: 0, torch.float16: 1, torch.bfloat16: 2}[job.dtype]
@@ -471,6 +472,8 @@ def cpu_baseline(args, job):
         if secs >= args.cpu_baseline_seconds:
             break
     return {"value": round(nbytes / secs / 1e9, 4), "unit": "GB/s", "cores": threads, "host_cpus": os.cpu_count(),
+            "affinity_cpus": affinity,
+            "threads_rule": "min(OMP_NUM_THREADS, CPUs in this process's affinity mask): the job's host-core share",
             "kind": "port", "ms_per_layer": round(secs / n * 1e3, 1),
             "sample": f"{n} of {args.layers} layers (S={job.S}, {job.H}x{job.D}, {args.dtype}), C oracle "
                       f"oracle/rtkv_oracle.c, OpenMP on {threads} host threads (aggregation and per-row "

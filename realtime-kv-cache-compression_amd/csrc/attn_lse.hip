@@ -23,6 +23,8 @@
 
 namespace rtkv {
 
+int launch_attention_lse32(const rtkv_qk_desc& q, float* lse, hipStream_t st);  // attn_lse32.hip
+
 namespace {
 
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
@@ -50,7 +52,8 @@ constexpr float kLFloor = -1e30f;  // initial running max
 struct LseArgs {
   rtkv_qk_desc q;
   float* lse;
-  int nblk;  // query blocks per (b, h)
+  int nblk;       // query blocks per (b, h)
+  int fixup = 0;  // recompute only the row blocks whose lse is +inf / NaN (after attn_lse32_kernel)
 };
 
 __device__ __forceinline__ void lds_dma16(const void* g, void* lds_base) {
@@ -82,6 +85,14 @@ __global__ __launch_bounds__(256, RG == 1 ? LSE_WPE : 1) void attn_lse_kernel(Ls
   const int S = (int)q.S, grp = (int)(q.H / q.Hkv);
   const int i0 = qb * kLRows;
   const int wrow0 = i0 + wave * 16 * RG;     // the wave's rows: RG groups of 16 from here
+  if (g.fixup) {  // the fix-up pass of attn_lse32.hip: blocks whose every lse is valid end here
+    int bad = 0;
+    if ((int)threadIdx.x < kLRows && i0 + (int)threadIdx.x < S) {
+      const float v = g.lse[b * q.lse_stride_b + (int64_t)h * q.lse_stride_h + i0 + threadIdx.x];
+      bad = v != v || v == INFINITY;
+    }
+    if (!__syncthreads_or(bad)) return;
+  }
   const float sc = q.scale * 1.4426950408889634f, inv_scale = 1.f / q.scale;
   const S_* Kh = static_cast<const S_*>(q.k_dev) + b * q.k_stride_b + (int64_t)(h / grp) * q.k_stride_h;
   // key rows this block needs: causal → up to its last query row (global position row0 + i)
@@ -286,9 +297,22 @@ int launch_attention_lse(const rtkv_qk_desc& q, float* lse, hipStream_t st) {
                    q.k_stride_h % 8 == 0 && q.k_stride_b % 8 == 0 && ((uintptr_t)q.q_dev % 16) == 0 &&
                    ((uintptr_t)q.k_dev % 16) == 0,
                "attention_lse: Q/K rows must be 16-byte aligned");
+  // head_dim 128: the 32x32x16 tiling (attn_lse32.hip); RTKV_LSE_KERNEL=16 keeps the 16x16x32 one
+  // (measurement knob)
+  static const bool t16 = [] {
+    const char* e = std::getenv("RTKV_LSE_KERNEL");
+    return e && std::atoi(e) == 16;
+  }();
   LseArgs a;
   a.q = q;
   a.lse = lse;
+  if (q.D == 128 && !t16) {
+    const int rc = launch_attention_lse32(q, lse, st);
+    if (rc) return rc;
+    a.fixup = 1;  // rows whose unchecked sum overflowed: recomputed by the checked kernel
+    if (q.dtype == RTKV_F16) return launch_lse_tpl<RTKV_F16, 4, 1>(a, q, st);
+    return launch_lse_tpl<RTKV_BF16, 4, 1>(a, q, st);
+  }
   const int ks = (int)(q.D / 32), rg = lse_row_groups();
 #define RTKV_L(DT, K, R) \
   if (q.dtype == DT && ks == K && rg == R) return launch_lse_tpl<DT, K, R>(a, q, st);

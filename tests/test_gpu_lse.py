@@ -72,6 +72,24 @@ def test_fused_importance_from_own_lse():
     torch.testing.assert_close(A, A_ref, rtol=1e-3, atol=1e-6)
 
 
+@pytest.mark.parametrize("dtype", [torch.float16, torch.bfloat16])
+def test_overflow_rows_take_the_fixup_pass(dtype):
+    """The 32x32 kernel sums against each row's first logit unchecked; a later logit ~180 log2 units
+    above it overflows the sum, and the fix-up pass must recompute those rows (attn_lse32.hip)."""
+    import rtkv
+    B, H, S, D = 1, 4, 1024, 128
+    g = torch.Generator(device="cuda").manual_seed(9)
+    Q = torch.randn(B, H, S, D, device="cuda", generator=g)
+    K = torch.randn(B, H, S, D, device="cuda", generator=g)
+    K[:, :, 700] = 4.0   # one key aligned with the boosted queries: q·k·scale ≈ 181 → 261 in log2 units
+    Q[:, :, 800:900] = 4.0
+    Q, K = Q.to(dtype), K.to(dtype)
+    lse = rtkv.attention_lse(Q, K)
+    ref = ref_lse(Q, K, True, 1.0 / D ** 0.5)
+    assert torch.isfinite(lse).all()
+    torch.testing.assert_close(lse, ref, rtol=1e-5, atol=2e-4)
+
+
 def test_rejects_unsupported():
     import rtkv
     Q = torch.zeros(1, 2, 64, 96, device="cuda", dtype=torch.float16)
