@@ -326,10 +326,16 @@ __device__ __forceinline__ void row_minmax(const Chunk<DT> (&raw)[NCH], int nch,
 
 // Quantize, pack, dequantize and store one row (one chunk at a time): packed codes at pk (w bits per
 // element) and the dequantized row at orow, either output optional.
+//
+// stage (fp32, CONTIG && FULL only; null elsewhere): a wave-private 2 KiB LDS buffer through which the
+// dequantized chunks are stored.  A lane's 8-element fp32 chunk is 32 B, so two direct 16-byte stores
+// per chunk each cover every other 16 B of the wave's 2 KiB span — partial 128-byte lines, which the
+// memory side counted as ~8 % extra write and ~5 % extra read traffic (profiles/r03_k4_traffic_split.json).
+// Through the stage, each store instruction writes 1 KiB contiguous (lane l: bytes 16l..16l+15).
 template <int DT, int NCH, bool CONTIG, bool FULL>
 __device__ __forceinline__ void emit_row(const Chunk<DT> (&raw)[NCH], const RowParams& rp, bool row_nan, int w,
                                        typename Dt<DT>::S* orow, const int (&out_off)[NCH], uint8_t* pk, int nch,
-                                       int lane, bool emit_deq, bool emit_pk) {
+                                       int lane, bool emit_deq, bool emit_pk, float4* stage = nullptr) {
   auto valid = [&](int k) { return FULL || (k * 64 + lane) < nch; };
   // ---- quantize, pack, dequantize, store (one chunk at a time)
   // DEQ = false (packed codes only): the code is clamp(rint(t), 0, qmax) as an integer — v_cvt_u32_f32
@@ -363,6 +369,19 @@ __device__ __forceinline__ void emit_row(const Chunk<DT> (&raw)[NCH], const RowP
           qi[e] = (uint32_t)q;
         }
         if (emit_pk) pack_store<W>(pk + c * W, qi, aligned);
+        if constexpr (DT == RTKV_F32 && CONTIG && FULL) {
+          if (stage) {  // 2 KiB of the row (chunks k*64 .. k*64+63) through LDS, stored contiguously
+            stage[2 * lane] = make_float4(d[0], d[1], d[2], d[3]);
+            stage[2 * lane + 1] = make_float4(d[4], d[5], d[6], d[7]);
+            const float4 lo = stage[lane], hi = stage[64 + lane];
+            float* blk = reinterpret_cast<float*>(orow) + k * 512;
+            nt_store16(blk + 4 * lane, __float_as_uint(lo.x), __float_as_uint(lo.y), __float_as_uint(lo.z),
+                       __float_as_uint(lo.w));
+            nt_store16(blk + 256 + 4 * lane, __float_as_uint(hi.x), __float_as_uint(hi.y), __float_as_uint(hi.z),
+                       __float_as_uint(hi.w));
+            continue;
+          }
+        }
         store_chunk_nt<DT>(reinterpret_cast<Chunk<DT>*>(orow + out_off[k]), f32_to_chunk<DT>(d));
       } else {
 #pragma unroll
@@ -485,6 +504,11 @@ __global__ __launch_bounds__(256, (DT == RTKV_F32 && NCH == 8 && FULL && CONTIG)
     }
   }
   auto valid = [&](int k) { return FULL || (k * 64 + lane) < nch; };
+  float4* stage = nullptr;  // fp32 dequantized rows go out through a wave-private LDS stage (emit_row)
+  if constexpr (DT == RTKV_F32 && CONTIG && FULL) {
+    __shared__ float4 k4_stage[4][128];  // 256-thread workgroups: 4 waves × 2 KiB
+    stage = k4_stage[wave & 3];
+  }
   for (int t = blockIdx.x * (blockDim.x >> 6) + wave; t < tasks; t += nw) {
     const int which = t & 1;
     const int rr = t >> 1;
@@ -546,7 +570,7 @@ __global__ __launch_bounds__(256, (DT == RTKV_F32 && NCH == 8 && FULL && CONTIG)
     if (a.out.scale_zp_dev && lane < 2) a.out.scale_zp_dev[sz_idx + lane] = lane == 0 ? rp.scale : rp.zp;
     if (emit_pk && !one_row) roff = a.out.row_offset_dev[(int64_t)b * cap + r];
     uint8_t* pk = emit_pk ? (which ? a.out.packed_v_dev : a.out.packed_k_dev) + roff : nullptr;
-    emit_row<DT, NCH, CONTIG, FULL>(raw, rp, row_nan, w, orow, out_off, pk, nch, lane, emit_deq, emit_pk);
+    emit_row<DT, NCH, CONTIG, FULL>(raw, rp, row_nan, w, orow, out_off, pk, nch, lane, emit_deq, emit_pk, stage);
   }
 }
 
