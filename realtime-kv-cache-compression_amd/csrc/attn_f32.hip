@@ -68,8 +68,18 @@ __global__ __launch_bounds__(256) void attn_lse_f32_kernel(LseF32Args g) {
   const rtkv_qk_desc& q = g.q;
   const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int c16 = lane & 15, kg = lane >> 4;
-  const int qb = g.nblk - 1 - (int)blockIdx.x;  // longest-first
-  const int h = blockIdx.y, b = blockIdx.z;
+  // XCD-aware order, as attn_lse32.hip: each XCD runs whole heads (longest query block first), so a
+  // head's keys stay in one L2
+  int qb, h, b;
+  {
+    const int nwg = (int)(gridDim.x * gridDim.y * gridDim.z);
+    int bid = (int)(blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z));
+    if ((nwg & 7) == 0) bid = (bid & 7) * (nwg >> 3) + (bid >> 3);
+    const int unit = bid / g.nblk;
+    qb = g.nblk - 1 - (bid - unit * g.nblk);
+    h = unit % (int)gridDim.y;
+    b = unit / (int)gridDim.y;
+  }
   const int S = (int)q.S, grp = (int)(q.H / q.Hkv);
   const int i0 = qb * 64, wrow0 = i0 + wave * 16, crow0 = wrow0 + 4 * kg;
   const float sc = q.scale * kL2E, inv_scale = 1.f / q.scale;

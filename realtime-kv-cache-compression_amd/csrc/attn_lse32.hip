@@ -76,8 +76,20 @@ __global__ __launch_bounds__(256, 3) void attn_lse32_kernel(Lse32Args g) {
   const rtkv_qk_desc& q = g.q;
   const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int r32 = lane & 31, hh = lane >> 5;
-  const int qb = g.nblk - 1 - (int)blockIdx.x;  // longest-first
-  const int hd = blockIdx.y, b = blockIdx.z;
+  // XCD-aware order (cdna_hip_programming.md T1): workgroups are dealt round-robin over the 8 XCDs, so
+  // the default order spreads every head's query blocks over all 8 L2s and each L2 cycles through the
+  // keys of many heads.  Remapped, XCD x runs a contiguous range of (head, query block) units — whole
+  // heads, longest query block first — and a head's keys (S·256 B) stay in its XCD's L2.
+  int qb, hd, b;
+  {
+    const int nwg = (int)(gridDim.x * gridDim.y * gridDim.z);
+    int bid = (int)(blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z));
+    if ((nwg & 7) == 0) bid = (bid & 7) * (nwg >> 3) + (bid >> 3);
+    const int unit = bid / g.nblk;  // (b, h) pair
+    qb = g.nblk - 1 - (bid - unit * g.nblk);  // longest-first within the head
+    hd = unit % (int)gridDim.y;
+    b = unit / (int)gridDim.y;
+  }
   const int S = (int)q.S, grp = (int)(q.H / q.Hkv);
   const int i0 = qb * kRows, wrow0 = i0 + 32 * wave;
   const float sc = q.scale * 1.4426950408889634f, inv_scale = 1.f / q.scale;
