@@ -19,9 +19,10 @@ Rank 0 prints ONE JSON line.  ``value`` = algorithmic bytes of the whole job ÷ 
 ``ttft_ms`` = the step's wall time with every layer strictly after the previous one (the reference
 caller's order: layer l+1's K/V come out of attention over layer l's compressed K'/V',
 modified_llama.py:113-157), i.e. Σ per-layer compress time;
-``roofline`` = the path's HBM-read roofline as the north star defines it (R = 2·S·H·D·e
-+ H·S·P·e bytes per layer over the per-layer time of the layer's kernels, HIP events on the launch
-stream); ``roofline_k4`` = the dominant kernel (quantize+pack+compact) on its own read+write bytes;
+``roofline`` = the dominant kernel (K4: quantize+pack+compact) on its own algorithmic read+write
+bytes over its average launch time (HIP events on the launch stream); ``roofline_path`` = the path's
+HBM-read roofline as the north star defines it (R = 2·S·H·D·e + H·S·P·e bytes per layer
+over the per-layer time of all the layer's kernels);
 ``cpu_baseline`` = the C oracle (OpenMP restatement of the reference) on a bounded sample of the
 same workload.  Extra legs (``--legs``, single GPU): ``f16`` (the workload in fp16), ``packed_only``
 (codes + scale/zp, no dequantized K'/V' — what the packed consumers read), ``drop_in`` (the reference
@@ -617,8 +618,8 @@ def main():
                                 "per_layer_collective": "RCCL all-gather of A (4 B/token)"}
         else:
             path, k4 = roofline_objects(args, job, kus, k4_bytes)
-            line["roofline"] = path
-            line["roofline_k4"] = k4
+            line["roofline"] = k4  # the contract's object: the dominant kernel (K4) on its algorithmic bytes
+            line["roofline_path"] = path  # the north star's: the whole layer path on its HBM-read bytes
             line["kernel_us_per_layer"] = kernel_us(job, kus)
             if args.importance == "qk":  # K1' on MFMA: the Q·K_P^T contraction against the dense peak
                 flops = 2.0 * job.H * job.S * job.P * job.D

@@ -1,9 +1,11 @@
 """One rank of tests/test_gpu_shard_procs.py (run as its own process; not collected by pytest).
 
-    python tests/shard_procs_worker.py RANK WORLD PORT S_TOTAL H D DTYPE LAYERS B MODE OVERLAP
+    python tests/shard_procs_worker.py RANK WORLD PORT S_TOTAL H D DTYPE LAYERS B MODE OVERLAP [COLL]
 
 Every rank drives rtkv.sharded.ShardedPrefillCompressor with the HIP stages (librtkv.so) on the
-shared GPU, over a gloo group with the exchanges staged through host memory (collectives='host'),
+shared GPU, over a gloo group with the exchanges staged through host memory (COLL = 'host', the
+default), or on its own GPU (cuda:RANK) over an RCCL group with COLL = 'torch' (torch.distributed) or
+'rtkv' (the C ABI's rtkv_comm_* / rtkv_allgather_* collectives),
 then checks what it holds after the exchange against the single-GPU rtkv_compress_layer of the whole
 sequence, computed in this same process from the same seeded inputs: kept indices, row offsets,
 packed K/V codes and scale/zero-point byte for byte, and its own dequantized rows."""
@@ -37,15 +39,22 @@ def inputs(l, B, S, H, D, td, qk):
 def main():
     rank, world, port, S_total, H, D = (int(x) for x in sys.argv[1:7])
     dtype, layers, B, mode, overlap = sys.argv[7], int(sys.argv[8]), int(sys.argv[9]), sys.argv[10], sys.argv[11] == "1"
-    torch.cuda.set_device(0)
-    dist.init_process_group("gloo", rank=rank, world_size=world, init_method=f"tcp://127.0.0.1:{port}")
+    coll = sys.argv[12] if len(sys.argv) > 12 else "host"
+    if coll == "host":
+        torch.cuda.set_device(0)
+        dist.init_process_group("gloo", rank=rank, world_size=world, init_method=f"tcp://127.0.0.1:{port}")
+    else:  # one GPU per rank, RCCL
+        torch.cuda.set_device(rank)
+        dist.init_process_group("nccl", rank=rank, world_size=world, init_method=f"tcp://127.0.0.1:{port}",
+                                device_id=torch.device("cuda", rank))
     import rtkv
     from rtkv.sharded import ShardedPrefillCompressor
     td = getattr(torch, dtype)
     cfg = rtkv.CompressionConfig(alpha=0.8, beta=0.1, gamma=0.1, theta_h=0.4, theta_m=0.25, high_precision_bits=8,
                                  medium_precision_bits=4, low_precision_bits=2, early_layer_ratio=0.8,
                                  middle_layer_ratio=0.6, later_layer_ratio=0.4, num_hidden_layers=layers)
-    comp = ShardedPrefillCompressor(cfg, device="cuda", collectives="host", overlap=overlap)
+    comp = ShardedPrefillCompressor(cfg, device=f"cuda:{torch.cuda.current_device()}", collectives=coll,
+                                    overlap=overlap)
     assert type(comp.stages).__name__ == "HipShardStages"
     S_local = S_total // world
     sl = slice(rank * S_local, (rank + 1) * S_local)
@@ -90,7 +99,8 @@ def main():
             assert torch.equal(k_loc[b, : r1 - r0], kr[b, r0:r1]), "local K' rows"
     dist.barrier()
     dist.destroy_process_group()
-    print(f"rank {rank} ok: {layers} layers, S_total={S_total}, world={world}, {dtype}, B={B}, mode={mode}", flush=True)
+    print(f"rank {rank} ok: {layers} layers, S_total={S_total}, world={world}, {dtype}, B={B}, mode={mode}, "
+          f"collectives={coll}", flush=True)
 
 
 if __name__ == "__main__":
