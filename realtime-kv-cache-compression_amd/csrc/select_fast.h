@@ -935,17 +935,21 @@ __device__ __forceinline__ void k2_body(const FastArgs& g, uint32_t* hist_lds) {
   const int G = (S + kST - 1) / kST;
   const int blk = blockIdx.x;
   K2_WG(0);
+  // this thread's token's A (and β·pos term) in flight together with the min/max partials: the loads
+  // do not depend on the row-wide min/max, and issued here they cost no round trip of their own
+  const int i = blk * kST + t;
+  const bool valid = i < S;
+  const float Ai = valid ? a.A[i] : 0.f;
+  const float T2i = (HAS_T2 && valid) ? a.T2[i] : 0.f;
   float mn, mx;
   amin_amax(a, mn, mx);
   K2_WG(1);
   const float den = Dt<DT>::rnd(mx - mn), eps = Dt<DT>::rnd(1e-8f);
   // ---- phase 1: this thread's token: score, class
-  const int i = blk * kST + t;
-  const bool valid = i < S;
   float s = 0.f;
   int l = 0;
   if (valid) {
-    s = token_score<DT, HAS_T2>(a, i, a.A[i], HAS_T2 ? a.T2[i] : 0.f, mn, den, eps);
+    s = token_score<DT, HAS_T2>(a, i, Ai, T2i, mn, den, eps);
     l = class_of(s, a.p);
     st_sc1(a.scores + i, s);
     a.labels[i] = (uint8_t)l;
