@@ -135,20 +135,23 @@ __device__ __forceinline__ uint32_t wave_scan_dpp(uint32_t v) {
   return (uint32_t)x;
 }
 
-__device__ __forceinline__ uint32_t block_excl_scan32(uint32_t v, uint32_t* sh, uint32_t* total) {
+// Exclusive block scan of four packed 16-bit fields (block totals < 65536 each) as two 32-bit DPP
+// scans sharing one barrier: the threshold bins of every partially kept group in one pass.
+// `sh` is a [2][kSW] LDS array private to the call site.
+__device__ __forceinline__ uint64_t block_excl_scan16x4(uint64_t v, uint32_t (*sh)[kSW]) {
   const int lane = threadIdx.x & (kWave - 1), wid = threadIdx.x / kWave;
-  const uint32_t inc = wave_scan_dpp(v);
-  if (lane == kWave - 1) sh[wid] = inc;
+  const uint32_t lo = (uint32_t)v, hi = (uint32_t)(v >> 32);
+  const uint32_t ilo = wave_scan_dpp(lo), ihi = wave_scan_dpp(hi);
+  if (lane == kWave - 1) { sh[0][wid] = ilo; sh[1][wid] = ihi; }
   __syncthreads();
-  uint32_t ws = sh[lane & (kSW - 1)];
+  uint32_t wlo = sh[0][lane & (kSW - 1)], whi = sh[1][lane & (kSW - 1)];
 #pragma unroll
   for (int o = 1; o < kSW; o <<= 1) {
-    const uint32_t n = __shfl_up(ws, o, kWave);
-    if ((lane & (kSW - 1)) >= o) ws += n;
+    const uint32_t nlo = __shfl_up(wlo, o, kWave), nhi = __shfl_up(whi, o, kWave);
+    if ((lane & (kSW - 1)) >= o) { wlo += nlo; whi += nhi; }
   }
-  *total = __shfl(ws, kSW - 1, kWave);
-  const uint32_t base = wid > 0 ? __shfl(ws, wid - 1, kWave) : 0u;
-  return base + inc - v;
+  const uint32_t blo = wid > 0 ? __shfl(wlo, wid - 1, kWave) : 0u, bhi = wid > 0 ? __shfl(whi, wid - 1, kWave) : 0u;
+  return ((uint64_t)(bhi + ihi - hi) << 32) | (uint64_t)(blo + ilo - lo);
 }
 
 // Ranks in thread order of NF one-bit flags per thread, and their workgroup totals, from wave
@@ -236,7 +239,13 @@ __device__ __forceinline__ uint64_t from11(uint64_t v11, int n) {
 // among those peers (the slot order within a bin is arbitrary anyway: slot lists are ranked by
 // (key, index)).  Attention-like importance piles thousands of tokens into a few bins, where one
 // returning atomic per token serialises on the address (~11 ns each).
-__device__ __forceinline__ uint32_t hist_slot(uint32_t* addr, uint32_t v, bool part) {
+// Split in two so that independent work can run while the atomic is in flight: hist_issue sends it,
+// hist_slot_of (the first use of its return value) waits for it.
+struct HistTicket {
+  uint32_t base;  // the leader's atomic return (pending until hist_slot_of)
+  int leader, below;
+};
+__device__ __forceinline__ HistTicket hist_issue(uint32_t* addr, uint32_t v, bool part) {
   uint64_t peers = __ballot(part);
 #pragma unroll
   for (int k = 0; k < 14; ++k) {
@@ -245,11 +254,15 @@ __device__ __forceinline__ uint32_t hist_slot(uint32_t* addr, uint32_t v, bool p
   }
   const int lane = threadIdx.x & (kWave - 1);
   const uint64_t below = peers & ((1ull << lane) - 1ull);
-  const int leader = peers ? __ffsll((unsigned long long)peers) - 1 : 0;
-  uint32_t base = 0u;
-  if (part && below == 0ull) base = atomicAdd(addr, (uint32_t)__popcll(peers));
-  base = (uint32_t)__shfl((int)base, leader, kWave);
-  return base + (uint32_t)__popcll(below);
+  HistTicket h;
+  h.leader = peers ? __ffsll((unsigned long long)peers) - 1 : 0;
+  h.below = __popcll(below);
+  h.base = 0u;
+  if (part && below == 0ull) h.base = atomicAdd(addr, (uint32_t)__popcll(peers));
+  return h;
+}
+__device__ __forceinline__ uint32_t hist_slot_of(const HistTicket& h) {
+  return (uint32_t)__shfl((int)h.base, h.leader, kWave) + (uint32_t)h.below;
 }
 
 // A 16-byte coherent load (global_load_dwordx4 ... sc1, as ld_sc1 for one word).  The compiler does not
@@ -431,7 +444,7 @@ __device__ __forceinline__ void rescan_thresholds(const FastArgs& g, uint32_t* h
 template <int TPT>
 __device__ __forceinline__ void select_thresholds(const FastArgs& g, uint32_t* hist_lds, uint64_t* s_selw) {
   const FinalizeArgs& a = g.f;
-  __shared__ uint32_t s_scan32[kGrp][kSW];
+  __shared__ uint32_t s_scan32[2][kSW];
   __shared__ uint32_t s_pick[kGrp][3];
   __shared__ uint32_t s_thr[kGrp];
   __shared__ int s_tie[kGrp];
@@ -545,15 +558,20 @@ __device__ __forceinline__ void select_thresholds(const FastArgs& g, uint32_t* h
   uint32_t thr[kGrp] = {0u, 0u, 0u, 0u};
   K2_PROBE(5);
   if (part) {
-    // ---- the bin holding each partial group's threshold: one 32-bit scan per partial group
+    // ---- the bin holding each partial group's threshold: every partial group's bin counts in one
+    // packed scan (16 bits per group: a group's total is at most S <= 32768)
     if (t < kGrp) { s_pick[t][0] = 0u; s_pick[t][1] = 0u; s_pick[t][2] = 0u; }
+    uint64_t pk = 0;
+#pragma unroll
+    for (int q = 0; q < kGrp; ++q)
+      if ((part >> q) & 1) pk |= (uint64_t)(c[q][0] + c[q][1] + c[q][2] + c[q][3]) << (16 * q);
+    const uint64_t ex = block_excl_scan16x4(pk, s_scan32);
+    K2_PROBE(6);
 #pragma unroll
     for (int q = 0; q < kGrp; ++q) {
       if (!((part >> q) & 1)) continue;
-      const uint32_t sum = c[q][0] + c[q][1] + c[q][2] + c[q][3];
-      uint32_t tot;
-      int run = (int)block_excl_scan32(sum, s_scan32[q], &tot);
-      K2_PROBE(6);
+      const uint32_t sum = fld(pk, q);
+      int run = (int)fld(ex, q);
       if (run < need[q] && need[q] <= run + (int)sum) {
         bool found = false;
 #pragma unroll
@@ -974,11 +992,11 @@ __device__ __forceinline__ void k2_body(const FastArgs& g, uint32_t* hist_lds) {
   if (a.mode_select == 1) {  // wave-uniform: every lane takes part in the peer matching
     const uint64_t entry = ((uint64_t)score_key(s) << 32) | (uint32_t)i;
     const int b = l * kNBin + bin_of(s, bin_lo_of(g, l), bin_inv_of(g, l));
-    const uint32_t slot = hist_slot(&g.L.hist[b], (uint32_t)b, valid);
+    const uint32_t slot = hist_slot_of(hist_issue(&g.L.hist[b], (uint32_t)b, valid));
     if (valid && slot < kCap) st_sc1(g.L.slots + (size_t)b * kCap + slot, entry);
     if (g.hist_fb) {
       const int b3 = 3 * kNBin + bin_of(s, g.bin_lo[3], g.bin_inv[3]);
-      const uint32_t slot3 = hist_slot(&g.L.hist[b3], (uint32_t)b3, valid);
+      const uint32_t slot3 = hist_slot_of(hist_issue(&g.L.hist[b3], (uint32_t)b3, valid));
       if (valid && slot3 < kCap) st_sc1(g.L.slots + (size_t)b3 * kCap + slot3, entry);
     }
   }
