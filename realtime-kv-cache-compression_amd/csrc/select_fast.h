@@ -71,9 +71,10 @@ struct FastHead {                  // zeroed before the launch (K1 or a memset):
   uint64_t part[kMaxG];            // phase 1, per workgroup: kTag | class counts (3 x 11 bits), from registers
   uint64_t ready[kMaxG];           // phase 1, per workgroup: kTag once its slot entries, partials, scores and
                                    // classes are complete (drained)
-  uint64_t sel[8];                 // phase 2: [q] kTag | fallback<<50 | mode<<48 | ties<<32 | T; [4], [5] the mean;
-                                   // [6] kTag | kept rows<<16 | fallback<<8 (fused)
-  uint64_t agg[kMaxG][2];          // phase 3, per workgroup: kTag | sure (3 x 11 bits), kTag | ties (4 x 11 bits)
+  uint64_t sel[8];                 // phase 2: [q] kTag | fallback<<50 | mode<<48 | cut<<32 | T; [4], [5] the mean;
+                                   // [6] kTag | kept rows<<16 | fallback<<8 (fused).  cut: the largest token
+                                   // index of group q's ties at T that are kept (ties go in token order)
+  uint64_t agg[kMaxG];             // phase 3, per workgroup: kTag | kept tokens per class (3 x 11 bits)
   uint64_t rowinfo[kMaxS][2];      // fused, phase 3, per kept row r: {kTag | class<<32 | token, kTag | k2<<32 |
                                    // k1<<16 | k0}, k_c = kept rows of class c before it (its packed offset)
 };
@@ -303,11 +304,14 @@ __device__ __forceinline__ uint64_t poll_tagged(const uint64_t* words, int strid
 // from the candidates on entry, tokens at the threshold key on exit.
 template <int TPT>
 __device__ __forceinline__ void rescan_thresholds(const FastArgs& g, uint32_t* hist_lds, int heavy, bool fallback,
-                                                  const int (&bstar)[kGrp], int (&need)[kGrp], uint32_t (&thr)[kGrp]) {
+                                                  const int (&bstar)[kGrp], int (&need)[kGrp], uint32_t (&thr)[kGrp],
+                                                  uint32_t (&cut)[kGrp]) {
   const FinalizeArgs& a = g.f;
   __shared__ uint64_t s_scan[4][kSW];
   __shared__ uint32_t s_key[2 * kGrp][kSW];
   __shared__ uint32_t s_pick[2][kGrp][2];
+  __shared__ uint32_t s_cs[2][kSW];
+  __shared__ uint32_t s_cut[kGrp];
   const int t = threadIdx.x, lane = t & (kWave - 1), wid = t / kWave;
   const int S = (int)a.S;
   const int i0 = t * TPT;
@@ -432,9 +436,43 @@ __device__ __forceinline__ void rescan_thresholds(const FastArgs& g, uint32_t* h
       hi[q] = nhi < (uint64_t)hi[q] ? (uint32_t)nhi : hi[q];
     }
   }
+  // the ties to take at the exact threshold key lo[q] are the first need[q] of the group's tokens at
+  // that key in token order (thread t holds tokens i0..i0+TPT-1, so a block scan of per-thread tie
+  // counts is in token order): the cutoff is the index of the last one taken
+  // (the scores are reloaded, 4 at a time, so that no per-token key stays live past the rounds)
+  uint32_t atm[kGrp] = {0u, 0u, 0u, 0u};
+  opaque(heavy);
+#pragma unroll 1
+  for (int k0 = 0; k0 < TPT; k0 += 4) {
+    float s4[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) s4[j] = ld_sc1(a.scores + (i0 + k0 + j < S ? i0 + k0 + j : S - 1));
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const uint32_t kk = score_key(s4[j]);
+      const int e = fallback ? 3 : class_of(s4[j], a.p);
+#pragma unroll
+      for (int q = 0; q < kGrp; ++q)
+        atm[q] |= (uint32_t)((k0 + j < nv) & (e == q) & (((heavy >> q) & 1) != 0) & (kk == lo[q])) << (k0 + j);
+    }
+  }
+  uint64_t pc = 0;
+#pragma unroll
+  for (int q = 0; q < kGrp; ++q) pc |= (uint64_t)__popc(atm[q]) << (16 * q);
+  const uint64_t ex = block_excl_scan16x4(pc, s_cs);
+#pragma unroll
+  for (int q = 0; q < kGrp; ++q) {
+    const int base = (int)fld(ex, q);
+    if (((heavy >> q) & 1) && base < need[q] && need[q] <= base + (int)fld(pc, q)) {
+      uint32_t m = atm[q];
+      for (int j = base + 1; j < need[q]; ++j) m &= m - 1u;  // drop the ties taken before the last one
+      s_cut[q] = (uint32_t)(i0 + __ffs((int)m) - 1);
+    }
+  }
+  __syncthreads();
 #pragma unroll
   for (int q = 0; q < kGrp; ++q)
-    if ((heavy >> q) & 1) thr[q] = lo[q];
+    if ((heavy >> q) & 1) { thr[q] = lo[q]; cut[q] = s_cut[q]; }
 }
 
 // ------------------------------------------------------------------------------------ phase 2
@@ -447,7 +485,7 @@ __device__ __forceinline__ void select_thresholds(const FastArgs& g, uint32_t* h
   __shared__ uint32_t s_scan32[2][kSW];
   __shared__ uint32_t s_pick[kGrp][3];
   __shared__ uint32_t s_thr[kGrp];
-  __shared__ int s_tie[kGrp];
+  __shared__ uint32_t s_cutw[kGrp];
   __shared__ double s_ssum;
   __shared__ uint32_t s_kr[2];
   __shared__ int s_q[2 * kGrp];
@@ -555,7 +593,7 @@ __device__ __forceinline__ void select_thresholds(const FastArgs& g, uint32_t* h
   int part = 0;
 #pragma unroll
   for (int q = 0; q < kGrp; ++q) part |= (mode[q] == M_PART) << q;
-  uint32_t thr[kGrp] = {0u, 0u, 0u, 0u};
+  uint32_t thr[kGrp] = {0u, 0u, 0u, 0u}, cut[kGrp] = {0u, 0u, 0u, 0u};
   K2_PROBE(5);
   if (part) {
     // ---- the bin holding each partial group's threshold: every partial group's bin counts in one
@@ -616,16 +654,18 @@ __device__ __forceinline__ void select_thresholds(const FastArgs& g, uint32_t* h
       const uint64_t hit = __ballot(lane < n && rank == r - 1);
       const int src = hit ? (__ffsll((unsigned long long)hit) - 1) : 0;
       const uint32_t T = (uint32_t)__shfl((int)k, src, kWave);
-      const uint64_t above = __ballot(lane < n && k > T);
-      if (lane == 0) { s_thr[q] = T; s_tie[q] = r - __popcll(above); }
+      // the r-th token in (key desc, index asc) order is the last one kept: the ties at T with an
+      // index up to its index are kept
+      const uint32_t cut = (uint32_t)__shfl((int)idx, src, kWave);
+      if (lane == 0) { s_thr[q] = T; s_cutw[q] = cut; }
     }
-    if (heavy) rescan_thresholds<TPT>(g, hist_lds, heavy, fallback, bstar, need, thr);
+    if (heavy) rescan_thresholds<TPT>(g, hist_lds, heavy, fallback, bstar, need, thr, cut);
     __syncthreads();
 #pragma unroll
     for (int q = 0; q < kGrp; ++q) {
       if (!((part >> q) & 1) || ((heavy >> q) & 1)) continue;
       thr[q] = s_thr[q];
-      need[q] = s_tie[q];
+      cut[q] = s_cutw[q];
     }
   } else {
     __syncthreads();  // s_ssum / s_kr
@@ -638,7 +678,7 @@ __device__ __forceinline__ void select_thresholds(const FastArgs& g, uint32_t* h
   const uint64_t mb = __builtin_bit_cast(uint64_t, mean);
   for (int q = 0; q < kGrp; ++q) {
     const uint64_t w = kTag | ((uint64_t)(fallback ? 1 : 0) << 50) | ((uint64_t)mode[q] << 48) |
-                       ((uint64_t)(need[q] & 0xffff) << 32) | thr[q];
+                       ((uint64_t)(cut[q] & 0xffff) << 32) | thr[q];
     if (!g.withhold) st_sc1(&g.L.head->sel[q], w);
     s_selw[q] = w;
   }
@@ -712,88 +752,48 @@ __device__ __forceinline__ void select_thresholds(const FastArgs& g, uint32_t* h
 
 // ------------------------------------------------------------------------------------ phase 3
 // Every workgroup: keep decisions for its token (s, l) still in registers, ranked across the row.
-// selw: the selection words in LDS.
+// selw: the selection words in LDS.  A token is kept iff its group takes all of its tokens, or takes
+// part and its key is above the threshold T, or at T with an index up to the group's cutoff (phase 2
+// resolved the ties, which go in token order): a local decision, so the only exchange is the kept
+// count per class for the ranks across workgroups (decoupled look-back).
 __device__ __forceinline__ void compact_phase(const FastArgs& g, float s, int l, int i, bool valid,
                                               const uint64_t* selw) {
   const FinalizeArgs& a = g.f;
-  __shared__ uint32_t s_f7[7][kSW];
   __shared__ uint32_t s_f3[3][kSW];
   __shared__ double s_d[2][kSW];
-  __shared__ uint64_t s_base[2];
+  __shared__ uint64_t s_base;
   const int t = threadIdx.x, lane = t & (kWave - 1), wid = t / kWave;
   const int blk = blockIdx.x;
-  int mode[kGrp], tq[kGrp];
-  uint32_t thr[kGrp];
+  const bool fallback = ((selw[0] >> 50) & 1u) != 0;
+  const double mean = __builtin_bit_cast(double, (selw[4] & 0xffffffffull) | ((selw[5] & 0xffffffffull) << 32));
+  const uint32_t key = score_key(s);
+  const int e = valid ? (fallback ? 3 : l) : 4;
+  bool kept = false;
 #pragma unroll
   for (int q = 0; q < kGrp; ++q) {
     const uint64_t w = selw[q];
-    mode[q] = (int)((w >> 48) & 3u);
-    tq[q] = (int)((w >> 32) & 0xffffu);
-    thr[q] = (uint32_t)w;
+    const int mode = (int)((w >> 48) & 3u);
+    const uint32_t thr = (uint32_t)w, cut = (uint32_t)((w >> 32) & 0xffffu);
+    kept |= (e == q) & ((mode == M_ALL) | ((mode == M_PART) & ((key > thr) | ((key == thr) & ((uint32_t)i <= cut)))));
   }
-  const bool fallback = ((selw[0] >> 50) & 1u) != 0;
-  const double mean = __builtin_bit_cast(double, (selw[4] & 0xffffffffull) | ((selw[5] & 0xffffffffull) << 32));
-  // the class of group q's tokens at its threshold: q for a class; for the fallback group, the class
-  // of the threshold score (equal scores have equal classes)
-  const int tcls3 = class_of(key_score(thr[3]), a.p);
-  const uint32_t key = score_key(s);
-  const int e = valid ? (fallback ? 3 : l) : 4;
-  // ---- flags: surely kept (per class) and ties at T (per group); their in-workgroup ranks and
-  // totals (the aggregates, published before any wait)
-  bool f7[7] = {false, false, false, false, false, false, false};
-  bool sure = false;  // kept regardless of the tie order
-#pragma unroll
-  for (int q = 0; q < kGrp; ++q) {
-    const bool mine = e == q;
-    sure |= mine & ((mode[q] == M_ALL) | ((mode[q] == M_PART) & (key > thr[q])));
-    f7[3 + q] = mine & (mode[q] == M_PART) & (key == thr[q]);
-  }
-#pragma unroll
-  for (int c = 0; c < 3; ++c) f7[c] = sure & (l == c);  // under the token's class (also in the fallback group)
-  uint32_t r7[7], t7[7];
-  block_flag_ranks<7>(f7, r7, t7, s_f7);
-  if (wid == 0) {
-    if (lane == 0) {
-      const uint64_t x = (uint64_t)t7[0] | ((uint64_t)t7[1] << 16) | ((uint64_t)t7[2] << 32);
-      const uint64_t y = (uint64_t)t7[3] | ((uint64_t)t7[4] << 16) | ((uint64_t)t7[5] << 32) | ((uint64_t)t7[6] << 48);
-      st_sc1(&g.L.head->agg[blk][0], kTag | to11(x, 3));
-      st_sc1(&g.L.head->agg[blk][1], kTag | to11(y, 4));
-    }
-    K2_WG(6);
-    // look-back: lane p < blk waits for workgroup p's aggregate
-    const uint64_t w0 = poll_tagged(&g.L.head->agg[0][0], 2, blk, g.spin_limit, a.stats);
-    const uint64_t w1 = poll_tagged(&g.L.head->agg[0][1], 2, blk, g.spin_limit, a.stats);
-    uint64_t ps = lane < blk ? from11(w0 & ~kTag, 3) : 0ull;
-    uint64_t pt = lane < blk ? from11(w1 & ~kTag, 4) : 0ull;
-    // ties that predecessor p takes: those of its ties whose row-wide rank is below the quota
-    const uint64_t before = wave_inclusive_scan(pt) - pt;
-    uint64_t taken = 0;  // per class
-#pragma unroll
-    for (int q = 0; q < kGrp; ++q) {
-      const int b4 = (int)fld(before, q), mine_t = (int)fld(pt, q);
-      int take = tq[q] - b4;
-      take = take < 0 ? 0 : (take > mine_t ? mine_t : take);
-      taken += (uint64_t)take << (16 * (q < 3 ? q : tcls3));
-    }
-    ps = wave_sum(ps);
-    taken = wave_sum(taken);
-    pt = wave_sum(pt);
-    if (lane == 0) { s_base[0] = ps + taken; s_base[1] = pt; }
-  }
-  __syncthreads();
-  K2_WG(7);
-  const uint64_t kept_before = s_base[0], ties_before = s_base[1];
-  // ---- keep decisions (ties by their row-wide rank), then kept-row ranks per class in index order
-  bool take = false;
-#pragma unroll
-  for (int q = 0; q < kGrp; ++q) take |= f7[3 + q] & ((int)(r7[3 + q] + fld(ties_before, q)) < tq[q]);
-  const bool kept = valid & (f7[0] | f7[1] | f7[2] | take);
+  // ---- kept-row ranks per class in index order; the workgroup's counts (the aggregate, published
+  // before any wait) and the predecessors' (look-back)
   bool f3[3];
 #pragma unroll
   for (int c = 0; c < 3; ++c) f3[c] = kept & (l == c);
   uint32_t r3[3], t3[3];
   block_flag_ranks<3>(f3, r3, t3, s_f3);
   const uint64_t kept_tot = (uint64_t)t3[0] | ((uint64_t)t3[1] << 16) | ((uint64_t)t3[2] << 32);
+  if (wid == 0) {
+    if (lane == 0) st_sc1(&g.L.head->agg[blk], kTag | to11(kept_tot, 3));
+    K2_WG(6);
+    const uint64_t w0 = poll_tagged(&g.L.head->agg[0], 1, blk, g.spin_limit, a.stats);
+    const uint64_t ps = wave_sum(lane < blk ? from11(w0 & ~kTag, 3) : 0ull);
+    if (lane == 0) s_base = ps;
+  }
+  __syncthreads();
+  K2_WG(7);
+  const uint64_t kept_before = s_base;
   K2_WG(9);
   int64_t rb[3];
 #pragma unroll

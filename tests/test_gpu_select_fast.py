@@ -81,6 +81,9 @@ CASES = [
     (4096, "float16", 0.5, dict(beta=0.0), "tie"),     # 3 distinct scores: threshold inside a tie block
     (9000, "bfloat16", 0.3, dict(beta=0.0, gamma=0.0), "tie"),
     (5000, "float16", 0.5, dict(beta=0.0), "const"),   # every score equal (den <= eps): pure index order
+    # heavy ties in the 32-tokens-per-thread rescan (16384 < S <= 32768): the tie cutoff index
+    (24576, "float32", 0.4, dict(beta=0.0), "tie"),
+    (32768, "bfloat16", 0.6, dict(beta=0.0), "const"),
 ]
 
 
