@@ -784,6 +784,12 @@ __device__ __forceinline__ void compact_phase(const FastArgs& g, float s, int l,
   uint32_t r3[3], t3[3];
   block_flag_ranks<3>(f3, r3, t3, s_f3);
   const uint64_t kept_tot = (uint64_t)t3[0] | ((uint64_t)t3[1] << 16) | ((uint64_t)t3[2] << 32);
+  // statistics partials (Σ kept scores, Σ (s - mean)^2) per wave, while wave 0 waits on the look-back
+  {
+    const double d = (double)s - mean;
+    const double ks = wave_sum(kept ? (double)s : 0.0), m2 = wave_sum(valid ? d * d : 0.0);
+    if (lane == 0) { s_d[0][wid] = ks; s_d[1][wid] = m2; }
+  }
   if (wid == 0) {
     if (lane == 0) st_sc1(&g.L.head->agg[blk], kTag | to11(kept_tot, 3));
     K2_WG(6);
@@ -815,12 +821,9 @@ __device__ __forceinline__ void compact_phase(const FastArgs& g, float s, int l,
       }
     }
   }
-  // ---- statistics: Σ kept scores, Σ (s - mean)^2 and the kept-token counts, added per workgroup
-  const double d = (double)s - mean;
-  const double ks = wave_sum(kept ? (double)s : 0.0), m2 = wave_sum(valid ? d * d : 0.0);
-  if (lane == 0) { s_d[0][wid] = ks; s_d[1][wid] = m2; }
-  __syncthreads();
-  if (wid == 0) {
+  // ---- statistics: Σ kept scores, Σ (s - mean)^2 and the kept-token counts, added per workgroup (the
+  // wave partials were complete at the look-back barrier)
+  if (wid == 1) {
     double x = s_d[0][lane & (kSW - 1)], y = s_d[1][lane & (kSW - 1)];
 #pragma unroll
     for (int o = kSW / 2; o > 0; o >>= 1) { x += __shfl_xor(x, o, kWave); y += __shfl_xor(y, o, kWave); }
@@ -988,19 +991,16 @@ __device__ __forceinline__ void k2_body(const FastArgs& g, uint32_t* hist_lds) {
     if (lane == 0) st_sc1(&g.L.head->part[blk], kTag | (uint64_t)c0 | ((uint64_t)c1 << 11) | ((uint64_t)c2 << 22));
   }
   K2_WG(2);
-  // ---- histogram bin + slot of the token
-  if (a.mode_select == 1) {  // wave-uniform: every lane takes part in the peer matching
-    const uint64_t entry = ((uint64_t)score_key(s) << 32) | (uint32_t)i;
-    const int b = l * kNBin + bin_of(s, bin_lo_of(g, l), bin_inv_of(g, l));
-    const uint32_t slot = hist_slot_of(hist_issue(&g.L.hist[b], (uint32_t)b, valid));
-    if (valid && slot < kCap) st_sc1(g.L.slots + (size_t)b * kCap + slot, entry);
-    if (g.hist_fb) {
-      const int b3 = 3 * kNBin + bin_of(s, g.bin_lo[3], g.bin_inv[3]);
-      const uint32_t slot3 = hist_slot_of(hist_issue(&g.L.hist[b3], (uint32_t)b3, valid));
-      if (valid && slot3 < kCap) st_sc1(g.L.slots + (size_t)b3 * kCap + slot3, entry);
-    }
+  // ---- histogram bin of the token: the (returning) atomics go out now, the workgroup partials below
+  // are reduced while they are in flight, and the slots are taken after
+  const bool hist = a.mode_select == 1;  // wave-uniform: every lane takes part in the peer matching
+  const int hb = l * kNBin + bin_of(s, bin_lo_of(g, l), bin_inv_of(g, l));
+  const int hb3 = 3 * kNBin + bin_of(s, g.bin_lo[3], g.bin_inv[3]);
+  HistTicket tk0{0u, 0, 0}, tk3{0u, 0, 0};
+  if (hist) {
+    tk0 = hist_issue(&g.L.hist[hb], (uint32_t)hb, valid);
+    if (g.hist_fb) tk3 = hist_issue(&g.L.hist[hb3], (uint32_t)hb3, valid);
   }
-  K2_WG(3);
   // ---- workgroup partials: score sum, score key range
   const double sw = wave_sum(valid ? (double)s : 0.0);
   uint32_t kmn = valid ? score_key(s) : 0xffffffffu, kmx = valid ? score_key(s) : 0u;
@@ -1026,6 +1026,16 @@ __device__ __forceinline__ void k2_body(const FastArgs& g, uint32_t* hist_lds) {
       st_sc1(&pp->ssum, ss);
       st_sc1(&pp->kmn, m0);
       st_sc1(&pp->kmx, m1);
+    }
+  }
+  K2_WG(3);
+  if (hist) {  // the slot of the token in its bin's list
+    const uint64_t entry = ((uint64_t)score_key(s) << 32) | (uint32_t)i;
+    const uint32_t slot = hist_slot_of(tk0);
+    if (valid && slot < kCap) st_sc1(g.L.slots + (size_t)hb * kCap + slot, entry);
+    if (g.hist_fb) {
+      const uint32_t slot3 = hist_slot_of(tk3);
+      if (valid && slot3 < kCap) st_sc1(g.L.slots + (size_t)hb3 * kCap + slot3, entry);
     }
   }
   K2_WG(4);
