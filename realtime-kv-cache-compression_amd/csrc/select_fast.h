@@ -44,7 +44,7 @@ __device__ unsigned long long g_k2_probe[16];   // the selecting workgroup's pha
 __device__ unsigned long long g_k2_clock[16];
 __device__ unsigned long long g_k2_wg[32][10];  // per workgroup phase timestamps
 __device__ int g_k2_rep;  // the probe's second pass over phase 2 (warm instruction cache) records at k + 8
-#define K2_PROBE(k) do { if (threadIdx.x == 0) { g_k2_probe[(k) + 8 * g_k2_rep] = __builtin_amdgcn_s_memrealtime(); g_k2_clock[(k) + 8 * g_k2_rep] = __builtin_amdgcn_s_memtime(); } } while (0)
+#define K2_PROBE(k) do { if (threadIdx.x == 0 && blockIdx.x == (unsigned)((g.f.S + kST - 1) / kST - 1)) { g_k2_probe[(k) + 8 * g_k2_rep] = __builtin_amdgcn_s_memrealtime(); g_k2_clock[(k) + 8 * g_k2_rep] = __builtin_amdgcn_s_memtime(); } } while (0)
 #define K2_WG(k) do { if (threadIdx.x == 0) g_k2_wg[blockIdx.x][k] = __builtin_amdgcn_s_memrealtime(); } while (0)
 __device__ int g_k2_twice;  // set by the probe: run phase 2 twice (the first pass cold)
 #else
@@ -480,7 +480,8 @@ __device__ __forceinline__ void rescan_thresholds(const FastArgs& g, uint32_t* h
 // selection words and the statistics.  s_selw receives the selection words (thread 0 writes them;
 // the caller's barrier publishes them to the workgroup).
 template <int TPT>
-__device__ __forceinline__ void select_thresholds(const FastArgs& g, uint32_t* hist_lds, uint64_t* s_selw) {
+__device__ __forceinline__ void select_thresholds(const FastArgs& g, uint32_t* hist_lds, uint64_t* s_selw,
+                                                  bool publish) {
   const FinalizeArgs& a = g.f;
   __shared__ uint32_t s_scan32[2][kSW];
   __shared__ uint32_t s_pick[kGrp][3];
@@ -533,7 +534,7 @@ __device__ __forceinline__ void select_thresholds(const FastArgs& g, uint32_t* h
       s_q[kGrp + 3] = (int)kf;
       md[3] = !fb ? M_NONE : (kf >= S ? M_ALL : M_PART);
       s_q[3] = md[3];
-      if (g.fused && !g.withhold) {  // the kept row count: quantization waves of rows beyond it end now
+      if (publish && g.fused && !g.withhold) {  // the kept row count: quantization waves of rows beyond it end now
         const int64_t nkept = fb ? (kf < S ? kf : S) : kept;
         st_sc1(&g.L.head->sel[6], kTag | ((uint64_t)nkept << 16) | ((uint64_t)(fb ? 1 : 0) << 8));
       }
@@ -672,23 +673,25 @@ __device__ __forceinline__ void select_thresholds(const FastArgs& g, uint32_t* h
   }
   K2_PROBE(3);
   if (t != 0) return;
-  // ---- the selection words first (the other workgroups wait on them), then the statistics
+  // ---- the selection words (this workgroup's phase 3 reads them from LDS; the publishing workgroup
+  // also stores them for the fused quantization waves and the probe), then the statistics
   const double ssum = s_ssum;
   const double mean = ssum / (double)S;
   const uint64_t mb = __builtin_bit_cast(uint64_t, mean);
   for (int q = 0; q < kGrp; ++q) {
     const uint64_t w = kTag | ((uint64_t)(fallback ? 1 : 0) << 50) | ((uint64_t)mode[q] << 48) |
                        ((uint64_t)(cut[q] & 0xffff) << 32) | thr[q];
-    if (!g.withhold) st_sc1(&g.L.head->sel[q], w);
+    if (publish && !g.withhold) st_sc1(&g.L.head->sel[q], w);
     s_selw[q] = w;
   }
   const uint64_t m_lo = kTag | (mb & 0xffffffffu), m_hi = kTag | (mb >> 32);
+  s_selw[4] = m_lo;
+  s_selw[5] = m_hi;
+  if (!publish) return;
   if (!g.withhold) {
     st_sc1(&g.L.head->sel[4], m_lo);
     st_sc1(&g.L.head->sel[5], m_hi);
   }
-  s_selw[4] = m_lo;
-  s_selw[5] = m_hi;
   // statistics known here; phase 3 adds the kept-token sums (stats zeroed before the launch)
   const int64_t ccount[3] = {s_cc[0], s_cc[1], s_cc[2]};
   const int64_t quota[3] = {s_quota[0], s_quota[1], s_quota[2]};
@@ -1042,24 +1045,22 @@ __device__ __forceinline__ void k2_body(const FastArgs& g, uint32_t* hist_lds) {
   // ---- this workgroup's slot entries, partials, scores and classes are complete
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  if (t == 0) st_sc1(&g.L.head->ready[blk], kTag);
-  // ---- phase 2 in workgroup G−1; the others wait for the selection words
-  if (blk == G - 1) {
+  // (RTKV_TEST_WITHHOLD_SELECTION: the last workgroup never reports ready, so every workgroup's phase-2
+  // wait runs into its poll bound)
+  if (t == 0 && !(g.withhold && blk == G - 1)) st_sc1(&g.L.head->ready[blk], kTag);
+  // ---- phase 2 in EVERY workgroup (the same inputs, the same deterministic result): no selection hand-off
+  // between workgroups; workgroup G−1 publishes the statistics and the early host mirror
 #ifdef RTKV_SELECT_PROBE
-    if (g_k2_twice) {
-      if (t == 0) g_k2_rep = 1;
-      __syncthreads();
-      select_thresholds<TPT>(g, hist_lds, s_selw);
-      __syncthreads();
-      if (t == 0) g_k2_rep = 0;
-      __syncthreads();
-    }
-#endif
-    select_thresholds<TPT>(g, hist_lds, s_selw);
-  } else if (wid == 0) {
-    const uint64_t w = poll_tagged(g.L.head->sel, 1, 6, g.spin_limit, a.stats);
-    if (lane < 6) s_selw[lane] = w;
+  if (g_k2_twice && blk == G - 1) {
+    if (t == 0) g_k2_rep = 1;
+    __syncthreads();
+    select_thresholds<TPT>(g, hist_lds, s_selw, false);
+    __syncthreads();
+    if (t == 0) g_k2_rep = 0;
+    __syncthreads();
   }
+#endif
+  select_thresholds<TPT>(g, hist_lds, s_selw, blk == G - 1);
   __syncthreads();
   K2_WG(5);
   compact_phase(g, s, l, i, valid, s_selw);
