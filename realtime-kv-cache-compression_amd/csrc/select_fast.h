@@ -17,25 +17,27 @@
 //           works: the histogram only has to tell which bin holds each class's threshold), and every
 //           token's (key, index) appended to a 64-entry slot list of its bin (slot = the histogram
 //           atomic's return value, one atomic per bin and wave).
-// 2 select  Workgroup G−1 (dispatched last): once every workgroup's counts are published, the quotas
-//           n_g from the class counts (the greedy in closed form), per partially kept class the bin
-//           where the count from the top reaches n_g, and the exact threshold from that bin's slot
-//           list (≤ 64 entries, one wave): key T and the number of tokens at T to take in index
-//           order.  A bin with more than 64 tokens (heavy ties) takes the exact rescan path: all S
-//           keys in registers, ≤ 3 LDS-histogram rounds.
-// 3 compact Every workgroup, its token still in registers: keep decisions from (mode, T, ties) per
-//           group; per-workgroup aggregates (surely kept tokens per class, ties per group); each
-//           workgroup sums its predecessors' aggregates (decoupled look-back: every aggregate is
-//           published before any is awaited, and all G <= 32 workgroups are resident at once), then
-//           ranks its tokens with block scans: mask, kept_index, row_label, row_offset; its
-//           kept-token statistics are added atomically.
+// 2 select  EVERY workgroup (the same inputs, the same deterministic result, so no selection word
+//           travels between workgroups; workgroup G−1 publishes the statistics and the early host
+//           mirror): once every workgroup's counts and ready words are published, the quotas n_g from
+//           the class counts (the greedy in closed form), per partially kept class the bin where the
+//           count from the top reaches n_g (one packed scan for all classes), and the exact threshold
+//           from that bin's slot list (≤ 64 entries, one wave): key T and the tie CUTOFF, the index of
+//           the n_g-th token in (key desc, index asc) order.  A bin with more than 64 tokens (heavy
+//           ties) takes the exact rescan path: all S keys in registers, ≤ 3 LDS-histogram rounds, the
+//           cutoff from a block scan of per-thread tie counts.
+// 3 compact Every workgroup, its token still in registers: keep decisions, all local (mode, T, cutoff
+//           per group); per-class ranks by wave ballots; the workgroup's kept counts per class
+//           published, its predecessors' summed (decoupled look-back: every count is published before
+//           any is awaited, and all G <= 32 workgroups are resident at once); mask, kept_index,
+//           row_label, row_offset; its kept-token statistics are added atomically.
 //
 // Hand-offs between workgroups are TAGGED 8-byte words (bit 63 set on a zeroed word: the region is
 // cleared before every launch), written with sc1 stores and polled with sc1 loads, so a consumer sees
 // data and flag in one round trip and producers need no drain between them (MI355X_MICROARCH.md
 // hand-off rows: each separate flag or drain costs a memory round trip, ≈1–2 µs).  The one drain
 // left is phase 1's: a workgroup's slot-list entries and score sums are complete (s_waitcnt
-// vmcnt(0)) before its tagged counts word, which is what the selecting workgroup polls.
+// vmcnt(0)) before its tagged ready word, which every workgroup's phase 2 polls.
 #pragma once
 #include "common.h"
 
