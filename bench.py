@@ -9,11 +9,17 @@ importance → quantization → selective propagation) through the C ABI's fused
 (rtkv_compress_layer: 3 kernels per layer, no host sync inside the step).  Inputs are synthetic
 (seeded, resident in HBM before timing).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config cfg3|cfg4|cfg5]
 
-N > 1 (launched by torch.distributed.run): sequence-chunk sharding with weak scaling (every rank
-owns S tokens of an N·S-token prefill; RCCL all-gather of per-token attention mass, global
-selection on every rank, local quantization, RCCL all-gather of the packed KV).
+Workloads (BASELINE.json configs): cfg3 (Llama-2-7B, 32 layers, S = 16384; the N = 1 default and
+the headline), cfg4 (Llama-2-7B, S = 65536 in total; the N > 1 default) and cfg5 (Llama-2-13B,
+40 layers, 40 heads, S = 32768 in total).  N > 1: sequence-chunk sharding of the SAME S_total
+(strong scaling: rank j owns tokens [j·S_total/N, (j+1)·S_total/N); RCCL all-gather of the
+per-token attention mass, global selection on every rank, local quantization, grouped RCCL
+send/recv of the packed KV).  ``python bench.py --gpus N`` without WORLD_SIZE in the environment
+starts ``python -m torch.distributed.run --nproc-per-node N ... bench.py ...`` as a child process
+before anything touches a GPU, waits for it and exits with its code; it fails at once when fewer
+than N GPUs are visible.  ``--launch-dry-run`` prints that command line and exits.
 
 Rank 0 prints ONE JSON line.  ``value`` = algorithmic bytes of the whole job ÷ wall time (GB/s);
 ``ttft_ms`` = the step's wall time with every layer strictly after the previous one (the reference
@@ -37,6 +43,8 @@ from __future__ import annotations
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -47,16 +55,67 @@ sys.path.insert(0, os.path.join(REPO, "realtime-kv-cache-compression_amd"))
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
 
+# BASELINE.json configs 3-5 (SURVEY §8 shorthand): KV shapes of the named models, S_total = tokens of the
+# whole prefill (split over the ranks at N > 1)
+CONFIGS = {
+    "cfg3": dict(model="Llama-2-7B", layers=32, heads=32, head_dim=128, seq_total=16384),
+    "cfg4": dict(model="Llama-2-7B", layers=32, heads=32, head_dim=128, seq_total=65536),
+    "cfg5": dict(model="Llama-2-13B", layers=40, heads=40, head_dim=128, seq_total=32768),
+}
+
+
+def resolve_config(args, world: int):
+    """Fill --layers/--heads/--head-dim/--seq from --config (default: cfg3 at N = 1, cfg4 at N > 1)."""
+    if args.config is None:
+        args.config = "cfg3" if world == 1 else "cfg4"
+    c = CONFIGS[args.config]
+    args.model = c["model"]
+    for k in ("layers", "heads", "head_dim"):
+        if getattr(args, k) is None:
+            setattr(args, k, c[k])
+    if args.seq is None:
+        if c["seq_total"] % world:
+            raise SystemExit(f"bench.py: {args.config}'s S = {c['seq_total']} does not split over {world} ranks")
+        args.seq = c["seq_total"] // world
+    return args
+
+
+def launch(args) -> int:
+    """--gpus N > 1 without a torch.distributed environment: run this script under
+    torch.distributed.run as a CHILD process (nothing here touches a GPU: device_count() does not
+    initialise HIP), relay its exit code.  Fails fast when fewer than N GPUs are visible."""
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    rest = [a for a in sys.argv[1:] if a != "--launch-dry-run"]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + rest
+    visible = torch.cuda.device_count()
+    if args.launch_dry_run:
+        print(json.dumps({"launch": cmd, "visible_gpus": visible}), flush=True)
+        return 0
+    if visible < args.gpus:
+        print(f"bench.py: --gpus {args.gpus} needs {args.gpus} visible GPUs, this process sees {visible}; "
+              f"not running (a smaller run would be mislabelled)", file=sys.stderr, flush=True)
+        return 2
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # the box's drivers support dmabuf IPC only
+    return subprocess.run(cmd, env=env).returncode
+
 
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--layers", type=int, default=32)
-    ap.add_argument("--seq", type=int, default=16384, help="tokens per rank")
-    ap.add_argument("--heads", type=int, default=32)
-    ap.add_argument("--head-dim", type=int, default=128)
+    ap.add_argument("--config", default=None, choices=sorted(CONFIGS),
+                    help="BASELINE workload: cfg3 (default at N = 1), cfg4 (default at N > 1) or cfg5")
+    ap.add_argument("--layers", type=int, default=None, help="override the config's layer count")
+    ap.add_argument("--seq", type=int, default=None, help="override: tokens per rank (default S_total / N)")
+    ap.add_argument("--heads", type=int, default=None)
+    ap.add_argument("--head-dim", type=int, default=None)
+    ap.add_argument("--launch-dry-run", action="store_true",
+                    help="--gpus N > 1 without WORLD_SIZE: print the torch.distributed.run command line and exit")
     ap.add_argument("--dtype", default="float32", choices=["float16", "bfloat16", "float32"],
                     help="K/V/attention dtype (default: the reference model's fp32)")
     ap.add_argument("--no-packed", action="store_true", help="skip the packed-code output")
@@ -86,9 +145,12 @@ def parse():
                          "(Q + prompt keys + row LSE, K1' on MFMA)")
     ap.add_argument("--sharded", action="store_true",
                     help="use the sequence-sharded driver even at world size 1 (plumbing check)")
-    ap.add_argument("--collectives", default="torch", choices=["torch", "rtkv"],
+    ap.add_argument("--collectives", default="torch", choices=["torch", "rtkv", "host"],
                     help="sharded driver: torch.distributed, or the C ABI's RCCL communicators "
                          "(rtkv_allgather_rows / rtkv_allgather_packed)")
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                    help="N > 1: nccl (RCCL over xGMI, one GPU per rank) or gloo (rehearsal of the multi-rank "
+                         "control flow with every collective staged through host memory; ranks may share a GPU)")
     ap.add_argument("--no-overlap", action="store_true",
                     help="sharded driver: exchange every layer's packed KV after the last layer instead of "
                          "overlapping each layer's exchange with the following layers")
@@ -356,9 +418,10 @@ def drop_in_leg(args, job, steps, warmup):
 
 
 class ShardedJob:
-    """Sequence-sharded prefill (weak scaling): this rank owns tokens [rank*S, (rank+1)*S) of an
-    N*S-token prefill.  One step = every layer's shard stages (K1 on own rows, RCCL all-gather of A,
-    global selection, K4 on own kept rows) + the end-of-prefill exchange of the packed KV."""
+    """Sequence-sharded prefill: this rank owns tokens [rank*S, (rank+1)*S) of the config's
+    S_total = N*S-token prefill (S = S_total / N: strong scaling over a fixed BASELINE workload).
+    One step = every layer's shard stages (K1 on own rows, RCCL all-gather of A, global selection,
+    K4 on own kept rows) + the exchange of the packed KV (overlapped with later layers by default)."""
 
     def __init__(self, args, device, rank, world):
         import rtkv
@@ -409,6 +472,49 @@ class ShardedJob:
             k4.append(kv_read + deq + packed + Sp * (4 + 8 + 1))
             tot.append(w_read + kv_read + deq + packed + meta)
         return tot, k4
+
+    def split_times(self, barrier, reps=3):
+        """This rank's milliseconds per step of the step's parts, each timed alone after the timed loop
+        (end-of-prefill exchange mode, so the parts do not overlap): ``compute_ms`` = every layer's
+        stages (K1, the all-gathers of A, the replicated selection, K4) with no packed KV moved;
+        ``exchange_ms`` = the grouped send/recv of every layer's packed KV (after a barrier, so a
+        slower peer's compute is not counted); ``allgather_A_ms`` = the layers' all-gathers of A alone
+        (part of compute_ms)."""
+        comp = self.comp
+        overlap = comp.overlap
+        comp.overlap = False
+        try:
+            def enqueue_all():
+                for l in range(self.args.layers):
+                    K, V, W = self.inputs[l]
+                    comp.enqueue_layer(K, V, W, l, params=self.params[l])
+            barrier()
+            t0 = time.perf_counter()
+            for _ in range(reps):
+                enqueue_all()
+                comp.exchange(transfer=False)
+            torch.cuda.synchronize(self.device)
+            compute = (time.perf_counter() - t0) / reps
+            ex = 0.0
+            for _ in range(reps):
+                enqueue_all()
+                torch.cuda.synchronize(self.device)
+                barrier()
+                t0 = time.perf_counter()
+                self.last = comp.exchange()
+                torch.cuda.synchronize(self.device)
+                ex += time.perf_counter() - t0
+            barrier()
+            t0 = time.perf_counter()
+            for _ in range(reps):
+                for _l in range(self.args.layers):
+                    comp.gather_A(1, self.S)
+            torch.cuda.synchronize(self.device)
+            ag = (time.perf_counter() - t0) / reps
+        finally:
+            comp.overlap = overlap
+        return {"compute_ms": round(compute * 1e3, 4), "exchange_ms": round(ex / reps * 1e3, 4),
+                "allgather_A_ms": round(ag * 1e3, 4)}
 
     def exchanged_bytes(self):
         """Bytes of packed KV (codes + scale/zero-point) this rank received in the exchange."""
@@ -532,11 +638,20 @@ def kernel_us(job, kus):
 
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch(args))  # before any GPU call
+    if args.launch_dry_run:
+        raise SystemExit("--launch-dry-run: only with --gpus N > 1 outside torch.distributed.run")
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if args.gpus != world and world > 1:
-        print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
+    if args.gpus != world:
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE {world}: refusing a mislabelled run", file=sys.stderr)
+        sys.exit(2)
+    resolve_config(args, world)
+    if args.dist_backend == "gloo":  # rehearsal: ranks may share the visible GPUs
+        local = local % max(1, torch.cuda.device_count())
+        args.collectives = "host"
     torch.cuda.set_device(local)
     device = torch.device("cuda", local)
     sharded = world > 1 or args.sharded
@@ -545,11 +660,16 @@ def main():
         if not dist.is_initialized():
             os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
             os.environ.setdefault("MASTER_PORT", "29531")
-            dist.init_process_group("nccl", device_id=device, rank=rank, world_size=world)
+            if args.dist_backend == "gloo":
+                dist.init_process_group("gloo", rank=rank, world_size=world)
+            else:
+                dist.init_process_group("nccl", device_id=device, rank=rank, world_size=world)
+        world = dist.get_world_size()
         job = ShardedJob(args, device, rank, world)
     else:
         dist = None
-        job = Job(args, device, rank, world)
+        # long sequences: 8 distinct layer inputs cycled over the layers (bounded HBM and setup time)
+        job = Job(args, device, rank, world, slots=8 if args.seq > 16384 else None)
         job.set_streams(max(1, args.streams))
 
     def barrier():
@@ -569,22 +689,32 @@ def main():
     barrier()
     elapsed = time.perf_counter() - t0
     if dist is not None:
-        t = torch.tensor([elapsed], device=device, dtype=torch.float64)
+        t = torch.tensor([elapsed], dtype=torch.float64, device=device if args.dist_backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     ms_per_step = elapsed / args.steps * 1e3
 
     kus = None
+    split = None
     if sharded:
         for _ in range(2):
             job.step()
         torch.cuda.synchronize(device)
+        split = job.split_times(barrier)  # per-rank compute / all-gather / exchange, outside the timed loop
     else:
         kus = job.kernel_times()  # per-kernel timing (HIP events on the launch stream), outside the timed loop
     tot_bytes, k4_bytes = job.layer_bytes()
     step_bytes = sum(tot_bytes)  # whole-job algorithmic bytes (the sharded job counts all N*S tokens)
     value = step_bytes / (ms_per_step / 1e3) / 1e9
 
+    ranks = None
+    if sharded:
+        props = torch.cuda.get_device_properties(device)
+        me = dict(rank=rank, local_rank=local, device=torch.cuda.current_device(),
+                  pci_bus_id=getattr(props, "pci_bus_id", None), received_bytes_per_step=job.exchanged_bytes(),
+                  **split)
+        ranks = [None] * world
+        dist.all_gather_object(ranks, me)
     if rank == 0:
         outs = "+".join(x for x, on in (("dequant", not args.no_dequant), ("packed", not args.no_packed)) if on)
         line = {
@@ -597,18 +727,23 @@ def main():
             "ms_per_step": round(ms_per_step, 4),
             "ttft_ms": round(ms_per_step, 4),
             "higher_is_better": True,
-            "scaling": "weak",
+            # N > 1 splits the config's S_total over the ranks: total work fixed as N grows
+            "scaling": "strong" if world > 1 else "weak",
             "vs_baseline": None,
             "dtype": {"float16": "f16", "bfloat16": "bf16", "float32": "f32"}[args.dtype],
             "data": "synthetic (seeded torch RNG; K,V ~ N(0,1), W = causal u^4-softmax-like prompt slice)",
-            "config": {"workload": f"Llama-2-7B prefill KV compression{' (fused Q/LSE importance)' if args.importance == 'qk' else ''}, {args.layers} layers, "
+            "config": {"workload": f"{args.config}: {args.model} prefill KV compression"
+                                   f"{' (fused Q/LSE importance)' if args.importance == 'qk' else ''}, {args.layers} layers, "
                                    f"S={job.S * world} ({job.S}/rank), {args.heads}x{args.head_dim}, {args.dtype}, "
-                                   f"P={job.P}, bits 8/4/2, ratios .8/.6/.4, {outs} outputs",
-                       "model": "Llama-2-7B (KV shapes only)", "global_batch": 1, "seq_len": job.S * world,
+                                   f"P={job.P}, bits 8/4/2, ratios .8/.6/.4, {outs} outputs"
+                                   + (f", {job.slots} distinct layer inputs cycled" if getattr(job, "slots", args.layers) < args.layers else ""),
+                       "model": f"{args.model} (KV shapes only)", "global_batch": 1, "seq_len": job.S * world,
                        "parallelism": f"sequence-shard x{world}" if world > 1 else "single GPU",
                        "layer_streams": 1 if sharded else max(1, args.streams)},
         }
         if sharded:
+            line["world_size"] = world
+            line["ranks"] = ranks
             line["exchange"] = {"received_bytes_per_rank_per_step": job.exchanged_bytes(),
                                 "kind": ("grouped RCCL send/recv per layer of packed K/V codes + scale/zp (exact byte "
                                          "ranges, all peers at once), " +

@@ -268,28 +268,31 @@ class ShardedPrefillCompressor:
                             torch.empty(B, S_total, dtype=torch.float32, device=self.device))
         return self._A[key]
 
+    def gather_A(self, B: int, S_local: int) -> torch.Tensor:
+        """Step 2: the all-gather of every rank's A [B, S_local] into token order [B, S_total]."""
+        S_total = S_local * self.world
+        A_local, A_parts, A = self._A_buffers(B, S_local)
+        if self.comm is not None:
+            self.comm.allgather_rows(A_local, A)  # straight into token order, any B
+            return A
+        if self._host:
+            parts = torch.empty(A_parts.numel(), dtype=A_parts.dtype)
+            dist.all_gather_into_tensor(parts, A_local.reshape(-1).cpu(), group=self.group)
+            A_parts.view(-1).copy_(parts)
+        else:
+            dist.all_gather_into_tensor(A_parts.view(-1), A_local.view(-1), group=self.group)
+        if B == 1:
+            return A_parts.view(1, S_total)  # rank-major = token order
+        A.copy_(A_parts.permute(1, 0, 2).reshape(B, S_total))
+        return A
+
     def _select_and_quantize(self, K, V, layout: str, layer_idx: int, p, bufs: ShardBuffers, a_dtype: int):
         """Steps 2-5 of a layer once this rank's A is computed: all-gather, global selection, bounds,
         local quantization, and the (overlapped) exchange bookkeeping."""
         B, S_local = bufs.B, bufs.S_local
         S_total = S_local * self.world
         row0 = self.rank * S_local
-        A_local, A_parts, A = self._A_buffers(B, S_local)
-        if self.comm is not None:
-            self.comm.allgather_rows(A_local, A)  # straight into token order, any B
-            A_glob = A
-        else:
-            if self._host:
-                parts = torch.empty(A_parts.numel(), dtype=A_parts.dtype)
-                dist.all_gather_into_tensor(parts, A_local.reshape(-1).cpu(), group=self.group)
-                A_parts.view(-1).copy_(parts)
-            else:
-                dist.all_gather_into_tensor(A_parts.view(-1), A_local.view(-1), group=self.group)
-            if B == 1:
-                A_glob = A_parts.view(1, S_total)  # rank-major = token order
-            else:
-                A.copy_(A_parts.permute(1, 0, 2).reshape(B, S_total))
-                A_glob = A
+        A_glob = self.gather_A(B, S_local)
         self.stages.finalize(A_glob, a_dtype, p, bufs)
         self.stages.ranges(bufs, self.world)
         self.stages.quantize(K, V, layout, row0, self.rank, self.world, p, bufs)
@@ -374,10 +377,14 @@ class ShardedPrefillCompressor:
         self.xcomm.allgather_packed(sl.ranges.reshape(-1).contiguous(), sl.bufs.B, sl.bufs.S_total, out,
                                     stream=xs.cuda_stream)
 
-    def exchange(self) -> List[ShardLayer]:
+    def exchange(self, transfer: bool = True) -> List[ShardLayer]:
         """Finish the exchange of every layer enqueued so far and return their host views.  Overlapped
         mode: issue the layers still queued, wait for everything in flight.  Otherwise: one host read
-        of every pending layer's rank bounds, then one grouped P2P launch per layer, waited once."""
+        of every pending layer's rank bounds, then one grouped P2P launch per layer, waited once.
+        ``transfer=False`` (end-of-prefill mode only) returns the host views without moving the packed
+        KV: each rank then holds its own byte ranges only (bench.py times the compute this way)."""
+        if not transfer and self.overlap:
+            raise ValueError("exchange(transfer=False) needs overlap=False (an overlapped exchange is in flight)")
         if self.overlap:
             self._issue(keep=0)
             for w in self._works:
@@ -392,7 +399,7 @@ class ShardedPrefillCompressor:
             return []
         host = torch.stack([self._bufs[l].ranges for l in layers]).cpu()  # the single sync
         out = [ShardLayer(l, self._bufs[l], host[k]) for k, l in enumerate(layers)]
-        if self.world == 1 or not self.emit_packed:
+        if self.world == 1 or not self.emit_packed or not transfer:
             return out
         if self.xcomm is not None:
             for sl in out:

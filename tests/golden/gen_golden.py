@@ -288,6 +288,12 @@ LAYER_CASES = [
     ("cfg5_13b_s32768_l20", COVERAGE, 40, 20, 1, 40, 40, 128, 32768, "float32"),
     ("cfg3_l0", COVERAGE, 32, 0, 1, 32, 32, 128, 16384, "float32"),
     ("cfg3_l25", PUBLISHED, 32, 25, 1, 32, 32, 128, 16384, "float32"),
+    # round 4: BASELINE cfg4's whole sequence (Llama-2-7B, S = 65536: the single-GPU pipeline selection
+    # and the 8-way shard union are compared with these), early (.8) and late (.4) ratio groups
+    ("cfg4_s65536_l0", COVERAGE, 32, 0, 1, 32, 32, 128, 65536, "float32"),
+    ("cfg4_s65536_l31", COVERAGE, 32, 31, 1, 32, 32, 128, 65536, "float32"),
+    ("cfg4_s65536_l0", PUBLISHED, 32, 0, 1, 32, 32, 128, 65536, "float16"),
+    ("cfg4_s65536_l31", PUBLISHED, 32, 31, 1, 32, 32, 128, 65536, "float16"),
 ]
 
 

@@ -290,3 +290,84 @@ def test_shards_union_equals_single_gpu_at_config_size(name, dtype, S_total, wor
     assert torch.equal(pk[:tot], ref.packed_k[:tot])
     assert torch.equal(pv[:tot], ref.packed_v[:tot])
     assert torch.equal(sz[:, :n], ref.scale_zp[:, :n])
+
+
+def _golden_cases(prefix):
+    from conftest import load_manifest
+    return [c for c in load_manifest()["cases"] if c["name"].startswith(prefix)]
+
+
+@pytest.mark.parametrize("case", _golden_cases("layer_cfg4_s65536"), ids=lambda c: c["name"])
+def test_shards_union_matches_reference_golden_cfg4(case):
+    """BASELINE configs[3] against the REFERENCE itself: the inputs of a reference-generated layer at
+    S = 65536 (tests/golden/gen_golden.py runs RealTimePrefillCompressor.compress_layer_kv_cache on
+    them) split over 8 simulated ranks.  Every rank's replicated scores / classes / mask equal the
+    reference's, the ranks' local dequantized rows concatenated in rank order are the reference's
+    K'/V' (sha256), and the assembled packed codes decode to the same bytes."""
+    import rtkv
+    from conftest import assert_matches, load_case
+    from rtkv import _lib as L
+    from rtkv.sharded import HipShardStages, ShardBuffers
+    s = case["spec"]
+    arrays = load_case(case)
+    world, S_total, F, dt = 8, s["S"], s["Hkv"] * s["D"], s["dtype"]
+    K, V = synth.kv(s["seed"], 1, S_total, F, dt)
+    W = synth.attention_slice(s["seed"], 1, s["H"], S_total, s["P"], dt)
+    Kd, Vd, Wd = _dev(K, dt), _dev(V, dt), _dev(W, dt)
+    del K, V, W
+    td = Kd.dtype
+    pr = s["params"]
+    cfg = rtkv.CompressionConfig(alpha=pr["alpha"], beta=pr["beta"], gamma=pr["gamma"], theta_h=pr["theta_h"],
+                                 theta_m=pr["theta_m"], num_hidden_layers=s["L"], low_precision_bits=s["bits"][0],
+                                 medium_precision_bits=s["bits"][1], high_precision_bits=s["bits"][2])
+    assert cfg.layer_weights[s["layer"]] == s["layer_weight"]
+    params = rtkv.params_from_config(cfg, s["layer"], s["P"], s["ratio"], L.EMIT_DEQUANT | L.EMIT_PACKED)
+    bits = tuple(s["bits"])
+    S_local = S_total // world
+    stages = HipShardStages("cuda")
+    A = torch.empty(1, S_total, dtype=torch.float32, device="cuda")
+    for j in range(world):
+        sl = slice(j * S_local, (j + 1) * S_local)
+        stages.aggregate(Wd[:, :, sl].contiguous(), s["P"], j * S_local, S_total, A[:, sl])
+    n = case["scalars"]["max_selected"]
+    k_all = torch.empty(1, n, F, dtype=td, device="cuda")
+    v_all = torch.empty(1, n, F, dtype=td, device="cuda")
+    bufs = ShardBuffers(1, S_local, world, F, td, "cuda", bits)  # one rank's buffers, reused rank after rank
+    pk = pv = sz = None
+    for j in range(world):
+        stages.finalize(A, L.TORCH_DTYPE_CODE[td], params, bufs)
+        stages.ranges(bufs, world)
+        sl = slice(j * S_local, (j + 1) * S_local)
+        stages.quantize(Kd[:, sl].contiguous(), Vd[:, sl].contiguous(), "bsf", j * S_local, j, world, params, bufs)
+        torch.cuda.synchronize()
+        gb = bufs.g
+        rg = bufs.ranges.cpu()
+        assert int(rg[0, -1, 0]) == n
+        if j == 0:  # the replicated global selection, against the reference
+            assert_matches(case, "scores", gb.scores.cpu().numpy(), arrays)
+            assert_matches(case, "labels", gb.labels.cpu().numpy(), arrays)
+            assert_matches(case, "mask", gb.mask.cpu().numpy(), arrays)
+            tot = int(rg[0, -1, 1])
+            pk = torch.zeros(tot + 256, dtype=torch.uint8, device="cuda")  # decoders may read a line past the end
+            pv = torch.zeros_like(pk)
+            sz = torch.zeros(1, n, 4, dtype=torch.float32, device="cuda")
+            kept_index, row_offset = gb.kept_index[:, :n].clone(), gb.row_offset[:, :n].clone()
+            labels = gb.labels.clone()
+        r0, r1 = int(rg[0, j, 0]), int(rg[0, j + 1, 0])
+        b0, b1 = int(rg[0, j, 1]), int(rg[0, j + 1, 1])
+        k_all[:, r0:r1] = bufs.k_local[:, : r1 - r0]
+        v_all[:, r0:r1] = bufs.v_local[:, : r1 - r0]
+        pk[b0:b1] = gb.packed_k[b0:b1]
+        pv[b0:b1] = gb.packed_v[b0:b1]
+        sz[:, r0:r1] = gb.scale_zp[:, r0:r1]
+
+    def storage(t):
+        t = t.cpu()
+        return t.numpy() if t.dtype == torch.float32 else t.view(torch.int16).numpy().view(np.uint16)
+    assert_matches(case, "k_out", storage(k_all), arrays)
+    assert_matches(case, "v_out", storage(v_all), arrays)
+    dk, dv = rtkv.unpack_layer(dict(codes_k=pk, codes_v=pv, row_offset=row_offset, scale_zp=sz, kept_index=kept_index,
+                                    labels=labels, rows=[n], bits=bits, dtype=td, feature_dim=F))
+    iv = torch.int32 if td == torch.float32 else torch.int16
+    assert torch.equal(dk.view(iv), k_all.view(iv))
+    assert torch.equal(dv.view(iv), v_all.view(iv))
