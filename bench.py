@@ -121,9 +121,9 @@ def parse():
     ap.add_argument("--no-packed", action="store_true", help="skip the packed-code output")
     ap.add_argument("--no-dequant", action="store_true", help="skip the dequantized K'/V' output (packed only)")
     ap.add_argument("--legs", default="f16,packed_only,drop_in,s4096,cfg2_s4096_quant,s65536,independent_layers,"
-                                      "prefill_7b",
+                                      "prefill_7b,prefill_7b_f32",
                     help="extra single-GPU legs after the main line: comma list of f16, packed_only, drop_in, "
-                         "s4096, cfg2_s4096_quant, s65536, independent_layers, prefill_7b (or 'none')")
+                         "s4096, cfg2_s4096_quant, s65536, independent_layers, prefill_7b, prefill_7b_f32 (or 'none')")
     ap.add_argument("--prefill-dtype", default="float16", choices=["float16", "bfloat16", "float32"],
                     help="dtype of the prefill_7b leg's random-init model")
     ap.add_argument("--prefill-modes", default="none,fused,eager",
@@ -136,9 +136,6 @@ def parse():
     ap.add_argument("--cpu-baseline-seconds", type=float, default=12.0,
                     help="CPU work budget of the oracle sample (layers are added until it is spent; 0 = skip)")
     ap.add_argument("--cpu-baseline-layers", type=int, default=32, help="at most this many layers in the sample")
-    ap.add_argument("--fused-quant", action="store_true",
-                    help="run the selection and the quantization as ONE launch (RTKV_FUSED_QUANT, csrc/fused.h) "
-                         "instead of two")
     ap.add_argument("--quiet", action="store_true")
     ap.add_argument("--importance", default="w", choices=["w", "qk"],
                     help="w: the reference's attention-weights input (prompt slice); qk: fused mode "
@@ -219,12 +216,7 @@ class Job:
         if not (self.emit_packed or self.emit_dequant):
             raise SystemExit("--no-packed and --no-dequant together leave nothing to compute")
         flags = (L.EMIT_DEQUANT if self.emit_dequant else 0) | (L.EMIT_PACKED if self.emit_packed else 0) | \
-            (L.NO_SELECTION if quant_only else 0) | (L.FUSED_QUANT if args.fused_quant else 0)
-        # with --fused-quant, rtkv_compress_layer runs K2 + K4 as one launch for one batch row of <= 32768 tokens
-        # with 4096-element rows (5120 in fp16/bf16): the K2 event interval is then empty and the fused kernel
-        # is the K4 interval
-        self.fused = (args.fused_quant and self.S <= 32768 and
-                      (self.F == 4096 or (self.F == 5120 and self.dtype != torch.float32)))
+            (L.NO_SELECTION if quant_only else 0)
         prop = rtkv.SelectiveTokenPropagator(self.cfg)
         gen = torch.Generator(device=device)
         gen.manual_seed(1234 + 7919 * rank)
@@ -598,24 +590,22 @@ def roofline_objects(args, job, kus, k4_bytes):
         traffic = round(sum(v["hbm_bytes"] for v in pmc.values()))
     path = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_source": src,
-            "scope": "path: every kernel of a layer (K1 + fused K2/K4, or K1 + K2 + K4), HIP events on the launch stream",
+            "scope": "path: every kernel of a layer (K1 + K2 + K4), HIP events on the launch stream",
             "algorithmic_bytes_per_launch": R,
             "algorithmic_bytes_def": "R = 2*S*H*D*e + H*S*P*e (every K/V element once + W prompt columns; "
                                      "SURVEY §8d, the north star's HBM-read roofline)",
             "avg_launch_us": round(layer_us, 2)}
-    fused = getattr(job, "fused", False)
-    k4_us = kus[1] + kus[2] if fused else kus[2]
+    k4_us = kus[2]
     k4_alg = sum(k4_bytes) / len(k4_bytes)
     k4_ach = k4_alg / (k4_us / 1e6) / 1e9
     k4_traffic = None
-    name = "fused_kernel" if fused else "quant_rows_kernel"
+    name = "quant_rows_kernel"
     if pmc:
         k4_traffic = next((round(v["hbm_bytes"]) for k, v in pmc.items() if name in k), None)
     k4 = {"bound": "hbm", "achieved": round(k4_ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
           "frac": round(k4_ach / HBM_PEAK_GBS, 4), "traffic": k4_traffic, "traffic_source": src,
           "algorithmic_bytes_per_launch": round(k4_alg),
-          "kernel": ("fused_kernel (K2 selection + K4 quantize/pack/compact in one launch)" if fused else
-                     "quant_rows_kernel (K4)") + ", K4's read + write bytes",
+          "kernel": "quant_rows_kernel (K4), K4's read + write bytes",
           "avg_launch_us": round(k4_us, 2)}
     return path, k4
 
@@ -631,8 +621,6 @@ def leg_summary(args, job, ms, kus):
 
 
 def kernel_us(job, kus):
-    if getattr(job, "fused", False):
-        return {"K1_aggregation": round(kus[0], 2), "K24_fused_select_quant": round(kus[1] + kus[2], 2)}
     return {"K1_aggregation": round(kus[0], 2), "K2_select": round(kus[1], 2), "K4_quant_pack": round(kus[2], 2)}
 
 
@@ -803,6 +791,13 @@ def main():
                     from prefill_model import prefill_leg
                     legs["prefill_7b"] = prefill_leg(device, S=job.S, dtype=getattr(torch, args.prefill_dtype),
                                                      modes=tuple(args.prefill_modes.split(",")))
+                elif name == "prefill_7b_f32":
+                    # the same at the reference model's own precision (modified_llama.py:368 builds the model
+                    # with default fp32 parameters): fp32 states, fp32 LSE / K1' on the f32 MFMA
+                    sys.path.insert(0, os.path.join(REPO, "tools"))
+                    from prefill_model import prefill_leg
+                    legs["prefill_7b_f32"] = prefill_leg(device, S=job.S, dtype=torch.float32,
+                                                         modes=tuple(args.prefill_modes.split(",")))
                 elif name == "drop_in":
                     legs["drop_in"] = drop_in_leg(args, job, args.leg_steps, 2)
                     legs["drop_in"]["raw_driver_ms_per_layer"] = round(ms_per_step / args.layers, 4)

@@ -56,7 +56,10 @@ enum rtkv_error_flag {
    * (a workgroup that never became resident, or a withheld hand-off in the test below): the waiting
    * workgroups gave up, so the layer's outputs are invalid.  The host wrapper raises
    * RTKV_ERR_TIMEOUT. */
-  RTKV_FLAG_SPIN_TIMEOUT = 2
+  RTKV_FLAG_SPIN_TIMEOUT = 2,
+  /* rtkv_compress_layer_finish: the layer's S'_max or packed byte count exceeds the buffers the caller
+   * declared (out_rows, packed_capacity); K4 wrote nothing. */
+  RTKV_FLAG_OUTPUT_OVERFLOW = 4
 };
 
 /* Flags for rtkv_layer_params.flags */
@@ -67,13 +70,12 @@ enum rtkv_layer_flag {
   RTKV_NO_FALLBACK = 8,    /* skip the top-10% emergency fallback (select_tokens_with_budget alone) */
   RTKV_SELECT_PIPELINE = 16, /* use the multi-workgroup selection pipeline even where the one-workgroup
                               selection applies (B = 1, S <= 32768); same results, for cross-checks */
-  RTKV_FUSED_QUANT = 32,   /* run the selection and the quantization as ONE launch (csrc/fused.h: the
-                              quantization workgroups start on the selection's early hand-offs) where it
-                              applies (B = 1, S <= 32768, contiguous 4096/5120-element rows); same results.
-                              Off by default: measured slower than the two launches on MI355X */
-  RTKV_TEST_WITHHOLD_SELECTION = 1 << 16 /* test only: the one-launch selection never publishes its
+  RTKV_TEST_WITHHOLD_SELECTION = 1 << 16, /* test only: the one-launch selection never publishes its
                               thresholds, so every waiting workgroup runs into its poll bound and the
                               layer reports RTKV_FLAG_SPIN_TIMEOUT instead of hanging */
+  RTKV_TEST_WITHHOLD_LOOKBACK = 1 << 17 /* test only: the one-launch selection publishes its early
+                              statistics, then workgroup 0 never publishes its kept counts, so the other
+                              workgroups' look-back runs into its poll bound AFTER the early publication */
 };
 
 /* ------------------------------------------------------------------------------------------------
@@ -307,6 +309,13 @@ typedef struct rtkv_early_stats {
   int32_t reserved;
   rtkv_layer_stats stats;    /* score_m2 not set */
   rtkv_batch_stats batch;    /* B = 1; kept_score_sum not set */
+  /* Written by rtkv_compress_layer_finish's K4 when it starts (all selection waits are over then):
+   * final_flags = the layer's complete RTKV_FLAG_* word, then final_seq = the begin call's seq
+   * (release, system scope).  A flag raised after the early publication (a look-back timeout) or by
+   * K4 itself (RTKV_FLAG_OUTPUT_OVERFLOW) is seen here without a stream sync. */
+  uint64_t final_seq;
+  int32_t final_flags;
+  int32_t reserved2;
 } rtkv_early_stats;
 
 int rtkv_compress_layer_early(const rtkv_kv_desc* kv, const rtkv_attn_desc* w, const rtkv_layer_params* p,
@@ -325,7 +334,20 @@ int rtkv_wait_early(const rtkv_early_stats* early_host, uint64_t seq, int64_t ti
  * >= S).  With S' and the packed byte count known (rtkv_wait_early, or stats_dev after a stream sync
  * when *published = 0), the caller allocates K'/V' of [B, S', F] and packed buffers of exactly that
  * many bytes and calls rtkv_compress_layer_finish (K4) with the same per-token buffers, the same
- * row_capacity and workspace, o_stride_b = -1, on the same stream. */
+ * row_capacity and workspace, o_stride_b = -1, on the same stream.
+ *
+ * Between begin and finish the workspace and the per-token buffers BELONG TO THE PENDING LAYER: K2
+ * leaves each kept row's class and the selection scratch there for K4, so a begin or compress call
+ * that reuses the same workspace before finish corrupts the pending layer (stream order hides it).
+ *
+ * finish: out_rows = the rows per batch row K'/V' hold (>= the published S'_max; ignored without
+ * EMIT_DEQUANT), out->packed_capacity = the bytes of each packed buffer; both must come from THIS
+ * layer's published statistics.  K4 compares them with the device statistics and, if either is too
+ * small, writes nothing and sets RTKV_FLAG_OUTPUT_OVERFLOW.  If the selection timed out
+ * (RTKV_FLAG_SPIN_TIMEOUT, possibly after the early publication) K4 writes NaN rows and NaN
+ * scale/zero-points instead of codes.  early_host (nullable, the begin call's buffer) + seq: K4
+ * publishes the layer's final flags there (final_flags / final_seq), so the host can check the
+ * layer before it trusts the outputs without syncing the stream. */
 int rtkv_compress_layer_begin(const rtkv_kv_desc* kv, const rtkv_attn_desc* w, const rtkv_layer_params* p,
                               const rtkv_layer_out* out, void* workspace_dev, size_t workspace_bytes, void* stream,
                               rtkv_early_stats* early_host, uint64_t seq, int32_t* published);
@@ -333,7 +355,8 @@ int rtkv_compress_layer_qk_begin(const rtkv_kv_desc* kv, const rtkv_qk_desc* q, 
                                  const rtkv_layer_out* out, void* workspace_dev, size_t workspace_bytes, void* stream,
                                  rtkv_early_stats* early_host, uint64_t seq, int32_t* published);
 int rtkv_compress_layer_finish(const rtkv_kv_desc* kv, const rtkv_layer_params* p, const rtkv_layer_out* out,
-                               void* workspace_dev, size_t workspace_bytes, void* stream);
+                               int64_t out_rows, void* workspace_dev, size_t workspace_bytes, void* stream,
+                               rtkv_early_stats* early_host, uint64_t seq);
 /* Pinned, device-coherent host memory for rtkv_early_stats (hipHostMalloc, coherent + mapped). */
 void* rtkv_host_alloc(size_t bytes);
 void rtkv_host_free(void* p);
@@ -417,6 +440,17 @@ size_t rtkv_qk_scratch_size(int64_t B, int64_t H, int64_t S);
 size_t rtkv_workspace_size_qk(int64_t B, int64_t H, int64_t S);
 int rtkv_importance_qk_lse_ws(const rtkv_qk_desc* q, int32_t prompt_len, float* A_dev, void* scratch_dev,
                               size_t scratch_bytes, void* stream);
+
+/* Model-side mask check (the mask the reference adds before its softmax,
+ * modified_llama.py:90-91).  mask[b*stride_b + i*stride_i + j*stride_j] for i, j < S, dtype fp32/f16/bf16
+ * (B = the mask's batch rows).  thr = finfo(dtype).min / 2 rounded to the dtype (the host passes it).
+ * Writes valid[b*valid_stride_b + j] = 1 unless the last query row masks key j, and ADDS to counts_dev
+ * (two uint64, zeroed by the caller): counts[0] = entries that break "causal ∧ key padding" (an entry
+ * must be 0 where j <= i and key j is valid, else <= thr), counts[1] = padded keys.  One pass over the
+ * mask, no [B, S, S] temporaries; the caller reads both counts with one sync. */
+int rtkv_mask_key_padding(const void* mask_dev, int32_t dtype, int64_t B, int64_t S, int64_t stride_b,
+                          int64_t stride_i, int64_t stride_j, float thr, uint8_t* valid_dev, int64_t valid_stride_b,
+                          unsigned long long* counts_dev, void* stream);
 
 /* Row log-sum-exp of the prefill attention: lse[b,h,i] = log Σ_j exp(q_i·k_j·scale)
  * over j ≤ i (causal) or all j < S, without materialising the [B,H,S,S] softmax of

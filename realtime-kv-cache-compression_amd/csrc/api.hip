@@ -292,17 +292,11 @@ static int compress_layer_impl(const rtkv_kv_desc* kv, const rtkv_attn_desc* w, 
     if (published) *published = 1;
   }
   if (stop_after_select) {
-    rc = launch_select(a, ws.sel, true, st);
+      rc = launch_select(a, ws.sel, true, st);
     if (rc) return rc;
     return mark(2);
   }
   const QuantArgs q = make_quant_args(kv, out->labels_dev, out->kept_index_dev, p, out, row_labels ? ws.labels : nullptr);
-  if (fused_eligible(a, q)) {  // K2 + K4 in one launch (fused.h): events 1 and 2 mark the same point
-    if ((rc = mark(2))) return rc;
-    rc = launch_select_quant_fused(a, ws.sel, q, st);
-    if (rc) return rc;
-    return mark(3);
-  }
   rc = launch_select(a, ws.sel, true, st);
   if (rc) return rc;
   if ((rc = mark(2))) return rc;
@@ -356,7 +350,8 @@ int rtkv_compress_layer_qk_begin(const rtkv_kv_desc* kv, const rtkv_qk_desc* q, 
 }
 
 int rtkv_compress_layer_finish(const rtkv_kv_desc* kv, const rtkv_layer_params* p, const rtkv_layer_out* out,
-                               void* workspace_dev, size_t workspace_bytes, void* stream) {
+                               int64_t out_rows, void* workspace_dev, size_t workspace_bytes, void* stream,
+                               rtkv_early_stats* early_host, uint64_t seq) {
   int rc = check_params(p);
   if (rc) return rc;
   RTKV_REQUIRE(kv && out && out->labels_dev && out->kept_index_dev && out->stats_dev,
@@ -367,15 +362,21 @@ int rtkv_compress_layer_finish(const rtkv_kv_desc* kv, const rtkv_layer_params* 
                      out->packed_capacity >= 1,
                  "EMIT_PACKED needs packed_k, packed_v (>= the published packed bytes), row_offset and scale_zp");
   if (p->flags & RTKV_EMIT_DEQUANT)
-    RTKV_REQUIRE(out->k_out_dev && out->v_out_dev && out->o_stride_b < 0,
-                 "EMIT_DEQUANT needs k_out / v_out of [B, S', F] rows packed at the kept count (o_stride_b = -1)");
+    RTKV_REQUIRE(out->k_out_dev && out->v_out_dev && out->o_stride_b < 0 && out_rows >= 1,
+                 "EMIT_DEQUANT needs k_out / v_out of [B, out_rows >= 1, F] rows packed at the kept count "
+                 "(o_stride_b = -1)");
   Workspace ws;
   rc = carve(workspace_dev, workspace_bytes, kv->B, kv->S, ws);
   if (rc) return rc;
   // the one-launch K2 (B = 1, S <= 32768) left each kept row's class in the workspace
   const bool row_labels = select_fast_shape(kv->B, kv->S) && !(p->flags & RTKV_SELECT_PIPELINE);
-  return launch_quant(make_quant_args(kv, out->labels_dev, out->kept_index_dev, p, out, row_labels ? ws.labels : nullptr),
-                      (hipStream_t)stream);
+  QuantArgs q = make_quant_args(kv, out->labels_dev, out->kept_index_dev, p, out, row_labels ? ws.labels : nullptr);
+  // the buffers were sized on the host from the published statistics: K4 checks them on the device
+  q.out_rows = (p->flags & RTKV_EMIT_DEQUANT) ? out_rows : ((int64_t)1 << 62);
+  if (!(p->flags & RTKV_EMIT_PACKED)) q.out.packed_capacity = (int64_t)1 << 62;
+  q.final_host = early_host;
+  q.final_seq = seq;
+  return launch_quant(q, (hipStream_t)stream);
 }
 
 int rtkv_wait_early(const rtkv_early_stats* early_host, uint64_t seq, int64_t timeout_us) {

@@ -266,14 +266,16 @@ struct QuantArgs {
   // (packed codes and scale/zero-point keep their global positions).
   int32_t shard_rank, shard_nranks;
   const int64_t* shard_ranges;
+  // rtkv_compress_layer_finish: the caller's buffers were sized from the early statistics.  out_rows > 0:
+  // K'/V' hold that many rows per batch row and out.packed_capacity bytes per code plane; K4 compares them
+  // with the device statistics first (RTKV_FLAG_OUTPUT_OVERFLOW, nothing written).  final_host: K4's first
+  // lane publishes the layer's final flags + final_seq there.
+  int64_t out_rows;
+  rtkv_early_stats* final_host;
+  uint64_t final_seq;
 };
 int launch_quant(const QuantArgs& a, hipStream_t st);
 
-// K2 + K4 in one launch (fused.h) for B = 1, S <= 32768, contiguous rows of 4096 or 5120 elements
-// (fp32: 4096), packed widths 2/4/8/16.  The selection scratch (select_fast_zero_bytes()) and the
-// statistics must be zero (K1 clears them), and a.T2 must be K1's position term.
-bool fused_eligible(const FinalizeArgs& a, const QuantArgs& q);
-int launch_select_quant_fused(const FinalizeArgs& a, void* sel_ws, const QuantArgs& q, hipStream_t st);
 
 int launch_shard_ranges(const int32_t* kept_index, const int64_t* row_offset, const rtkv_layer_stats* stats, int64_t B,
                         int64_t cap, int64_t S_local, int nranks, int64_t* ranges, hipStream_t st);

@@ -350,16 +350,44 @@ __global__ __launch_bounds__(64 * kDW) void decode_split_kernel(DecodeArgs a) {
   // Rows of this wave: r0 + wave + kDW·t.  Metadata of 64 rows at a time, one row per lane; the
   // rows of each field width are then taken together (ballot), so the code loads have the width's
   // exact size (W bytes per chunk) and PD rows of them are kept in flight.
+  // A row's width comes from its byte span: rows are back to back, so row_offset[r + 1] − row_offset[r]
+  // = F·W/8 — two independent loads instead of kept_index → labels (two dependent round trips); only
+  // the row list's last row (no successor) takes its class.  A span that matches no width (corrupt
+  // metadata) leaves the row out.  The next 64 rows' metadata is in flight while this batch's rows are
+  // processed.
+  const int64_t bcap = (int64_t)b * a.cap;
+  auto meta = [&](int64_t jb, int64_t& off, int64_t& offn, float4& sz) {
+    const int64_t jr = jb + (int64_t)kDW * lane;
+    const bool ok = jr < r1, nx = jr + 1 < nrows;
+    const int64_t rj = bcap + (ok ? jr : jb);
+    off = a.row_offset[rj];
+    offn = (ok && nx) ? a.row_offset[rj + 1] : -1;
+    sz = *reinterpret_cast<const float4*>(a.scale_zp + rj * 4);
+  };
+  int64_t m_off = 0, m_offn = -1;
+  float4 m_sz = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (r0 + wave < r1) meta(r0 + wave, m_off, m_offn, m_sz);
   for (int64_t jb = r0 + wave; jb < r1; jb += 64 * kDW) {
     const int64_t jr = jb + (int64_t)kDW * lane;
     const bool ok = jr < r1;
-    const int64_t rj = (int64_t)b * a.cap + (ok ? jr : jb);
-    const int ki0 = a.kept_index[rj];
-    const int ki = ki0 < 0 ? 0 : (ki0 >= a.S ? (int)a.S - 1 : ki0);
-    const int64_t off = a.row_offset[rj];
-    const float4 sz = *reinterpret_cast<const float4*>(a.scale_zp + rj * 4);
-    const int lab = a.labels[(int64_t)b * a.S + ki];
-    const int wl = lab == 2 ? a.w[2] : (lab == 1 ? a.w[1] : a.w[0]);
+    const int64_t off = m_off;
+    const float4 sz = m_sz;
+    int wl = 0;
+    {
+      const int64_t span = m_offn - off;  // F·W/8 for a consistent row
+      const int fb8 = F / 8;
+#pragma unroll
+      for (int c = 0; c < 3; ++c)
+        if (span == (int64_t)fb8 * a.w[c]) wl = a.w[c];
+      const bool lastrow = ok && jr + 1 == nrows;
+      if (__ballot(lastrow)) {  // the list's last row: its class (kept index → label)
+        const int ki0 = a.kept_index[bcap + (lastrow ? jr : jb)];
+        const int ki = ki0 < 0 ? 0 : (ki0 >= a.S ? (int)a.S - 1 : ki0);
+        const int lab = a.labels[(int64_t)b * a.S + ki];
+        if (lastrow) wl = lab == 2 ? a.w[2] : (lab == 1 ? a.w[1] : a.w[0]);
+      }
+    }
+    if (jb + 64 * kDW < r1) meta(jb + 64 * kDW, m_off, m_offn, m_sz);  // the next batch, in flight meanwhile
     const uint32_t off_lo = (uint32_t)off, off_hi = (uint32_t)(off >> 32);
     auto by_width = [&](auto wtag) {
       constexpr int W = decltype(wtag)::value;

@@ -195,14 +195,23 @@ __global__ __launch_bounds__(256) void aggregation_vec_kernel(const typename Dt<
 // HB heads per load batch; PF: the next batch's loads are issued before the current batch is
 // summed (two batches in flight, so every wave keeps streaming).  The per-element addition order is
 // the same for every (HB, PF): heads in order, the cascade step after every 16th head.
-template <int DT, int CPR, int HB = 16, bool PF = false, int BT = 256>
-__global__ __launch_bounds__(BT) void aggregation_shfl_kernel(const typename Dt<DT>::S* __restrict__ W, int H,
+//
+// SPLIT (32 <= H <= 64): the workgroup's two halves stream the head range in two parts at once —
+// half 0 the first ceil(nb/2) 16-head blocks, half 1 the other full blocks (each summed from zero, as
+// multi_row_sum sums a block before adding it into the level-1 accumulator) and the tail — so a
+// 16-byte chunk per thread gives twice the threads (waves per CU) of the unsplit kernel, and every
+// thread's loads are in flight at once.  Half 1 hands its block sums over through LDS; half 0 adds
+// them in block order (a1 += block, the cascade step) and takes the tail as a0: the same additions
+// in the same order as the sequential loop.
+template <int DT, int CPR, int HB = 16, bool PF = false, int BT = 256, bool SPLIT = false, int HC = 0>
+__global__ __launch_bounds__(BT, SPLIT ? 2 * BT / 256 : 1) void aggregation_shfl_kernel(const typename Dt<DT>::S* __restrict__ W, int H,
                                                                int64_t S, int64_t sb, int64_t sh, int64_t ss,
                                                                int64_t lim, float* __restrict__ A, AggExtras ex) {
   using S_ = typename Dt<DT>::S;
   using V = uint4;
   constexpr int P = 8 * CPR;
-  constexpr int TT = BT / CPR;   // tokens per block
+  constexpr int HALF = SPLIT ? BT / 2 : BT;
+  constexpr int TT = HALF / CPR; // tokens per block
   constexpr int NV = CPR / 2;    // 16-column groups
   constexpr int NQ = NV / 4;
   constexpr int NW = BT / 64;
@@ -210,7 +219,9 @@ __global__ __launch_bounds__(BT) void aggregation_shfl_kernel(const typename Dt<
   zero_regions(ex);
   const int b = blockIdx.y;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int tok = threadIdx.x / CPR, ch = threadIdx.x % CPR;
+  const int half = SPLIT ? (int)(threadIdx.x >= HALF) : 0;
+  const int tid = threadIdx.x - half * HALF;
+  const int tok = tid / CPR, ch = tid % CPR;
   const int64_t i = (int64_t)blockIdx.x * TT + tok;
   const bool valid = i < S;
   const int64_t ic = valid ? i : S - 1;  // clamped row (its loads are discarded)
@@ -248,7 +259,78 @@ __global__ __launch_bounds__(BT) void aggregation_shfl_kernel(const typename Dt<
     }
   };
   int h = 0;
-  if constexpr (!PF) {
+  if constexpr (SPLIT) {
+    static_assert(!PF && HC >= 32 && HC <= 64, "split: a compile-time head count in [32, 64]");
+    __shared__ float4 xfer[3][HALF][2];  // half 1's full-block sums (<= 2) and tail sum, 8 floats per thread
+    constexpr int nfull = HC >> 4, nb0 = (nfull + 1) >> 1;
+    // 4-head load batches (as the fp32 kernel): <= 64 VGPRs, so two 1024-thread workgroups (32 waves,
+    // 128 KB of loads in flight) fit a CU
+    auto add4 = [&](int h0) {
+      V v[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) v[j] = load16_nt(base + (int64_t)(h0 + j) * sh);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        float x[8];
+        unpack_vec<DT, 8>(v[j], x);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) a0[e] += x[e];
+      }
+      // the next batch's loads stay behind this one's adds (the sums are pinned here, then no memory
+      // op crosses): 4 loads in flight per thread, 32 waves per CU
+      asm volatile("" : "+v"(a0[0]), "+v"(a0[1]), "+v"(a0[2]), "+v"(a0[3]), "+v"(a0[4]), "+v"(a0[5]), "+v"(a0[6]),
+                   "+v"(a0[7])::"memory");
+      __builtin_amdgcn_sched_barrier(0);
+    };
+    if (half == 0) {
+#pragma unroll
+      for (; h < 16 * nb0; h += 16) {
+        add4(h);
+        add4(h + 4);
+        add4(h + 8);
+        add4(h + 12);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {  // the cascade step (H <= 64: a2, a3 stay zero)
+          a1[e] += a0[e];
+          a0[e] = 0.f;
+        }
+      }
+    } else {
+      int k = 0;
+#pragma unroll
+      for (h = 16 * nb0; h + 16 <= HC; h += 16, ++k) {
+        add4(h);
+        add4(h + 4);
+        add4(h + 8);
+        add4(h + 12);
+        xfer[k][tid][0] = make_float4(a0[0], a0[1], a0[2], a0[3]);
+        xfer[k][tid][1] = make_float4(a0[4], a0[5], a0[6], a0[7]);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) a0[e] = 0.f;
+      }
+#pragma unroll
+      for (; h < HC; ++h) {  // the tail (H % 16 heads), sequential from zero
+        float x[8];
+        unpack_vec<DT, 8>(*reinterpret_cast<const V*>(base + (int64_t)h * sh), x);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) a0[e] += x[e];
+      }
+      xfer[2][tid][0] = make_float4(a0[0], a0[1], a0[2], a0[3]);
+      xfer[2][tid][1] = make_float4(a0[4], a0[5], a0[6], a0[7]);
+    }
+    __syncthreads();
+    if (half == 0) {
+      for (int k = 0; k < nfull - nb0; ++k) {  // blocks nb0.. in order: the cascade step of each
+        const float4 u = xfer[k][tid][0], w = xfer[k][tid][1];
+        const float blk[8] = {u.x, u.y, u.z, u.w, w.x, w.y, w.z, w.w};
+#pragma unroll
+        for (int e = 0; e < 8; ++e) a1[e] += blk[e];
+      }
+      const float4 u = xfer[2][tid][0], w = xfer[2][tid][1];
+      a0[0] = u.x; a0[1] = u.y; a0[2] = u.z; a0[3] = u.w; a0[4] = w.x; a0[5] = w.y; a0[6] = w.z; a0[7] = w.w;
+    }
+    h = HC;
+  } else if constexpr (!PF) {
     while (h + HB <= H) {
       V v[HB];
       load_batch(v, h);
@@ -285,7 +367,9 @@ __global__ __launch_bounds__(BT) void aggregation_shfl_kernel(const typename Dt<
     s += a2[k];
     s += a3[k];
     const int64_t col = ic * P + ch * 8 + k;
-    if (col >= lim) {  // columns past the 32-aligned block: row_sum (ilp 4) order
+    // columns past the 32-aligned block of the flattened [S*P] take row_sum's (ilp 4) order; with P a
+    // multiple of 32 every column is inside it (lim = S*P), and the branch compiles away
+    if (P % 32 != 0 && col >= lim && half == 0) {
       const S_* colp = W + b * sb + ic * ss + ch * 8 + k;
       s = row_sum_ilp4([&](int hh) { return Dt<DT>::load(colp[(int64_t)hh * sh]); }, H);
     }
@@ -304,11 +388,13 @@ __global__ __launch_bounds__(BT) void aggregation_shfl_kernel(const typename Dt<
 #pragma unroll
     for (int j = 0; j < NQ; ++j) acc += __shfl(y[k], tl + 2 * (4 * j + (ch >> 1 & 3)), 64);
     part[k] = acc;
+    if constexpr (SPLIT) __builtin_amdgcn_sched_barrier(0);  // one k at a time: fits 64 VGPRs
   }
   // chunk 0 folds: part0 (+ tail groups) + part1 + part2 + part3, then the 8 vector lanes
   float fin = 0.f;
 #pragma unroll
   for (int k = 0; k < 8; ++k) {
+    if constexpr (SPLIT) __builtin_amdgcn_sched_barrier(0);
     float p0 = part[k];
 #pragma unroll
     for (int mm = 4 * NQ; mm < NV; ++mm) p0 += __shfl(y[k], tl + 2 * mm, 64);
@@ -320,7 +406,7 @@ __global__ __launch_bounds__(BT) void aggregation_shfl_kernel(const typename Dt<
   }
   const float Ai = Dt<DT>::rnd(fin);
   float mn = INFINITY, mx = -INFINITY;
-  if (ch == 0 && valid) {
+  if (ch == 0 && valid && half == 0) {  // (SPLIT: half 1's waves only streamed heads)
     A[(int64_t)b * S + i] = Ai;
     if (ex.t2 && b == 0) ex.t2[i] = ex.beta * ((S > 1) ? torch_logf((uint32_t)(i + 1)) / ex.logS : 0.f);
     mn = mx = Ai;
@@ -415,7 +501,7 @@ __global__ __launch_bounds__(BT) void aggregation_shfl32_kernel(const float* __r
     s += a2[k];
     s += a3[k];
     const int64_t col = ic * P + ch * 4 + k;
-    if (col >= lim) {  // columns past the 32-aligned block: row_sum (ilp 4) order
+    if (P % 32 != 0 && col >= lim) {  // columns past the 32-aligned block: row_sum (ilp 4) order
       const float* colp = W + b * sb + ic * ss + ch * 4 + k;
       s = row_sum_ilp4([&](int hh) { return colp[(int64_t)hh * sh]; }, H);
     }
@@ -540,6 +626,17 @@ static int64_t cascade_limit(int dt, int64_t M) {
   return (M / 4) * 4;
 }
 
+// Register-path workgroup size: 1024 threads (16 KB contiguous per head per workgroup, the fastest at
+// cfg3) as long as that still gives every CU a workgroup; smaller workgroups below, so that short
+// prompts (S = 4096: 128 workgroups of 1024 threads would leave half the CUs idle) fill the chip.
+// chunks = 16-byte chunks per token row (16 fp16/bf16, 32 fp32 at P = 128).
+static int k1_block_threads(int64_t tokens, int chunks) {
+  const int64_t want = 256;  // one per CU
+  for (int bt = 1024; bt > 256; bt >>= 1)
+    if (tokens / (bt / chunks) >= want) return bt;
+  return 256;
+}
+
 template <int DT>
 static int launch_agg_dt(const rtkv_attn_desc& w, int P, float* A, hipStream_t st, const AggExtras& x) {
   using S_ = typename Dt<DT>::S;
@@ -557,11 +654,26 @@ static int launch_agg_dt(const rtkv_attn_desc& w, int P, float* A, hipStream_t s
       // 4-head batches with the next one in flight (isolated, tools/k1_grid_probe.hip: 28.7 vs 24.9).
       // 1024-thread workgroups: 64 tokens, 16 KB contiguous per head per workgroup (cfg3 fp16 in the
       // pipeline: 27.8 us against 30.0 for 512 threads and 30.1 for 256).  RTKV_K1_BT16: 256/512/1024.
-      static const int bt = [] {
+      static const int bt_env = [] {
         const char* e = getenv("RTKV_K1_BT16");
-        const int v = e ? atoi(e) : 1024;
-        return v == 256 || v == 512 ? v : 1024;
+        const int v = e ? atoi(e) : 0;
+        return v == 256 || v == 512 || v == 1024 ? v : 0;
       }();
+      if ((H == 32 || H == 40) && !getenv("RTKV_K1_NOSPLIT")) {
+        // Llama-2-7B / 13B heads: the head range in two halves per workgroup, twice the waves per CU
+        // (RTKV_K1_NOSPLIT: the unsplit kernel, for cross-checks)
+        dim3 grid((unsigned)((w.S + 31) / 32), (unsigned)w.B);
+        if (x.nparts) *x.nparts = (int)grid.x;
+        if (H == 32)
+          hipLaunchKernelGGL((aggregation_shfl_kernel<DT, 16, 16, false, 1024, true, 32>), grid, dim3(1024), 0, st,
+                             W, H, w.S, w.stride_b, w.stride_h, w.stride_s, lim, A, x);
+        else
+          hipLaunchKernelGGL((aggregation_shfl_kernel<DT, 16, 16, false, 1024, true, 40>), grid, dim3(1024), 0, st,
+                             W, H, w.S, w.stride_b, w.stride_h, w.stride_s, lim, A, x);
+        RTKV_HIP_CHECK(hipGetLastError());
+        return RTKV_OK;
+      }
+      const int bt = bt_env ? bt_env : k1_block_threads(w.S * w.B, 16);
       const int tt = bt / 16;
       dim3 grid((unsigned)((w.S + tt - 1) / tt), (unsigned)w.B);
       if (x.nparts) *x.nparts = (int)grid.x;
@@ -582,11 +694,12 @@ static int launch_agg_dt(const rtkv_attn_desc& w, int P, float* A, hipStream_t s
       // 4 heads per load batch (tools/k1_grid_probe.hip: 46.5 us vs 56 us for 16-head batches at cfg3);
       // 1024-thread workgroups: 32 tokens, i.e. 16 KB contiguous per head per workgroup (cfg3 in the
       // pipeline: 47.1 us against 48.6 for 512 threads and 52.8 for 256).  RTKV_K1_BT: 256/512/1024.
-      static const int bt = [] {
+      static const int bt_env = [] {
         const char* e = getenv("RTKV_K1_BT");
-        const int v = e ? atoi(e) : 1024;
-        return v == 256 || v == 512 ? v : 1024;
+        const int v = e ? atoi(e) : 0;
+        return v == 256 || v == 512 || v == 1024 ? v : 0;
       }();
+      const int bt = bt_env ? bt_env : k1_block_threads(w.S * w.B, 32);
       const int tt = bt / 32;
       dim3 grid((unsigned)((w.S + tt - 1) / tt), (unsigned)w.B);
       if (x.nparts) *x.nparts = (int)grid.x;

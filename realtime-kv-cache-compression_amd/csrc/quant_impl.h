@@ -450,6 +450,56 @@ __device__ __forceinline__ void emit_row(const Chunk<DT> (&raw)[NCH], const RowP
   else by_width(std::false_type{});
 }
 
+// Layer-level checks of a K4 launch, made before its first row (every workgroup reads the same
+// statistics, K2 having finished before this launch):
+//  * finish (a.out_rows > 0): the caller sized K'/V' and the code planes from the early statistics;
+//    a layer whose S'_max or packed byte count exceeds them is flagged RTKV_FLAG_OUTPUT_OVERFLOW and
+//    nothing is written;
+//  * a selection that timed out (RTKV_FLAG_SPIN_TIMEOUT, possibly after the early publication) left
+//    kept_index unwritten: its rows are written as NaN (scale/zero-point too) so that stale buffers
+//    never pass for results;
+//  * finish with a host mirror: lane 0 of workgroup 0 publishes the final flags + final_seq there.
+// Returns true when the launch must not quantize.
+template <int DT>
+__device__ __forceinline__ bool k4_layer_gate(const QuantArgs& a) {
+  if (!a.stats) return false;
+  rtkv_layer_stats* st = const_cast<rtkv_layer_stats*>(a.stats);
+  int flags = st->error_flags;
+  const int64_t max_kept = st->max_kept, nbytes = st->total_packed_bytes;
+  const bool over = a.out_rows > 0 && ((a.out.k_out_dev && max_kept > a.out_rows) ||
+                                       (a.out.packed_k_dev && nbytes > a.out.packed_capacity));
+  if (over) flags |= RTKV_FLAG_OUTPUT_OVERFLOW;
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    if (over) atomicOr(&st->error_flags, (int)RTKV_FLAG_OUTPUT_OVERFLOW);
+    if (a.final_host) {
+      __hip_atomic_store(&a.final_host->final_flags, flags, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      __hip_atomic_store(&a.final_host->final_seq, a.final_seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+  }
+  if (over) return true;
+  if (!(flags & RTKV_FLAG_SPIN_TIMEOUT)) return false;
+  if (a.S_glob != 0 || !a.kept_index) return true;  // shard launches: the host raises; nothing to poison locally
+  using S_ = typename Dt<DT>::S;
+  const int64_t B = a.kv.B, D = a.kv.D, F = a.kv.H * a.kv.D;
+  int64_t R = max_kept < 0 ? 0 : max_kept;
+  if (R > a.out.row_capacity) R = a.out.row_capacity;
+  if (a.out_rows > 0 && R > a.out_rows) R = a.out_rows;
+  const int64_t osb = a.out.o_stride_b >= 0 ? a.out.o_stride_b : R * a.out.o_stride_s;
+  const float qnan = __builtin_nanf("");
+  const int lane = threadIdx.x & 63;
+  const int64_t nw = (int64_t)gridDim.x * (blockDim.x >> 6);
+  for (int64_t t = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); t < 2 * B * R; t += nw) {
+    const int which = (int)(t & 1);
+    const int64_t rr = t >> 1, b = rr / R, r = rr - b * R;
+    if (a.out.k_out_dev) {
+      S_* orow = static_cast<S_*>(which ? a.out.v_out_dev : a.out.k_out_dev) + b * osb + r * a.out.o_stride_s;
+      for (int64_t f = lane; f < F; f += 64) orow[(f / D) * a.out.o_stride_h + (f % D)] = Dt<DT>::store(qnan);
+    }
+    if (a.out.scale_zp_dev && lane < 2) a.out.scale_zp_dev[(b * a.out.row_capacity + r) * 4 + which * 2 + lane] = qnan;
+  }
+  return true;
+}
+
 // Contiguous fp32 rows of exactly 4096 elements fit 128 VGPRs (4 waves/SIMD); the gate bookkeeping would push the
 // compiler to 129 (3 waves) without the bound.  Wider fp32 rows keep the 256-register budget.
 // Row geometry shared by every task of a launch: element f of a row lives at (f / D) * stride_h + f % D.
@@ -484,8 +534,7 @@ __global__ __launch_bounds__(256, (DT == RTKV_F32 && NCH == 8 && FULL && CONTIG)
     osb = a.out.o_stride_b >= 0 ? a.out.o_stride_b : (int64_t)R * a.out.o_stride_s;
   }
   const rtkv_batch_stats* bst = a.stats ? reinterpret_cast<const rtkv_batch_stats*>(a.stats + 1) : nullptr;
-  // a selection that timed out (RTKV_FLAG_SPIN_TIMEOUT) left kept_index unwritten: read nothing
-  if (a.stats && (a.stats->error_flags & RTKV_FLAG_SPIN_TIMEOUT)) return;
+  if (k4_layer_gate<DT>(a)) return;  // buffer sizes, final flags, a timed-out selection
   const bool emit_deq = a.out.k_out_dev != nullptr;
   const bool emit_pk = a.out.packed_k_dev != nullptr;
   // per-lane in-row offsets of each chunk (task independent)
@@ -589,7 +638,7 @@ __global__ __launch_bounds__(256) void quant_rows_generic_kernel(QuantArgs a) {
   int64_t R = a.kept_index ? a.stats->max_kept : S;
   if (R > cap) R = cap;
   const rtkv_batch_stats* bst = a.stats ? reinterpret_cast<const rtkv_batch_stats*>(a.stats + 1) : nullptr;
-  if (a.stats && (a.stats->error_flags & RTKV_FLAG_SPIN_TIMEOUT)) return;
+  if (k4_layer_gate<DT>(a)) return;
   const bool emit_deq = a.out.k_out_dev != nullptr;
   const bool emit_pk = a.out.packed_k_dev != nullptr;
   const int64_t osb = a.out.o_stride_b >= 0 ? a.out.o_stride_b : R * a.out.o_stride_s;

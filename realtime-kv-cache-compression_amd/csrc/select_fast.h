@@ -73,12 +73,7 @@ struct FastHead {                  // zeroed before the launch (K1 or a memset):
   uint64_t part[kMaxG];            // phase 1, per workgroup: kTag | class counts (3 x 11 bits), from registers
   uint64_t ready[kMaxG];           // phase 1, per workgroup: kTag once its slot entries, partials, scores and
                                    // classes are complete (drained)
-  uint64_t sel[8];                 // phase 2: [q] kTag | fallback<<50 | mode<<48 | cut<<32 | T; [4], [5] the mean;
-                                   // [6] kTag | kept rows<<16 | fallback<<8 (fused).  cut: the largest token
-                                   // index of group q's ties at T that are kept (ties go in token order)
   uint64_t agg[kMaxG];             // phase 3, per workgroup: kTag | kept tokens per class (3 x 11 bits)
-  uint64_t rowinfo[kMaxS][2];      // fused, phase 3, per kept row r: {kTag | class<<32 | token, kTag | k2<<32 |
-                                   // k1<<16 | k0}, k_c = kept rows of class c before it (its packed offset)
 };
 struct FastPartial {               // phase 1, per workgroup (complete before its counts word)
   double ssum;
@@ -100,8 +95,10 @@ struct FastArgs {
   rtkv_early_stats* early;         // host-mapped stats mirror (nullable), published by the selecting workgroup
   uint64_t early_seq;
   uint32_t spin_limit;             // polls before a hand-off wait gives up (poll_tagged)
-  int withhold;                    // RTKV_TEST_WITHHOLD_SELECTION: never publish the selection words
-  int fused;                       // the quantization waves of the same launch consume sel[6..7] and tokrow
+  int withhold;                    // RTKV_TEST_WITHHOLD_SELECTION: workgroup G-1 never publishes its ready
+                                   // word (phase 2 times out everywhere); RTKV_TEST_WITHHOLD_LOOKBACK:
+                                   // workgroup 0 never publishes its phase-3 counts (the look-back times out
+                                   // AFTER the early statistics are out)
 };
 
 __device__ __forceinline__ float key_score(uint32_t k) {
@@ -481,6 +478,71 @@ __device__ __forceinline__ void rescan_thresholds(const FastArgs& g, uint32_t* h
 // Workgroup G−1, after its own phase 1: quotas, threshold bins, exact thresholds; publishes the
 // selection words and the statistics.  s_selw receives the selection words (thread 0 writes them;
 // the caller's barrier publishes them to the workgroup).
+// The layer statistics phase 2 knows (class counts, quotas = the final kept counts unless the fallback
+// runs, score sum and range, the f16 16-bit flag) into the device block and, with an early buffer, the
+// host mirror — published by the selecting workgroup as soon as the quotas and the partials are in,
+// before its threshold search: the drop-in host allocates the exact outputs while the selection runs.
+__device__ __forceinline__ void publish_stats(const FastArgs& g, bool fallback, double ssum, uint32_t kr0, uint32_t kr1,
+                                           const int64_t (&ccount)[3], const int64_t (&quota)[3]) {
+  const FinalizeArgs& a = g.f;
+  rtkv_layer_stats* hs = a.stats;
+  rtkv_batch_stats* bs = reinterpret_cast<rtkv_batch_stats*>(hs + 1);
+  for (int q = 0; q < 3; ++q) bs->class_count[q] = ccount[q];
+  bs->fallback = fallback ? 1 : 0;
+  hs->score_sum = ssum;
+  hs->score_min = key_score(kr0);
+  hs->score_max = key_score(kr1);
+  int flags = 0;
+  if (a.kv_dtype == RTKV_F16)
+    for (int q = 0; q < 3; ++q)
+      if (ccount[q] > 0 && a.p.bits[q] >= 16) flags |= RTKV_FLAG_F16_QMAX_OVERFLOW;
+  if (flags) atomicOr(&hs->error_flags, flags);  // a spin timeout may have been flagged already
+  hs->B = 1;
+  if (!fallback) {  // the kept counts are the quotas: final here (phase 3 adds only the score sums)
+    int64_t n = 0, units = 0, bytes = 0;
+    for (int q = 0; q < 3; ++q) {
+      bs->kept_class[q] = quota[q];
+      n += quota[q];
+      units += quota[q] * (int64_t)a.p.bits[q];
+      bytes += quota[q] * row_bytes(a, q);
+    }
+    bs->kept = n;
+    bs->cost_units = units;
+    bs->packed_bytes = bytes;
+    hs->max_kept = n;
+    hs->total_packed_bytes = bytes;
+  }
+  if (g.early) {  // host-mapped mirror for the caller's early return (rtkv_compress_layer_early)
+    rtkv_early_stats* e = g.early;
+    auto put64 = [](void* dst, uint64_t v) {
+      __hip_atomic_store(reinterpret_cast<uint64_t*>(dst), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    };
+    auto put32 = [](void* dst, uint32_t v) {
+      __hip_atomic_store(reinterpret_cast<uint32_t*>(dst), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    };
+    const bool complete = !fallback && g.withhold != 1;  // withheld: the host takes the synchronised statistics
+    put32(&e->complete, complete ? 1u : 0u);
+    if (complete) {
+      put64(&e->stats.max_kept, (uint64_t)bs->kept);
+      put64(&e->stats.total_packed_bytes, (uint64_t)bs->packed_bytes);
+      put64(&e->stats.score_sum, __builtin_bit_cast(uint64_t, ssum));
+      put32(&e->stats.score_min, __builtin_bit_cast(uint32_t, hs->score_min));
+      put32(&e->stats.score_max, __builtin_bit_cast(uint32_t, hs->score_max));
+      put32(&e->stats.error_flags, (uint32_t)(flags | ld_sc1(&hs->error_flags)));
+      put32(&e->stats.B, 1u);
+      for (int q = 0; q < 3; ++q) {
+        put64(&e->batch.class_count[q], (uint64_t)ccount[q]);
+        put64(&e->batch.kept_class[q], (uint64_t)quota[q]);
+      }
+      put64(&e->batch.kept, (uint64_t)bs->kept);
+      put64(&e->batch.cost_units, (uint64_t)bs->cost_units);
+      put64(&e->batch.packed_bytes, (uint64_t)bs->packed_bytes);
+      put32(&e->batch.fallback, 0u);
+    }
+    __hip_atomic_store(&e->seq, g.early_seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
+
 template <int TPT>
 __device__ __forceinline__ void select_thresholds(const FastArgs& g, uint32_t* hist_lds, uint64_t* s_selw,
                                                   bool publish) {
@@ -536,10 +598,6 @@ __device__ __forceinline__ void select_thresholds(const FastArgs& g, uint32_t* h
       s_q[kGrp + 3] = (int)kf;
       md[3] = !fb ? M_NONE : (kf >= S ? M_ALL : M_PART);
       s_q[3] = md[3];
-      if (publish && g.fused && !g.withhold) {  // the kept row count: quantization waves of rows beyond it end now
-        const int64_t nkept = fb ? (kf < S ? kf : S) : kept;
-        st_sc1(&g.L.head->sel[6], kTag | ((uint64_t)nkept << 16) | ((uint64_t)(fb ? 1 : 0) << 8));
-      }
     }
   } else if (wid == 1) {
     // ---- every workgroup's phase-1 stores complete (slot lists, partials, scores, classes)
@@ -589,6 +647,11 @@ __device__ __forceinline__ void select_thresholds(const FastArgs& g, uint32_t* h
   }
 #endif
   __syncthreads();
+  if (publish && t == 0) {  // statistics known here; phase 3 adds the kept-token sums (stats zeroed before)
+    const int64_t ccount[3] = {s_cc[0], s_cc[1], s_cc[2]};
+    const int64_t quota[3] = {s_quota[0], s_quota[1], s_quota[2]};
+    publish_stats(g, s_q[3] != M_NONE, s_ssum, s_kr[0], s_kr[1], ccount, quota);
+  }
   int mode[kGrp], need[kGrp];
 #pragma unroll
   for (int q = 0; q < kGrp; ++q) { mode[q] = s_q[q]; need[q] = s_q[kGrp + q]; }
@@ -675,84 +738,18 @@ __device__ __forceinline__ void select_thresholds(const FastArgs& g, uint32_t* h
   }
   K2_PROBE(3);
   if (t != 0) return;
-  // ---- the selection words (this workgroup's phase 3 reads them from LDS; the publishing workgroup
-  // also stores them for the fused quantization waves and the probe), then the statistics
+  // ---- the selection words (this workgroup's phase 3 reads them from LDS), then the statistics
   const double ssum = s_ssum;
   const double mean = ssum / (double)S;
   const uint64_t mb = __builtin_bit_cast(uint64_t, mean);
   for (int q = 0; q < kGrp; ++q) {
     const uint64_t w = kTag | ((uint64_t)(fallback ? 1 : 0) << 50) | ((uint64_t)mode[q] << 48) |
                        ((uint64_t)(cut[q] & 0xffff) << 32) | thr[q];
-    if (publish && !g.withhold) st_sc1(&g.L.head->sel[q], w);
     s_selw[q] = w;
   }
   const uint64_t m_lo = kTag | (mb & 0xffffffffu), m_hi = kTag | (mb >> 32);
   s_selw[4] = m_lo;
   s_selw[5] = m_hi;
-  if (!publish) return;
-  if (!g.withhold) {
-    st_sc1(&g.L.head->sel[4], m_lo);
-    st_sc1(&g.L.head->sel[5], m_hi);
-  }
-  // statistics known here; phase 3 adds the kept-token sums (stats zeroed before the launch)
-  const int64_t ccount[3] = {s_cc[0], s_cc[1], s_cc[2]};
-  const int64_t quota[3] = {s_quota[0], s_quota[1], s_quota[2]};
-  rtkv_layer_stats* hs = a.stats;
-  rtkv_batch_stats* bs = reinterpret_cast<rtkv_batch_stats*>(hs + 1);
-  for (int q = 0; q < 3; ++q) bs->class_count[q] = ccount[q];
-  bs->fallback = fallback ? 1 : 0;
-  hs->score_sum = ssum;
-  hs->score_min = key_score(s_kr[0]);
-  hs->score_max = key_score(s_kr[1]);
-  int flags = 0;
-  if (a.kv_dtype == RTKV_F16)
-    for (int q = 0; q < 3; ++q)
-      if (ccount[q] > 0 && a.p.bits[q] >= 16) flags |= RTKV_FLAG_F16_QMAX_OVERFLOW;
-  if (flags) atomicOr(&hs->error_flags, flags);  // a spin timeout may have been flagged already
-  hs->B = 1;
-  if (!fallback) {  // the kept counts are the quotas: final here (phase 3 adds only the score sums)
-    int64_t n = 0, units = 0, bytes = 0;
-    for (int q = 0; q < 3; ++q) {
-      bs->kept_class[q] = quota[q];
-      n += quota[q];
-      units += quota[q] * (int64_t)a.p.bits[q];
-      bytes += quota[q] * row_bytes(a, q);
-    }
-    bs->kept = n;
-    bs->cost_units = units;
-    bs->packed_bytes = bytes;
-    hs->max_kept = n;
-    hs->total_packed_bytes = bytes;
-  }
-  if (g.early) {  // host-mapped mirror for the caller's early return (rtkv_compress_layer_early)
-    rtkv_early_stats* e = g.early;
-    auto put64 = [](void* dst, uint64_t v) {
-      __hip_atomic_store(reinterpret_cast<uint64_t*>(dst), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    };
-    auto put32 = [](void* dst, uint32_t v) {
-      __hip_atomic_store(reinterpret_cast<uint32_t*>(dst), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    };
-    const bool complete = !fallback && !g.withhold;  // withheld: the host takes the synchronised statistics
-    put32(&e->complete, complete ? 1u : 0u);
-    if (complete) {
-      put64(&e->stats.max_kept, (uint64_t)bs->kept);
-      put64(&e->stats.total_packed_bytes, (uint64_t)bs->packed_bytes);
-      put64(&e->stats.score_sum, __builtin_bit_cast(uint64_t, ssum));
-      put32(&e->stats.score_min, __builtin_bit_cast(uint32_t, hs->score_min));
-      put32(&e->stats.score_max, __builtin_bit_cast(uint32_t, hs->score_max));
-      put32(&e->stats.error_flags, (uint32_t)(flags | ld_sc1(&hs->error_flags)));
-      put32(&e->stats.B, 1u);
-      for (int q = 0; q < 3; ++q) {
-        put64(&e->batch.class_count[q], (uint64_t)ccount[q]);
-        put64(&e->batch.kept_class[q], (uint64_t)quota[q]);
-      }
-      put64(&e->batch.kept, (uint64_t)bs->kept);
-      put64(&e->batch.cost_units, (uint64_t)bs->cost_units);
-      put64(&e->batch.packed_bytes, (uint64_t)bs->packed_bytes);
-      put32(&e->batch.fallback, 0u);
-    }
-    __hip_atomic_store(&e->seq, g.early_seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-  }
 }
 
 // ------------------------------------------------------------------------------------ phase 3
@@ -796,7 +793,7 @@ __device__ __forceinline__ void compact_phase(const FastArgs& g, float s, int l,
     if (lane == 0) { s_d[0][wid] = ks; s_d[1][wid] = m2; }
   }
   if (wid == 0) {
-    if (lane == 0) st_sc1(&g.L.head->agg[blk], kTag | to11(kept_tot, 3));
+    if (lane == 0 && !(g.withhold == 2 && blk == 0)) st_sc1(&g.L.head->agg[blk], kTag | to11(kept_tot, 3));
     K2_WG(6);
     const uint64_t w0 = poll_tagged(&g.L.head->agg[0], 1, blk, g.spin_limit, a.stats);
     const uint64_t ps = wave_sum(lane < blk ? from11(w0 & ~kTag, 3) : 0ull);
@@ -819,10 +816,6 @@ __device__ __forceinline__ void compact_phase(const FastArgs& g, float s, int l,
         a.kept_index[row] = i;
         if (a.row_label) a.row_label[row] = (uint8_t)l;
         if (a.row_offset) a.row_offset[row] = k0 * rb[0] + k1 * rb[1] + k2 * rb[2];
-        if (g.fused) {  // the fused quantization waves of row `row` wait on it
-          st_sc1(&g.L.head->rowinfo[row][0], kTag | ((uint64_t)l << 32) | (uint32_t)i);
-          st_sc1(&g.L.head->rowinfo[row][1], kTag | ((uint64_t)k2 << 32) | ((uint64_t)k1 << 16) | (uint64_t)k0);
-        }
       }
     }
   }
@@ -865,7 +858,7 @@ inline FastArgs make_fast_args(const FinalizeArgs& f, void* ws) {
   g.f = f;
   g.early = f.early;
   g.early_seq = f.early_seq;
-  g.withhold = (f.p.flags & RTKV_TEST_WITHHOLD_SELECTION) ? 1 : 0;
+  g.withhold = (f.p.flags & RTKV_TEST_WITHHOLD_SELECTION) ? 1 : ((f.p.flags & RTKV_TEST_WITHHOLD_LOOKBACK) ? 2 : 0);
   static const uint32_t spin_limit = [] {  // RTKV_SPIN_LIMIT: polls per hand-off wait (default ≈ 2 s)
     const char* e = getenv("RTKV_SPIN_LIMIT");
     return e ? (uint32_t)strtoul(e, nullptr, 10) : (1u << 21);
@@ -900,7 +893,6 @@ inline FastArgs make_fast_args(const FinalizeArgs& f, void* ws) {
     for (int k = 0; k < 3; ++k) wmax = f.p.bits[k] > wmax ? f.p.bits[k] : wmax;
     g.hist_fb = (f.mode_select == 1 && !(f.p.flags & RTKV_NO_FALLBACK) && !(u8 >= (double)wmax)) ? 1 : 0;
   }
-  g.fused = 0;
   return g;
 }
 
@@ -1049,7 +1041,7 @@ __device__ __forceinline__ void k2_body(const FastArgs& g, uint32_t* hist_lds) {
   __syncthreads();
   // (RTKV_TEST_WITHHOLD_SELECTION: the last workgroup never reports ready, so every workgroup's phase-2
   // wait runs into its poll bound)
-  if (t == 0 && !(g.withhold && blk == G - 1)) st_sc1(&g.L.head->ready[blk], kTag);
+  if (t == 0 && !(g.withhold == 1 && blk == G - 1)) st_sc1(&g.L.head->ready[blk], kTag);
   // ---- phase 2 in EVERY workgroup (the same inputs, the same deterministic result): no selection hand-off
   // between workgroups; workgroup G−1 publishes the statistics and the early host mirror
 #ifdef RTKV_SELECT_PROBE

@@ -1,6 +1,6 @@
-// select_fast.hip — host side of the one-launch K2 (device code: select_fast.h) and of the fused
-// K2 + K4 launch (fused.h; per-dtype instantiations in fused_{f32,f16,bf16}.hip).
-#include "select_fast.h"
+// select_fast.hip — host side of the one-launch K2 (device code: select_fast.h, and select_one.h for
+// S <= 8192: the whole selection in one workgroup).
+#include "select_one.h"
 
 namespace rtkv {
 
@@ -40,6 +40,26 @@ template <int TPT, bool HAS_T2> static int launch_fsel_dt(const FastArgs& g, int
   }
 }
 
+template <int TPT, bool HAS_T2> static int launch_fsel1_dt(const FastArgs& g, hipStream_t st) {
+  switch (g.f.a_dtype) {
+    case RTKV_F16: hipLaunchKernelGGL((fsel1_kernel<TPT, HAS_T2, RTKV_F16>), dim3(1), dim3(kST), 0, st, g); break;
+    case RTKV_BF16: hipLaunchKernelGGL((fsel1_kernel<TPT, HAS_T2, RTKV_BF16>), dim3(1), dim3(kST), 0, st, g); break;
+    default: hipLaunchKernelGGL((fsel1_kernel<TPT, HAS_T2, RTKV_F32>), dim3(1), dim3(kST), 0, st, g); break;
+  }
+  RTKV_HIP_CHECK(hipGetLastError());
+  return RTKV_OK;
+}
+
+// The one-workgroup K2 (select_one.h) up to this many tokens; RTKV_K2_ONE_MAXS overrides (0: always the
+// multi-workgroup K2, for cross-checks and A/B timing).  The test-only withholding flags exercise the
+// multi-workgroup hand-offs and keep that kernel.
+static int64_t one_wg_max_s(const FinalizeArgs& f) {
+  if (f.p.flags & (RTKV_TEST_WITHHOLD_SELECTION | RTKV_TEST_WITHHOLD_LOOKBACK)) return 0;
+  const char* e = getenv("RTKV_K2_ONE_MAXS");
+  const int64_t v = e ? atoll(e) : kOneMaxS;
+  return v < kOneMaxS ? v : kOneMaxS;
+}
+
 int launch_select_fast(const FinalizeArgs& f, void* ws, bool zeroed, hipStream_t st) {
   RTKV_REQUIRE(select_fast_eligible(f), "select_fast: not eligible");
   FastArgs g = make_fast_args(f, ws);
@@ -47,51 +67,15 @@ int launch_select_fast(const FinalizeArgs& f, void* ws, bool zeroed, hipStream_t
     RTKV_HIP_CHECK(hipMemsetAsync(ws, 0, select_fast_zero_bytes(), st));
     RTKV_HIP_CHECK(hipMemsetAsync(f.stats, 0, rtkv_stats_bytes(f.B), st));
   }
+  if (f.S <= one_wg_max_s(f)) {
+    if (f.S <= 4 * kST) return f.T2 ? launch_fsel1_dt<4, true>(g, st) : launch_fsel1_dt<4, false>(g, st);
+    return f.T2 ? launch_fsel1_dt<8, true>(g, st) : launch_fsel1_dt<8, false>(g, st);
+  }
   // All G <= 32 workgroups (1024 threads, 64 KB of LDS: one per CU) are resident at once, which the
   // waits of phases 2 and 3 rely on; a busy GPU only delays the last ones.
   const int G = (int)((f.S + kST - 1) / kST);
   if (f.S <= 16 * kST) return f.T2 ? launch_fsel_dt<16, true>(g, G, st) : launch_fsel_dt<16, false>(g, G, st);
   return f.T2 ? launch_fsel_dt<32, true>(g, G, st) : launch_fsel_dt<32, false>(g, G, st);
-}
-
-// ------------------------------------------------------------------------------------ fused K2 + K4
-int launch_fused_f32(const FinalizeArgs& f, void* sel_ws, const QuantArgs& q, hipStream_t st);
-int launch_fused_f16(const FinalizeArgs& f, void* sel_ws, const QuantArgs& q, hipStream_t st);
-int launch_fused_bf16(const FinalizeArgs& f, void* sel_ws, const QuantArgs& q, hipStream_t st);
-
-bool fused_eligible(const FinalizeArgs& f, const QuantArgs& q) {
-  if (!(f.p.flags & RTKV_FUSED_QUANT) || !select_fast_eligible(f) || !f.T2 || !f.row_label) return false;
-  const rtkv_kv_desc& kv = q.kv;
-  if (kv.B != 1 || kv.S != f.S || q.S_glob != 0 || q.shard_ranges || q.kept_index != f.kept_index) return false;
-  const int64_t F = kv.H * kv.D;
-  if (F != f.F || !(F == 4096 || (F == 5120 && kv.dtype != RTKV_F32))) return false;
-  if (!(kv.dtype == f.a_dtype || f.a_dtype == RTKV_F32)) return false;
-  const int esz = kv.dtype == RTKV_F32 ? 4 : 2;
-  auto al16 = [](const void* p) { return p == nullptr || ((uintptr_t)p % 16) == 0; };
-  // contiguous rows: element e of a row at e (input and dequantized output), 16-byte aligned
-  if (!(kv.H == 1 || kv.stride_h == kv.D) || (kv.stride_s * esz) % 16 != 0 || !al16(kv.k_dev) || !al16(kv.v_dev))
-    return false;
-  if (q.out.k_out_dev && (!(kv.H == 1 || q.out.o_stride_h == kv.D) || (q.out.o_stride_s * esz) % 16 != 0 ||
-                          !al16(q.out.k_out_dev) || !al16(q.out.v_out_dev)))
-    return false;
-  if (q.out.packed_k_dev) {
-    if (!al16(q.out.packed_k_dev) || !al16(q.out.packed_v_dev) || !q.out.row_offset_dev) return false;
-    for (int g = 0; g < 3; ++g) {
-      const int w = field_width(kv.dtype, q.bits[g]);
-      if (!(w == 2 || w == 4 || w == 8 || w == 16)) return false;
-    }
-  }
-  return q.out.row_capacity >= f.S;
-}
-
-int launch_select_quant_fused(const FinalizeArgs& f, void* sel_ws, const QuantArgs& q, hipStream_t st) {
-  RTKV_REQUIRE(fused_eligible(f, q), "fused selection + quantization: not eligible");
-  switch (q.kv.dtype) {
-    case RTKV_F32: return launch_fused_f32(f, sel_ws, q, st);
-    case RTKV_F16: return launch_fused_f16(f, sel_ws, q, st);
-    case RTKV_BF16: return launch_fused_bf16(f, sel_ws, q, st);
-  }
-  RTKV_REQUIRE(false, "fused selection + quantization: bad dtype");
 }
 
 }  // namespace rtkv

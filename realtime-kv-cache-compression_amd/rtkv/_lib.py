@@ -18,9 +18,8 @@ LIB_PATH = os.environ.get("RTKV_LIB", os.path.join(ROOT, "librtkv.so"))
 
 F32, F16, BF16 = 0, 1, 2
 EMIT_DEQUANT, EMIT_PACKED, NO_SELECTION, NO_FALLBACK, SELECT_PIPELINE = 1, 2, 4, 8, 16
-FUSED_QUANT = 32
-TEST_WITHHOLD_SELECTION = 1 << 16
-FLAG_F16_QMAX_OVERFLOW, FLAG_SPIN_TIMEOUT = 1, 2
+TEST_WITHHOLD_SELECTION, TEST_WITHHOLD_LOOKBACK = 1 << 16, 1 << 17
+FLAG_F16_QMAX_OVERFLOW, FLAG_SPIN_TIMEOUT, FLAG_OUTPUT_OVERFLOW = 1, 2, 4
 ERR_NAMES = {-1: "RTKV_ERR_INVALID", -2: "RTKV_ERR_UNSUPPORTED", -3: "RTKV_ERR_HIP", -4: "RTKV_ERR_WORKSPACE",
              -5: "RTKV_ERR_TIMEOUT"}
 ERR_TIMEOUT = -5
@@ -76,7 +75,7 @@ class LayerOut(ctypes.Structure):
 class EarlyStats(ctypes.Structure):
     """rtkv_early_stats: the layer statistics the device publishes to host memory (B = 1)."""
     _fields_ = [("seq", ctypes.c_uint64), ("complete", c_i32), ("reserved", c_i32), ("stats", LayerStatsHeader),
-                ("batch", BatchStats)]
+                ("batch", BatchStats), ("final_seq", ctypes.c_uint64), ("final_flags", c_i32), ("reserved2", c_i32)]
 
 
 def stats_bytes(B: int) -> int:
@@ -121,7 +120,8 @@ _SIGS = {
     "rtkv_wait_early": ([c_p, ctypes.c_uint64, c_i64], c_i32),
     "rtkv_compress_layer_begin": ([c_p, c_p, c_p, c_p, c_p, c_sz, c_p, c_p, ctypes.c_uint64, c_p], c_i32),
     "rtkv_compress_layer_qk_begin": ([c_p, c_p, c_p, c_p, c_p, c_sz, c_p, c_p, ctypes.c_uint64, c_p], c_i32),
-    "rtkv_compress_layer_finish": ([c_p, c_p, c_p, c_p, c_sz, c_p], c_i32),
+    "rtkv_compress_layer_finish": ([c_p, c_p, c_p, c_i64, c_p, c_sz, c_p, c_p, ctypes.c_uint64], c_i32),
+    "rtkv_mask_key_padding": ([c_p, c_i32, c_i64, c_i64, c_i64, c_i64, c_i64, c_f, c_p, c_i64, c_p, c_p], c_i32),
     "rtkv_host_alloc": ([c_sz], c_p),
     "rtkv_host_free": ([c_p], None),
     "rtkv_comm_unique_id": ([c_p, c_sz], c_i32),

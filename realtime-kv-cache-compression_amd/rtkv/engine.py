@@ -122,6 +122,17 @@ def qk_desc(Q: torch.Tensor, K: torch.Tensor, lse: torch.Tensor, scale: Optional
     return d
 
 
+def check_flags(flags: int, what: str = "compress_layer"):
+    """Raise for the RTKV_FLAG_* bits that make a layer's outputs invalid."""
+    if flags & L.FLAG_SPIN_TIMEOUT:
+        raise RuntimeError(f"rtkv: {what} failed (RTKV_ERR_TIMEOUT): a cross-workgroup hand-off of the selection "
+                           "kernel did not arrive within its poll bound; the layer's outputs are invalid (NaN rows, "
+                           "RTKV_FLAG_SPIN_TIMEOUT)")
+    if flags & L.FLAG_OUTPUT_OVERFLOW:
+        raise RuntimeError(f"rtkv: {what} failed: the output buffers are smaller than the layer's published sizes; "
+                           "nothing was written (RTKV_FLAG_OUTPUT_OVERFLOW)")
+
+
 @dataclass
 class LayerStats:
     max_kept: int
@@ -178,6 +189,14 @@ class EarlyStatsBuffer:
     def _read(self) -> L.EarlyStats:
         return L.EarlyStats.from_buffer_copy(self._view)
 
+    def final_flags(self, seq: int) -> Optional[int]:
+        """The final RTKV_FLAG_* word K4 published for call `seq` (rtkv_compress_layer_finish), or None
+        while that K4 has not started (or a later layer's K4 has overwritten it)."""
+        e = self._view
+        if ctypes.c_uint64.from_address(ctypes.addressof(e) + L.EarlyStats.final_seq.offset).value != seq:
+            return None
+        return int(e.final_flags)
+
     def wait(self, seq: int, device=None) -> L.EarlyStats:
         """The statistics of call `seq` once the device has published them.  A queue slower than the
         spin timeout (a long backlog, preemption) is not an error: the device that runs the layer is
@@ -198,14 +217,22 @@ class EarlyStatsBuffer:
 
 
 class Workspace:
-    """Caller-owned scratch for the C ABI, grown on demand (one per device)."""
+    """Caller-owned scratch for the C ABI, grown on demand (one per device).
+
+    Between compress_layer_begin and PendingLayer.finish the workspace belongs to the pending layer
+    (K2 leaves the kept rows' classes and the selection scratch there for K4): ``get`` refuses to hand
+    it out meanwhile (include/rtkv.h, rtkv_compress_layer_begin)."""
 
     def __init__(self, device):
         self.device = torch.device(device)
         self.buf = torch.empty(0, dtype=torch.uint8, device=self.device)
+        self.pending = None  # the PendingLayer that owns the workspace until its finish()
 
     def get(self, B: int, S: int, H: Optional[int] = None) -> torch.Tensor:
         """H: query heads of the fused importance mode (room for the head-major K1' scratch)."""
+        if self.pending is not None:
+            raise RuntimeError("rtkv: the workspace belongs to a layer begun with compress_layer_begin whose "
+                               "finish() has not run; finish it (or use another Workspace) first")
         need = int(L.lib().rtkv_workspace_size(B, S) if H is None else L.lib().rtkv_workspace_size_qk(B, H, S))
         if self.buf.numel() < need:
             self.buf = torch.empty(need, dtype=torch.uint8, device=self.device)
@@ -310,10 +337,7 @@ class LayerResult:
 
     @staticmethod
     def _checked(st: LayerStats) -> LayerStats:
-        if st.error_flags & L.FLAG_SPIN_TIMEOUT:
-            raise RuntimeError("rtkv: compress_layer failed (RTKV_ERR_TIMEOUT): a cross-workgroup hand-off of the "
-                               "selection kernel did not arrive within its poll bound; the layer's outputs are "
-                               "invalid (RTKV_FLAG_SPIN_TIMEOUT)")
+        check_flags(st.error_flags)
         return st
 
     def stats(self) -> LayerStats:
@@ -424,33 +448,78 @@ class PendingLayer(LayerResult):
     """A layer whose K1 and K2 are enqueued (rtkv_compress_layer_begin): stats() gives S' and the packed
     byte count (early publication, or a stream sync); finish() enqueues K4 into exactly-sized buffers."""
 
-    def __init__(self, bufs: LayerBuffers, kd: L.KVDesc, params: L.LayerParams, workspace: torch.Tensor, stream: int,
+    def __init__(self, bufs: LayerBuffers, kd: L.KVDesc, params: L.LayerParams, workspace: "Workspace", stream: int,
                  early: Optional[EarlyStatsBuffer], seq: int, out: L.LayerOut):
         super().__init__(bufs, kd.B, early, seq, stream=stream)
-        self._kd, self._params, self._ws, self._stream, self._out = kd, params, workspace, stream, out
+        self._kd, self._params, self._wso, self._stream, self._out = kd, params, workspace, stream, out
+        self._ws = workspace.buf
         self.k_out = self.v_out = self.packed_k = self.packed_v = None
+        workspace.pending = self
+        self.finished = False
+        self._raw = None    # the early publication as the device wrote it (converted lazily by stats())
+        self._sizes = None
+
+    def sizes(self):
+        """(S'_max, packed bytes per code plane, error flags) for the output allocation: straight from the
+        early publication (no conversion on this path: the device runs only K2's tail meanwhile), else
+        from the synchronised statistics."""
+        if self._sizes is None:
+            if self._early is not None and self._stats is None:
+                e = self._early.wait(self._seq, self.bufs.device)
+                if e.complete:
+                    self._raw = e
+                    self._sizes = (e.stats.max_kept, e.stats.total_packed_bytes, e.stats.error_flags)
+                    return self._sizes
+            st = self.stats()
+            self._sizes = (st.max_kept, st.total_packed_bytes, st.error_flags)
+        return self._sizes
+
+    def stats(self) -> LayerStats:
+        if self._stats is None and self._raw is not None:
+            self._stats = self._checked(_early_to_stats(self._raw))
+        return super().stats()
+
+    def final_flags(self) -> Optional[int]:
+        """The layer's complete RTKV_FLAG_* word as K4 published it (no stream sync), or None when it is
+        not (yet) available: no early buffer, K4 not started, or overwritten by a later layer's K4."""
+        return self._early.final_flags(self._seq) if self._early is not None and self.finished else None
 
     def finish(self) -> "PendingLayer":
         """Allocate K'/V' [B, S', F] and the packed codes at their exact sizes and enqueue K4 into them.
         Between the early statistics and this launch the device only runs K2's tail, so this path is
         kept short: one allocation for K'+V', one for both code planes, the begin call's LayerOut patched."""
-        st = self.stats()
+        Sp, pb, flags = self.sizes()
+        check_flags(flags)
         b = self.bufs
-        dev, Sp, pb = b.device, st.max_kept, st.total_packed_bytes
+        dev = b.device
         out = self._out
         if b.emit_dequant:
-            kv = torch.empty(2, self.B, Sp, b.F, dtype=b.dtype, device=dev)
-            self.k_out, self.v_out = kv[0], kv[1]
-            out.k_out_dev, out.v_out_dev = self.k_out.data_ptr(), self.v_out.data_ptr()
+            kv = torch.empty((2, self.B, Sp, b.F), dtype=b.dtype, device=dev)
+            kp = kv.data_ptr()
+            out.k_out_dev, out.v_out_dev = kp, kp + self.B * Sp * b.F * kv.element_size()
+            self._kv = kv
         if b.emit_packed:
             n = (max(pb, 1) + 255) // 256 * 256
-            codes = torch.empty(2, n, dtype=torch.uint8, device=dev)
-            self.packed_k, self.packed_v = codes[0], codes[1]
-            out.packed_k_dev, out.packed_v_dev = self.packed_k.data_ptr(), self.packed_v.data_ptr()
+            codes = torch.empty((2, n), dtype=torch.uint8, device=dev)
+            cp = codes.data_ptr()
+            out.packed_k_dev, out.packed_v_dev = cp, cp + n
             out.packed_capacity = n
-        L.check(L.lib().rtkv_compress_layer_finish(ctypes.byref(self._kd), ctypes.byref(self._params), ctypes.byref(out),
-                                                   self._ws.data_ptr(), self._ws.numel(), self._stream),
-                "rtkv_compress_layer_finish")
+            self._codes = codes
+        try:
+            L.check(L.lib().rtkv_compress_layer_finish(ctypes.byref(self._kd), ctypes.byref(self._params), ctypes.byref(out),
+                                                       max(Sp, 1), self._ws.data_ptr(), self._ws.numel(), self._stream,
+                                                       self._early.ptr if self._early is not None else None,
+                                                       self._seq),
+                    "rtkv_compress_layer_finish")
+        finally:
+            self._wso.pending = None
+        self.finished = True
+        if b.emit_dequant:  # views made after the launch: nothing but the allocation precedes it
+            self.k_out, self.v_out = self._kv[0], self._kv[1]
+            del self._kv
+        if b.emit_packed:
+            self.packed_k, self.packed_v = self._codes[0], self._codes[1]
+            del self._codes
         self.done.record(torch.cuda.ExternalStream(self._stream, device=dev)
                          if self._stream != torch.cuda.current_stream(dev).cuda_stream else torch.cuda.current_stream(dev))
         return self
@@ -482,5 +551,5 @@ def compress_layer_begin(K, V, W, params: L.LayerParams, bufs: LayerBuffers, wor
     seq, pub = (early.next_seq(), ctypes.c_int32(0)) if early is not None else (0, ctypes.c_int32(0))
     L.check(fn(ctypes.byref(kd), ctypes.byref(xd), ctypes.byref(params), ctypes.byref(out), ws.data_ptr(), ws.numel(),
                st, early.ptr if early is not None else None, seq, ctypes.byref(pub)), name)
-    return PendingLayer(bufs, kd, params, ws, st, early if pub.value else None, seq, out)
+    return PendingLayer(bufs, kd, params, workspace, st, early if pub.value else None, seq, out)
 

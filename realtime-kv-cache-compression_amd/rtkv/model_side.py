@@ -130,8 +130,12 @@ class CompressedPrefillAttention:
             elif mask.dtype != torch.bool:
                 # a query row the model's mask hides every key from (padding): the reference's softmax
                 # of equal logits is uniform, so its output is the mean of the values (SDPA kernels may
-                # return zeros for such rows)
-                blind = (mask <= torch.finfo(mask.dtype).min / 2).all(-1, keepdim=True)   # [B|1, 1, S, 1]
+                # return zeros for such rows).  Query i sees key j < n_keys iff j <= i and key j is valid
+                # (the validated mask): blind iff no valid key among the first min(i + 1, n_keys).
+                n_keys = keys.shape[2]
+                seen = valid_key[:, :n_keys].long().cumsum(-1)                       # [B, n_keys]
+                last = torch.arange(S, device=Q.device).clamp(max=n_keys - 1)
+                blind = (seen[:, last] == 0)[:, None, :, None]                      # [B, 1, S, 1]
                 out = torch.where(blind, vals.mean(dim=2, keepdim=True).to(out.dtype), out)
         return out, (ck, cv), info
 
@@ -139,24 +143,34 @@ class CompressedPrefillAttention:
 def split_attention_mask(attention_mask: torch.Tensor, B: int, S: int):
     """The model's additive mask [B or 1, 1, S, >=S] → (key_bias, valid_key): None, None for the plain
     causal mask; else the fp32 [B, S] key bias (0 real key, -inf padding key) and the bool [B, S]
-    key validity, when the mask is exactly causal ∧ key-padding.  Anything else raises ValueError."""
+    key validity, when the mask is exactly causal ∧ key-padding.  Anything else raises ValueError.
+
+    One pass of rtkv_mask_key_padding over the mask (no [B, S, S] temporaries) and one host sync: key
+    validity from the last query row (which sees every unpadded key), every entry checked against it."""
+    import ctypes
+    from . import _lib as L
     if attention_mask.dim() != 4 or attention_mask.shape[1] != 1 or attention_mask.shape[0] not in (1, B) \
             or attention_mask.shape[2] < S or attention_mask.shape[3] < S:
         raise ValueError(f"attention_mask must be [B, 1, S, S] (got {tuple(attention_mask.shape)})")
-    m = attention_mask[..., :S, :S]
-    if not m.dtype.is_floating_point:
-        raise ValueError("attention_mask must be the model's additive (floating-point) mask")
-    masked = m <= torch.finfo(m.dtype).min / 2
-    if not bool(((m == 0) | masked).all()):
-        raise ValueError("attention_mask entries must be 0 or <= finfo.min/2 (an additive causal + padding mask)")
-    visible = ~masked[:, 0]                                   # [B|1, S, S]
-    valid_key = visible[:, S - 1, :]                          # the last query sees every unpadded key
-    causal = torch.ones(S, S, dtype=torch.bool, device=m.device).tril()
-    if not bool(torch.equal(visible, causal[None] & valid_key[:, None, :])):
-        raise ValueError("attention_mask is not a causal mask with key padding (unsupported by the fused "
-                         "importance mode)")
-    valid_key = valid_key.expand(B, S)
-    if bool(valid_key.all()):
+    m = attention_mask
+    if m.dtype not in L.TORCH_DTYPE_CODE:
+        raise ValueError("attention_mask must be the model's additive float32/float16/bfloat16 mask")
+    L.require_device(m)
+    Bm = m.shape[0]
+    # finfo.min / 2 as the comparison `m <= finfo.min / 2` sees it: rounded to the mask's dtype
+    thr = float(torch.tensor(torch.finfo(m.dtype).min / 2, dtype=m.dtype).float())
+    valid = torch.empty(Bm, S, dtype=torch.uint8, device=m.device)
+    counts = torch.zeros(2, dtype=torch.int64, device=m.device)
+    L.check(L.lib().rtkv_mask_key_padding(m.data_ptr(), L.TORCH_DTYPE_CODE[m.dtype], Bm, S, m.stride(0), m.stride(2),
+                                          m.stride(3), ctypes.c_float(thr), valid.data_ptr(), S, counts.data_ptr(),
+                                          L.stream_ptr(m.device)), "rtkv_mask_key_padding")
+    bad, padded = (int(x) for x in counts.tolist())  # the one host sync
+    if bad:
+        raise ValueError("attention_mask is not a causal mask with key padding: every entry must be 0 or "
+                         "<= finfo.min/2, and 0 exactly where j <= i and key j is unpadded "
+                         f"({bad} entries are not); unsupported by the fused importance mode")
+    if padded == 0:
         return None, None
+    valid_key = valid.bool().expand(B, S).contiguous()
     bias = torch.zeros(B, S, dtype=torch.float32, device=m.device).masked_fill_(~valid_key, float("-inf"))
-    return bias.contiguous(), valid_key.contiguous()
+    return bias, valid_key

@@ -16,8 +16,8 @@ import torch
 
 from . import _lib as L
 from .dynamic_quantization import F16_OVERFLOW_MSG, DynamicPrecisionQuantizer
-from .engine import (EarlyStatsBuffer, LayerBuffers, Workspace, compress_layer_begin, params_from_config,
-                     prompt_length)
+from .engine import (EarlyStatsBuffer, LayerBuffers, Workspace, check_flags, compress_layer_begin,
+                     params_from_config, prompt_length)
 from .selective_propagation import SelectiveTokenPropagator
 from .token_importance import LayerWiseImportanceTracker
 
@@ -92,6 +92,11 @@ class RealTimePrefillCompressor:
         self.emit_packed = emit_packed
         self._workspaces: Dict[torch.device, Workspace] = {}
         self._early: Dict[torch.device, EarlyStatsBuffer] = {}
+        # per device: the last layer returned before its K4 ran, (PendingLayer, layer_idx); its final flags
+        # (a selection timeout raised after the early statistics, an output overflow) are checked at the
+        # next call on that device or by get_overall_compression_stats, without a stream sync
+        self._unverified: Dict[torch.device, tuple] = {}
+        self._test_flags = 0  # RTKV_TEST_* bits OR-ed into every layer's flags (tests only)
 
     # ------------------------------------------------------------------ reference API
     def identify_prompt_tokens(self, input_ids: torch.Tensor, special_tokens: Optional[List[int]] = None):
@@ -140,7 +145,7 @@ class RealTimePrefillCompressor:
         emit_packed = self.emit_packed and all(L.lib().rtkv_field_width(L.dtype_code(K), b) > 0 for b in bits)
         if K.dtype == torch.float16 and any((1 << b) - 1 > 65504 for b in bits):
             emit_packed = False
-        flags = L.EMIT_DEQUANT | (L.EMIT_PACKED if emit_packed else 0)
+        flags = L.EMIT_DEQUANT | (L.EMIT_PACKED if emit_packed else 0) | self._test_flags
         params = params_from_config(self.config, layer_idx, P, ratio, flags)
         # per-token buffers only: K'/V' and the packed codes are allocated at their exact sizes once S' is
         # known (rtkv_compress_layer_begin / _finish), so a layer retains 2·S'·F elements + its codes
@@ -151,8 +156,9 @@ class RealTimePrefillCompressor:
         early = self._early.get(K.device)
         if early is None:
             early = self._early[K.device] = EarlyStatsBuffer()
+        stream = torch.cuda.current_stream(K.device)  # the stream the layer's kernels run on
         t_start = torch.cuda.Event(enable_timing=True)
-        t_start.record()
+        t_start.record(stream)
         if fused:
             Q = query_states if query_states.stride(-1) == 1 else query_states.contiguous()
             res = compress_layer_begin(K, V, None, params, bufs, ws, early, Q=Q, lse=attention_lse.contiguous(),
@@ -161,12 +167,20 @@ class RealTimePrefillCompressor:
             res = compress_layer_begin(K, V, W, params, bufs, ws, early)
         # the one host wait of the layer: the device publishes S' and the counts as soon as K2 has its
         # thresholds; the exactly-sized outputs are allocated then and K4 is enqueued into them
+        try:
+            flags = res.sizes()[2]  # the early publication's S', code bytes and flags (K2 still running)
+            self._verify_previous(K.device)  # the previous layer's K4 has run by now (stream order)
+            if flags & L.FLAG_F16_QMAX_OVERFLOW:
+                raise RuntimeError(F16_OVERFLOW_MSG)
+            res.finish()
+        finally:
+            if ws.pending is res:  # an error before finish(): the workspace is free again
+                ws.pending = None
         st = res.stats()
-        if st.error_flags & L.FLAG_F16_QMAX_OVERFLOW:
-            raise RuntimeError(F16_OVERFLOW_MSG)
-        res.finish()
+        if res._early is not None:
+            self._unverified[K.device] = (res, layer_idx)
         t_end = torch.cuda.Event(enable_timing=True)
-        t_end.record()
+        t_end.record(stream)
         selected_keys, selected_values = res.kv()
         Sp = st.max_kept
         scores = bufs.scores
@@ -196,8 +210,11 @@ class RealTimePrefillCompressor:
             m2 = res.final_stats().score_m2
             return (m2 / (n - 1)) ** 0.5 if n > 1 else float("nan")
         host_time = time.time() - start_time
-        # processing_time: the layer's device time, K1 start to K4 end (HIP events on the stream; read,
-        # with its wait, on first access).  host_return_time: when this call returned (K4 still running).
+        # processing_time: the layer's device time, K1 start to K4 end (HIP events on the layer's stream;
+        # read, with its wait, on first access).  The reference's is the host wall time of its synchronous
+        # call (unified_compressor.py:118,148), which on the device path is exactly that span plus its
+        # Python overhead; the device span is what this call costs the caller's stream.  host_return_time:
+        # when this call returned (K4 still running).
         compression_info = _LazyDict({
             "layer_idx": layer_idx,
             "processing_time": _Lazy(lambda: t_start.elapsed_time(_synced(t_end)) / 1e3),
@@ -229,8 +246,29 @@ class RealTimePrefillCompressor:
         self.layer_states[layer_idx] = compression_info
         return selected_keys, selected_values, compression_info
 
+    def _verify_previous(self, device):
+        """Raise if the last layer returned on `device` turned out invalid after it was returned: a
+        selection hand-off that timed out after the early statistics (its K'/V' are NaN rows) or
+        buffers smaller than its sizes.  Reads the flags K4 published to the host mirror; waits for that
+        layer only if its K4 has not published them yet."""
+        prev = self._unverified.pop(device, None)
+        if prev is None:
+            return
+        res, layer_idx = prev
+        flags = res.final_flags()
+        if flags is None:  # its K4 has not started (another stream): wait for the layer
+            res.done.synchronize()
+            flags = res.final_flags()
+            if flags is None:
+                flags = res.final_stats().error_flags
+        if flags & (L.FLAG_SPIN_TIMEOUT | L.FLAG_OUTPUT_OVERFLOW):
+            self.layer_states.pop(layer_idx, None)
+            check_flags(flags, f"compress_layer_kv_cache (layer {layer_idx}, returned before its K4 ran)")
+
     def get_overall_compression_stats(self) -> Dict:
         """Aggregate of every processed layer (unified_compressor.py:174-230)."""
+        for device in list(self._unverified):
+            self._verify_previous(device)
         if not self.layer_states:
             return {}
         states = list(self.layer_states.values())
@@ -266,6 +304,7 @@ class RealTimePrefillCompressor:
     def reset_compression_state(self):
         self.layer_states = {}
         self.importance_tracker.layer_scores = {}
+        self._unverified = {}
 
     def estimate_memory_usage(self) -> Dict[str, float]:
         try:

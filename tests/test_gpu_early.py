@@ -146,3 +146,109 @@ def test_withheld_selection_times_out_instead_of_hanging():
         good = rtkv.LayerBuffers(1, S, F, Kd.dtype, "cuda", (2, 4, 8))
         st = rtkv.compress_layer(Kd, Vd, Wd, ok, good, ws, early=early).final_stats()
         assert st.error_flags == 0 and 0 < st.max_kept < S
+
+
+def _lookback_inputs():
+    import rtkv
+    S, H, D, dtype = 4096, 8, 64, "float16"
+    F, P = H * D, rtkv.prompt_length(S)
+    K, V = synth.kv(6, 1, S, F, dtype)
+    W = synth.attention_slice(6, 1, H, S, P, dtype)
+    cfg = rtkv.CompressionConfig(alpha=0.8, beta=0.1, gamma=0.1, theta_h=0.4, theta_m=0.25, num_hidden_layers=4,
+                                 high_precision_bits=8, medium_precision_bits=4, low_precision_bits=2)
+    return S, F, P, cfg, _dev(K, dtype), _dev(V, dtype), _dev(W, dtype)
+
+
+def test_lookback_timeout_after_the_early_publication_is_caught():
+    """A hand-off that fails AFTER the early statistics are out (RTKV_TEST_WITHHOLD_LOOKBACK: workgroup 0
+    never publishes its phase-3 counts): the early statistics are complete and clean, K4 then finds
+    RTKV_FLAG_SPIN_TIMEOUT, writes NaN rows instead of codes and publishes the flag in the host mirror
+    (final_flags), and the layer's final statistics raise RTKV_ERR_TIMEOUT."""
+    import rtkv
+    from rtkv import _lib as L
+    from rtkv.engine import EarlyStatsBuffer, compress_layer_begin
+    S, F, P, cfg, Kd, Vd, Wd = _lookback_inputs()
+    p = rtkv.params_from_config(cfg, 0, P, 0.6, L.EMIT_DEQUANT | L.EMIT_PACKED | L.TEST_WITHHOLD_LOOKBACK)
+    ws, early = rtkv.Workspace("cuda"), EarlyStatsBuffer()
+    bufs = rtkv.LayerBuffers(1, S, F, Kd.dtype, "cuda", (2, 4, 8), outputs=False)
+    res = compress_layer_begin(Kd, Vd, Wd, p, bufs, ws, early)
+    with pytest.raises(RuntimeError, match=r"finish\(\) has not run"):
+        ws.get(1, S)  # the workspace belongs to the pending layer
+    st = res.stats()  # the early publication: complete, no flag yet
+    assert res._early is not None and st.error_flags == 0 and 0 < st.max_kept < S
+    res.finish()
+    torch.cuda.synchronize()
+    assert ws.pending is None
+    assert res.final_flags() & L.FLAG_SPIN_TIMEOUT
+    k, v = res.kv()
+    assert torch.isnan(k.float()).all() and torch.isnan(v.float()).all()
+    with pytest.raises(RuntimeError, match="RTKV_ERR_TIMEOUT"):
+        res.final_stats()
+
+
+def test_drop_in_reports_a_late_timeout_at_the_next_call():
+    """The drop-in returns on the early statistics; a layer whose selection failed after them is
+    reported by the next call on the device (and by get_overall_compression_stats) from K4's host
+    flags, without a stream sync per layer, and the layer is dropped from layer_states.  The layers
+    after it are unaffected."""
+    import rtkv
+    S, F, P, cfg, Kd, Vd, Wd = _lookback_inputs()
+    ids = torch.zeros(1, S, dtype=torch.long, device="cuda")
+    from rtkv import _lib as L
+    comp = rtkv.RealTimePrefillCompressor(cfg)
+    k0, v0, _ = comp.compress_layer_kv_cache(Kd, Vd, Wd, ids, 0)  # good layer
+    comp._test_flags = L.TEST_WITHHOLD_LOOKBACK
+    k1, v1, _ = comp.compress_layer_kv_cache(Kd, Vd, Wd, ids, 1)  # returns on its (clean) early statistics
+    comp._test_flags = 0
+    with pytest.raises(RuntimeError, match="layer 1"):
+        comp.compress_layer_kv_cache(Kd, Vd, Wd, ids, 2)
+    torch.cuda.synchronize()
+    assert torch.isnan(k1.float()).all()
+    k3, v3, _ = comp.compress_layer_kv_cache(Kd, Vd, Wd, ids, 3)
+    torch.cuda.synchronize()
+    ref = rtkv.RealTimePrefillCompressor(cfg)
+    r3, _, _ = ref.compress_layer_kv_cache(Kd, Vd, Wd, ids, 3)
+    assert torch.equal(k3.view(torch.int16), r3.view(torch.int16))
+    assert sorted(comp.layer_states) == [0, 3]
+    assert comp.get_overall_compression_stats()["total_layers_processed"] == 2
+    # the same through get_overall_compression_stats when the failing layer is the last one
+    comp._test_flags = L.TEST_WITHHOLD_LOOKBACK
+    comp.compress_layer_kv_cache(Kd, Vd, Wd, ids, 2)
+    comp._test_flags = 0
+    with pytest.raises(RuntimeError, match="layer 2"):
+        comp.get_overall_compression_stats()
+
+
+def test_finish_with_undersized_outputs_writes_nothing():
+    """rtkv_compress_layer_finish with buffers smaller than the layer's published sizes (out_rows below
+    S'_max, or packed_capacity below the code bytes): K4 writes nothing, flags
+    RTKV_FLAG_OUTPUT_OVERFLOW in the statistics and in the host mirror."""
+    import ctypes
+    import rtkv
+    from rtkv import _lib as L
+    from rtkv.engine import EarlyStatsBuffer, compress_layer_begin
+    S, F, P, cfg, Kd, Vd, Wd = _lookback_inputs()
+    p = rtkv.params_from_config(cfg, 0, P, 0.6, L.EMIT_DEQUANT | L.EMIT_PACKED)
+    for short in ("rows", "bytes"):
+        ws, early = rtkv.Workspace("cuda"), EarlyStatsBuffer()
+        bufs = rtkv.LayerBuffers(1, S, F, Kd.dtype, "cuda", (2, 4, 8), outputs=False)
+        res = compress_layer_begin(Kd, Vd, Wd, p, bufs, ws, early)
+        st = res.stats()
+        n, nb = st.max_kept, st.total_packed_bytes
+        rows = n - 1 if short == "rows" else n
+        cap = nb if short == "rows" else nb - 1
+        kv = torch.full((2, 1, n, F), 7.0, dtype=Kd.dtype, device="cuda")  # room for n rows, declared `rows`
+        codes = torch.full((2, nb + 256), 0xAB, dtype=torch.uint8, device="cuda")
+        out = res._out
+        out.k_out_dev, out.v_out_dev = kv[0].data_ptr(), kv[1].data_ptr()
+        out.packed_k_dev, out.packed_v_dev = codes[0].data_ptr(), codes[1].data_ptr()
+        out.packed_capacity = cap
+        L.check(L.lib().rtkv_compress_layer_finish(ctypes.byref(res._kd), ctypes.byref(p), ctypes.byref(out), rows,
+                                                   ws.buf.data_ptr(), ws.buf.numel(), L.stream_ptr(Kd.device),
+                                                   early.ptr, res._seq), "finish")
+        ws.pending = None
+        torch.cuda.synchronize()
+        assert early.final_flags(res._seq) & L.FLAG_OUTPUT_OVERFLOW
+        assert bool((kv == 7.0).all()) and bool((codes == 0xAB).all())
+        with pytest.raises(RuntimeError, match="RTKV_FLAG_OUTPUT_OVERFLOW"):
+            res.final_stats()

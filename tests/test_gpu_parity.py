@@ -113,6 +113,26 @@ def test_fp32_register_aggregation_matches_lds_path_and_oracle(B, H, S, monkeypa
     assert np.array_equal(reg, orc.attention_aggregation(W, 0, P))
 
 
+@pytest.mark.parametrize("B,H,S,dtype", [(1, 32, 16384, "float16"), (2, 40, 3001, "bfloat16"), (1, 40, 4096, "float16"),
+                                          (1, 32, 4096, "bfloat16"), (2, 32, 77, "float16")])
+def test_split_head_aggregation_matches_unsplit_and_oracle(B, H, S, dtype, monkeypatch):
+    """fp16/bf16, P = 128, H = 32 or 40: K1's split-head kernel (the workgroup's halves stream the two
+    halves of the head range, half 1 hands its block sums over through LDS) == the unsplit kernel
+    (RTKV_K1_NOSPLIT) == the oracle, bit for bit; ragged token blocks and the 13B head tail (40 = 2·16 + 8)
+    included."""
+    import rtkv
+    P = 128
+    W = synth.attention_slice(950 + S + H, B, H, S, P, dtype)
+    Wd = dev(W, dtype)
+    sc = rtkv.PromptGuidedImportanceScorer(config(COVERAGE, 4))
+    idx = torch.arange(P, device="cuda")
+    split = host(sc.compute_attention_aggregation(Wd, idx, 0).float())
+    monkeypatch.setenv("RTKV_K1_NOSPLIT", "1")
+    whole = host(sc.compute_attention_aggregation(Wd, idx, 0).float())
+    assert np.array_equal(split.view(np.uint32), whole.view(np.uint32))
+    assert np.array_equal(split, orc.attention_aggregation(W, synth.DTYPES[dtype], P))
+
+
 @pytest.mark.parametrize("case", by_kind("normalize"), ids=lambda c: c["name"])
 def test_normalize_edges(case):
     import rtkv

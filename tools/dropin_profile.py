@@ -27,6 +27,7 @@ def main():
     ap.add_argument("--dtype", default="float32")
     ap.add_argument("--layers", type=int, default=8)
     ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--no-cprofile", action="store_true", help="timings only (under a kernel trace)")
     a = ap.parse_args()
     sys.argv = ["bench.py", "--dtype", a.dtype, "--layers", str(a.layers)]
     args = bench.parse()
@@ -51,6 +52,8 @@ def main():
     raw_ms, kus = job.timed(a.reps, 2)
     print(f"drop-in {drop:.1f} us/layer; raw driver {raw_ms / args.layers * 1e3:.1f} us/layer "
           f"(K1 {kus[0]:.1f} K2 {kus[1]:.1f} K4 {kus[2]:.1f})", flush=True)
+    if a.no_cprofile:
+        return
     pr = cProfile.Profile()
     pr.enable()
     for _ in range(a.reps):
