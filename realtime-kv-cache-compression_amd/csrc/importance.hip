@@ -659,9 +659,11 @@ static int launch_agg_dt(const rtkv_attn_desc& w, int P, float* A, hipStream_t s
         const int v = e ? atoi(e) : 0;
         return v == 256 || v == 512 || v == 1024 ? v : 0;
       }();
-      if ((H == 32 || H == 40) && !getenv("RTKV_K1_NOSPLIT")) {
-        // Llama-2-7B / 13B heads: the head range in two halves per workgroup, twice the waves per CU
-        // (RTKV_K1_NOSPLIT: the unsplit kernel, for cross-checks)
+      if ((H == 32 || H == 40) && w.S * w.B < 16384 && !getenv("RTKV_K1_NOSPLIT")) {
+        // Llama-2-7B / 13B heads, short prompts: the head range in two halves per workgroup, twice the
+        // waves per CU (S = 4096 f16: 14.3 against 17.6 us; at S = 16384, where the unsplit grid already
+        // gives every CU a workgroup, the split measured slower: 31.0 against 27.8 us, r04b).
+        // RTKV_K1_NOSPLIT: the unsplit kernel, for cross-checks.
         dim3 grid((unsigned)((w.S + 31) / 32), (unsigned)w.B);
         if (x.nparts) *x.nparts = (int)grid.x;
         if (H == 32)

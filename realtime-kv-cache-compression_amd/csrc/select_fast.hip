@@ -1,6 +1,5 @@
-// select_fast.hip — host side of the one-launch K2 (device code: select_fast.h, and select_one.h for
-// S <= 8192: the whole selection in one workgroup).
-#include "select_one.h"
+// select_fast.hip — host side of the one-launch K2 (device code: select_fast.h).
+#include "select_fast.h"
 
 namespace rtkv {
 
@@ -40,36 +39,12 @@ template <int TPT, bool HAS_T2> static int launch_fsel_dt(const FastArgs& g, int
   }
 }
 
-template <int TPT, bool HAS_T2> static int launch_fsel1_dt(const FastArgs& g, hipStream_t st) {
-  switch (g.f.a_dtype) {
-    case RTKV_F16: hipLaunchKernelGGL((fsel1_kernel<TPT, HAS_T2, RTKV_F16>), dim3(1), dim3(kST), 0, st, g); break;
-    case RTKV_BF16: hipLaunchKernelGGL((fsel1_kernel<TPT, HAS_T2, RTKV_BF16>), dim3(1), dim3(kST), 0, st, g); break;
-    default: hipLaunchKernelGGL((fsel1_kernel<TPT, HAS_T2, RTKV_F32>), dim3(1), dim3(kST), 0, st, g); break;
-  }
-  RTKV_HIP_CHECK(hipGetLastError());
-  return RTKV_OK;
-}
-
-// The one-workgroup K2 (select_one.h) up to this many tokens; RTKV_K2_ONE_MAXS overrides (0: always the
-// multi-workgroup K2, for cross-checks and A/B timing).  The test-only withholding flags exercise the
-// multi-workgroup hand-offs and keep that kernel.
-static int64_t one_wg_max_s(const FinalizeArgs& f) {
-  if (f.p.flags & (RTKV_TEST_WITHHOLD_SELECTION | RTKV_TEST_WITHHOLD_LOOKBACK)) return 0;
-  const char* e = getenv("RTKV_K2_ONE_MAXS");
-  const int64_t v = e ? atoll(e) : kOneMaxS;
-  return v < kOneMaxS ? v : kOneMaxS;
-}
-
 int launch_select_fast(const FinalizeArgs& f, void* ws, bool zeroed, hipStream_t st) {
   RTKV_REQUIRE(select_fast_eligible(f), "select_fast: not eligible");
   FastArgs g = make_fast_args(f, ws);
   if (!zeroed) {  // else K1 cleared them
     RTKV_HIP_CHECK(hipMemsetAsync(ws, 0, select_fast_zero_bytes(), st));
     RTKV_HIP_CHECK(hipMemsetAsync(f.stats, 0, rtkv_stats_bytes(f.B), st));
-  }
-  if (f.S <= one_wg_max_s(f)) {
-    if (f.S <= 4 * kST) return f.T2 ? launch_fsel1_dt<4, true>(g, st) : launch_fsel1_dt<4, false>(g, st);
-    return f.T2 ? launch_fsel1_dt<8, true>(g, st) : launch_fsel1_dt<8, false>(g, st);
   }
   // All G <= 32 workgroups (1024 threads, 64 KB of LDS: one per CU) are resident at once, which the
   // waits of phases 2 and 3 rely on; a busy GPU only delays the last ones.

@@ -187,43 +187,3 @@ def test_pipeline_with_adversarial_caller_inputs(B, S, ratio, monotone):
     assert m.shape == (B, S) and m.dtype == bool
     assert ks.shape[1] == pinfo["max_selected_length"]
 
-
-ONE_CASES = [c for c in CASES if c[0] <= 8192] + [
-    (1024, "float16", 0.6, {}, "rand"), (1025, "float32", 0.5, {}, "rand"), (8192, "bfloat16", 0.4, {}, "rand"),
-    (6000, "float16", 0.5, dict(beta=0.0), "tie"), (8192, "float32", 0.7, dict(beta=0.0), "const"),
-    (2048, "float16", 1.0, {}, "rand"),  # every class taken whole
-]
-
-
-@pytest.mark.parametrize("S,dtype,ratio,over,kind", ONE_CASES, ids=lambda v: str(v))
-def test_one_workgroup_matches_multi_workgroup(S, dtype, ratio, over, kind, monkeypatch):
-    """S <= 8192: the one-workgroup K2 (select_one.h: LDS radix select, no cross-workgroup hand-off)
-    against the multi-workgroup K2 (RTKV_K2_ONE_MAXS=0) byte for byte, statistics included."""
-    import rtkv
-    from rtkv import _lib as L
-    H, D = 2, 64
-    F = H * D
-    P = rtkv.prompt_length(S)
-    K, V = synth.kv(800 + S, 1, S, F, dtype)
-    if kind == "rand":
-        W = synth.attention_slice(800 + S, 1, H, S, P, dtype)
-    elif kind == "tie":
-        W = tied_attention(800 + S, H, S, P, dtype)
-    else:
-        W = synth.cast(np.full((1, H, S, P), 0.25, np.float32), dtype)
-    Kd, Vd, Wd = dev(K, dtype), dev(V, dtype), dev(W, dtype)
-    kw = dict(COV, **over)
-    base = L.EMIT_DEQUANT | L.EMIT_PACKED
-    a, sa = run(Kd, Vd, Wd, dtype, S, F, kw, 1, ratio, base)
-    monkeypatch.setenv("RTKV_K2_ONE_MAXS", "0")
-    b, sb = run(Kd, Vd, Wd, dtype, S, F, kw, 1, ratio, base)
-    for name in a:
-        assert torch.equal(a[name].view(torch.uint8) if a[name].dtype != torch.uint8 else a[name],
-                           b[name].view(torch.uint8) if b[name].dtype != torch.uint8 else b[name]), name
-    assert (sa.max_kept, sa.total_packed_bytes, sa.error_flags, sa.score_min, sa.score_max) == \
-        (sb.max_kept, sb.total_packed_bytes, sb.error_flags, sb.score_min, sb.score_max)
-    ra, rb = sa.batch[0], sb.batch[0]
-    for k in ("class_count", "kept", "kept_class", "cost_units", "packed_bytes", "fallback"):
-        assert ra[k] == rb[k], k
-    for x, y in ((sa.score_sum, sb.score_sum), (sa.score_m2, sb.score_m2), (ra["kept_score_sum"], rb["kept_score_sum"])):
-        assert abs(x - y) <= 1e-12 * max(1.0, abs(y))

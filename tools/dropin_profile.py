@@ -30,7 +30,7 @@ def main():
     ap.add_argument("--no-cprofile", action="store_true", help="timings only (under a kernel trace)")
     a = ap.parse_args()
     sys.argv = ["bench.py", "--dtype", a.dtype, "--layers", str(a.layers)]
-    args = bench.parse()
+    args = bench.resolve_config(bench.parse(), 1)
     dev = torch.device("cuda", 0)
     job = bench.Job(args, dev, 0, 1)
     comp = rtkv.RealTimePrefillCompressor(job.cfg)

@@ -20,6 +20,10 @@ for dt in float32 float16; do
   timeout -k 10 300 $B --seq 8192 --dtype $dt > gpurun_out/r04b_s8192_${dt}_one.json 2>/dev/null || exit $?
   RTKV_K2_ONE_MAXS=0 timeout -k 10 300 $B --seq 8192 --dtype $dt > gpurun_out/r04b_s8192_${dt}_multi.json 2>/dev/null || exit $?
 done
+RTKV_K2_ONE_MAXS=32768 timeout -k 10 300 $B > gpurun_out/r04b_f32_one16k.json 2>/dev/null || exit $?
+RTKV_K2_ONE_MAXS=32768 timeout -k 10 300 $B --dtype float16 > gpurun_out/r04b_f16_one16k.json 2>/dev/null || exit $?
+RTKV_K2_ONE_MAXS=32768 timeout -k 10 300 $B --seq 32768 --layers 8 > gpurun_out/r04b_s32k_one.json 2>/dev/null || exit $?
+timeout -k 10 300 $B --seq 32768 --layers 8 > gpurun_out/r04b_s32k_multi.json 2>/dev/null || exit $?
 timeout -k 10 400 python bench.py --steps 10 --warmup 3 --legs drop_in --cpu-baseline-seconds 0 > gpurun_out/r04b_dropin.json 2>/dev/null || exit $?
 bash tools/dropin_gaps.sh > gpurun_out/r04b_dropin_gaps.txt 2>&1 || exit $?
 timeout -k 10 300 python -u -m pytest -x -v --timeout 120 --timeout-method thread tests/test_gpu_decode.py -m gpu > gpurun_out/r04b_decode_tests.log 2>&1 || exit $?
