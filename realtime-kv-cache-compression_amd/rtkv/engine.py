@@ -242,9 +242,10 @@ class Workspace:
 class LayerBuffers:
     """Output buffers of one compressed layer, sized for B batch rows of S tokens (capacity = S).
 
-    Every buffer is a view into ONE device allocation (the drop-in path creates fresh buffers per
+    Every buffer is a slice of ONE device allocation (the drop-in path creates fresh buffers per
     layer call, as the reference returns fresh tensors; one allocation instead of ten keeps that
-    cheap).  Views are 256-byte aligned."""
+    cheap).  Slices are 256-byte aligned.  The kernels need only their addresses (``out_struct``), so
+    the tensor views (a few µs of host time each) are made on first access."""
 
     def __init__(self, B: int, S: int, F: int, dtype: torch.dtype, device, bits, emit_dequant=True, emit_packed=True,
                  outputs: bool = True):
@@ -254,63 +255,66 @@ class LayerBuffers:
         self.B, self.S, self.F, self.dtype = B, S, F, dtype
         self.emit_dequant, self.emit_packed = emit_dequant, emit_packed
         dev = self.device = torch.device(device)
-        esz = torch.tensor([], dtype=dtype).element_size()
+        esz = dtype.itemsize
         cap = 0
         if emit_packed and outputs:
             b3 = (ctypes.c_int32 * 3)(*bits)
             cap = int(L.lib().rtkv_packed_capacity(B, S, F, L.TORCH_DTYPE_CODE[dtype], b3))
-        plan = [("scores", B * S * 4), ("labels", B * S), ("mask", B * S), ("kept_index", B * S * 4),
-                ("stats", L.stats_bytes(B))]
+        plan = [("scores", B * S * 4, torch.float32, (B, S)), ("labels", B * S, torch.uint8, (B, S)),
+                ("mask", B * S, torch.uint8, (B, S)), ("kept_index", B * S * 4, torch.int32, (B, S)),
+                ("stats", L.stats_bytes(B), torch.uint8, (L.stats_bytes(B),))]
         if emit_dequant and outputs:
-            plan += [("k_out", B * S * F * esz), ("v_out", B * S * F * esz)]
+            plan += [("k_out", B * S * F * esz, dtype, (B * S * F,)), ("v_out", B * S * F * esz, dtype, (B * S * F,))]
         if emit_packed:
             if outputs:
-                plan += [("packed_k", max(cap, 1)), ("packed_v", max(cap, 1))]
-            plan += [("row_offset", B * S * 8), ("scale_zp", B * S * 16)]
+                plan += [("packed_k", max(cap, 1), torch.uint8, (max(cap, 1),)),
+                         ("packed_v", max(cap, 1), torch.uint8, (max(cap, 1),))]
+            plan += [("row_offset", B * S * 8, torch.int64, (B, S)), ("scale_zp", B * S * 16, torch.float32, (B, S, 4))]
         offs, total = {}, 0
-        for name, n in plan:
-            offs[name] = (total, n)
+        for name, n, dt, shape in plan:
+            offs[name] = (total, n, dt, shape)
             total += (n + 255) // 256 * 256
         self.arena = torch.empty(max(total, 1), dtype=torch.uint8, device=dev)
+        self._base = self.arena.data_ptr()
+        self._offs = offs
+        for name in ("k_out", "v_out", "packed_k", "packed_v", "row_offset", "scale_zp"):
+            if name not in offs:
+                setattr(self, name, None)
+        self.packed_capacity = cap if (emit_packed and outputs) else 0
 
-        def view(name, dt, shape):
-            o, n = offs[name]
-            return self.arena[o:o + n].view(dt).view(shape)
+    def __getattr__(self, name):
+        """The view of buffer `name`, made (and kept) on first access."""
+        offs = self.__dict__.get("_offs")
+        if offs is None or name not in offs:
+            raise AttributeError(name)
+        o, n, dt, shape = offs[name]
+        v = self.arena[o:o + n].view(dt).view(shape)
+        self.__dict__[name] = v
+        return v
 
-        self.scores = view("scores", torch.float32, (B, S))
-        self.labels = view("labels", torch.uint8, (B, S))
-        self.mask = view("mask", torch.uint8, (B, S))
-        self.kept_index = view("kept_index", torch.int32, (B, S))
-        self.stats = view("stats", torch.uint8, (L.stats_bytes(B),))
-        self.k_out = view("k_out", dtype, (B * S * F,)) if emit_dequant and outputs else None
-        self.v_out = view("v_out", dtype, (B * S * F,)) if emit_dequant and outputs else None
-        self.packed_k = self.packed_v = self.row_offset = self.scale_zp = None
-        self.packed_capacity = 0
-        if emit_packed:
-            if outputs:
-                self.packed_k = view("packed_k", torch.uint8, (max(cap, 1),))
-                self.packed_v = view("packed_v", torch.uint8, (max(cap, 1),))
-                self.packed_capacity = cap
-            self.row_offset = view("row_offset", torch.int64, (B, S))
-            self.scale_zp = view("scale_zp", torch.float32, (B, S, 4))
+    def ptr(self, name: str) -> int:
+        """Device address of buffer `name` (0 when absent), without making its view."""
+        o = self._offs.get(name)
+        return self._base + o[0] if o is not None else 0
 
     def matches(self, B, S, F, dtype, emit_dequant, emit_packed) -> bool:
         return (self.B, self.S, self.F, self.dtype) == (B, S, F, dtype) and \
-            (self.k_out is not None) == emit_dequant and (self.packed_k is not None) == emit_packed
+            ("k_out" in self._offs) == emit_dequant and ("packed_k" in self._offs) == emit_packed
 
     def out_struct(self, packed_batch_rows: bool = True) -> L.LayerOut:
         o = L.LayerOut()
-        o.k_out_dev, o.v_out_dev = L.ptr(self.k_out), L.ptr(self.v_out)
+        p = self.ptr
+        o.k_out_dev, o.v_out_dev = p("k_out"), p("v_out")
         # dequant rows packed back to back at the runtime row count: a contiguous [B, S', F] view
         o.o_stride_b = -1 if packed_batch_rows else self.S * self.F
         o.o_stride_s, o.o_stride_h = self.F, self.F
         o.row_capacity = self.S
-        o.scores_dev, o.labels_dev, o.mask_dev = L.ptr(self.scores), L.ptr(self.labels), L.ptr(self.mask)
-        o.kept_index_dev = L.ptr(self.kept_index)
-        o.packed_k_dev, o.packed_v_dev = L.ptr(self.packed_k), L.ptr(self.packed_v)
+        o.scores_dev, o.labels_dev, o.mask_dev = p("scores"), p("labels"), p("mask")
+        o.kept_index_dev = p("kept_index")
+        o.packed_k_dev, o.packed_v_dev = p("packed_k"), p("packed_v")
         o.packed_capacity = self.packed_capacity
-        o.row_offset_dev, o.scale_zp_dev = L.ptr(self.row_offset), L.ptr(self.scale_zp)
-        o.stats_dev = L.ptr(self.stats)
+        o.row_offset_dev, o.scale_zp_dev = p("row_offset"), p("scale_zp")
+        o.stats_dev = p("stats")
         return o
 
 
@@ -322,7 +326,7 @@ class LayerResult:
     kept_score_sum are NaN; ``final_stats()`` syncs the stream and reads them all."""
 
     def __init__(self, bufs: LayerBuffers, B: int, early: Optional[EarlyStatsBuffer] = None, seq: int = 0,
-                 stream: Optional[int] = None):
+                 stream: Optional[int] = None, record: bool = True):
         self.bufs = bufs
         self.B = B
         self._early, self._seq = early, seq
@@ -331,9 +335,13 @@ class LayerResult:
         # the layer's completion on the stream it was launched on: final_stats() waits for exactly that,
         # whatever stream is current when it is called
         self.done = torch.cuda.Event()
-        cur = torch.cuda.current_stream(bufs.device)
+        if record:
+            self._record(stream)
+
+    def _record(self, stream: Optional[int]):
+        cur = torch.cuda.current_stream(self.bufs.device)
         self.done.record(cur if stream is None or stream == cur.cuda_stream
-                         else torch.cuda.ExternalStream(stream, device=bufs.device))
+                         else torch.cuda.ExternalStream(stream, device=self.bufs.device))
 
     @staticmethod
     def _checked(st: LayerStats) -> LayerStats:
@@ -450,7 +458,8 @@ class PendingLayer(LayerResult):
 
     def __init__(self, bufs: LayerBuffers, kd: L.KVDesc, params: L.LayerParams, workspace: "Workspace", stream: int,
                  early: Optional[EarlyStatsBuffer], seq: int, out: L.LayerOut):
-        super().__init__(bufs, kd.B, early, seq, stream=stream)
+        # the completion event is recorded after K4 (finish()); until then final_stats() syncs the stream
+        super().__init__(bufs, kd.B, early, seq, stream=stream, record=False)
         self._kd, self._params, self._wso, self._stream, self._out = kd, params, workspace, stream, out
         self._ws = workspace.buf
         self.k_out = self.v_out = self.packed_k = self.packed_v = None
@@ -520,9 +529,13 @@ class PendingLayer(LayerResult):
         if b.emit_packed:
             self.packed_k, self.packed_v = self._codes[0], self._codes[1]
             del self._codes
-        self.done.record(torch.cuda.ExternalStream(self._stream, device=dev)
-                         if self._stream != torch.cuda.current_stream(dev).cuda_stream else torch.cuda.current_stream(dev))
+        self._record(self._stream)
         return self
+
+    def final_stats(self) -> LayerStats:
+        if not self.finished and self._final is None:  # no completion event yet: K1+K2 on the layer's stream
+            torch.cuda.ExternalStream(self._stream, device=self.bufs.device).synchronize()
+        return super().final_stats()
 
     def kv(self):
         return self.k_out, self.v_out

@@ -97,6 +97,7 @@ class RealTimePrefillCompressor:
         # next call on that device or by get_overall_compression_stats, without a stream sync
         self._unverified: Dict[torch.device, tuple] = {}
         self._test_flags = 0  # RTKV_TEST_* bits OR-ed into every layer's flags (tests only)
+        self._packable: Dict[tuple, bool] = {}  # (dtype, bits) → whether the packed codes are emitted
 
     # ------------------------------------------------------------------ reference API
     def identify_prompt_tokens(self, input_ids: torch.Tensor, special_tokens: Optional[List[int]] = None):
@@ -142,9 +143,12 @@ class RealTimePrefillCompressor:
         P = prompt_length(S)
         ratio = self.propagator.get_layer_propagation_ratio(layer_idx)
         bits = self._bits()
-        emit_packed = self.emit_packed and all(L.lib().rtkv_field_width(L.dtype_code(K), b) > 0 for b in bits)
-        if K.dtype == torch.float16 and any((1 << b) - 1 > 65504 for b in bits):
-            emit_packed = False
+        emit_packed = self._packable.get((K.dtype, bits, self.emit_packed))
+        if emit_packed is None:
+            emit_packed = self.emit_packed and all(L.lib().rtkv_field_width(L.dtype_code(K), b) > 0 for b in bits)
+            if K.dtype == torch.float16 and any((1 << b) - 1 > 65504 for b in bits):
+                emit_packed = False
+            self._packable[(K.dtype, bits, self.emit_packed)] = emit_packed
         flags = L.EMIT_DEQUANT | (L.EMIT_PACKED if emit_packed else 0) | self._test_flags
         params = params_from_config(self.config, layer_idx, P, ratio, flags)
         # per-token buffers only: K'/V' and the packed codes are allocated at their exact sizes once S' is
@@ -202,7 +206,8 @@ class RealTimePrefillCompressor:
                                 "bit_assignments": _Lazy(lambda labels=bufs.labels: labels.long().cpu().numpy())})
         # the score spread and the kept-score sums come from K2's second kernel: read on first access
         propagation_info = _LazyDict({"layer_idx": layer_idx, "propagation_ratio": ratio, "original_length": S,
-                                      "max_selected_length": Sp, "selection_mask": bufs.mask.view(torch.bool),
+                                      "max_selected_length": Sp,
+                                      "selection_mask": _Lazy(lambda: bufs.mask.view(torch.bool)),
                                       "selection_stats": _Lazy(lambda: self.propagator._selection_info(
                                           scores, res.final_stats(), ratio, S))})
 
@@ -230,18 +235,20 @@ class RealTimePrefillCompressor:
             "propagation_info": propagation_info,
         })
         if emit_packed:
-            compression_info["packed"] = {
-                "codes_k": res.packed_k[: st.total_packed_bytes],
-                "codes_v": res.packed_v[: st.total_packed_bytes],
-                "row_offset": bufs.row_offset[:, :Sp],
-                "scale_zp": bufs.scale_zp[:, :Sp],
-                "kept_index": bufs.kept_index[:, :Sp],
-                "labels": bufs.labels,
+            # views made on first access (each costs host time on the path between two layers)
+            pk, pv, nb = res.packed_k, res.packed_v, st.total_packed_bytes
+            compression_info["packed"] = _LazyDict({
+                "codes_k": _Lazy(lambda: pk[:nb]),
+                "codes_v": _Lazy(lambda: pv[:nb]),
+                "row_offset": _Lazy(lambda: bufs.row_offset[:, :Sp]),
+                "scale_zp": _Lazy(lambda: bufs.scale_zp[:, :Sp]),
+                "kept_index": _Lazy(lambda: bufs.kept_index[:, :Sp]),
+                "labels": _Lazy(lambda: bufs.labels),
                 "rows": [r["kept"] for r in st.batch],
                 "bits": bits,
                 "dtype": K.dtype,
                 "feature_dim": F,
-            }
+            })
         res.k_out = res.v_out = None  # the caller owns K'/V'; nothing kept here pins them
         self.layer_states[layer_idx] = compression_info
         return selected_keys, selected_values, compression_info

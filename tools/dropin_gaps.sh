@@ -5,7 +5,7 @@
 set -euo pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
-out=gpurun_out/dropin_gaps
+out=gpurun_out/dropin_gaps${DROPIN_OUT:+_$DROPIN_OUT}
 rm -rf "$out"; mkdir -p "$out"
 timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d "$out" -o trace -- python3 tools/dropin_profile.py \
   --layers 32 --reps 5 --no-cprofile ${DROPIN_ARGS:-} > "$out/run.log" 2>&1
