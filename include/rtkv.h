@@ -357,6 +357,12 @@ int rtkv_compress_layer_qk_begin(const rtkv_kv_desc* kv, const rtkv_qk_desc* q, 
 int rtkv_compress_layer_finish(const rtkv_kv_desc* kv, const rtkv_layer_params* p, const rtkv_layer_out* out,
                                int64_t out_rows, void* workspace_dev, size_t workspace_bytes, void* stream,
                                rtkv_early_stats* early_host, uint64_t seq);
+/* Between begin and finish (drop-in path, no reference counterpart): read the first kept rows of K
+ * and V — K4's first tasks — up to max_bytes in total, with the default cache policy, so that they are
+ * in the Infinity Cache when K4 starts.  Enqueue right after begin, on its stream: it runs while the
+ * host waits for the early statistics and allocates the outputs.  Loads only (no output); a no-op for
+ * B > 1 or rows that are not contiguous and 16-byte aligned. */
+int rtkv_prefetch_kept_rows(const rtkv_kv_desc* kv, const rtkv_layer_out* out, int64_t max_bytes, void* stream);
 /* Pinned, device-coherent host memory for rtkv_early_stats (hipHostMalloc, coherent + mapped). */
 void* rtkv_host_alloc(size_t bytes);
 void rtkv_host_free(void* p);

@@ -379,6 +379,11 @@ int rtkv_compress_layer_finish(const rtkv_kv_desc* kv, const rtkv_layer_params* 
   return launch_quant(q, (hipStream_t)stream);
 }
 
+int rtkv_prefetch_kept_rows(const rtkv_kv_desc* kv, const rtkv_layer_out* out, int64_t max_bytes, void* stream) {
+  RTKV_REQUIRE(out != nullptr, "null output descriptor");
+  return launch_prefetch_rows(kv, out->kept_index_dev, out->stats_dev, max_bytes, (hipStream_t)stream);
+}
+
 int rtkv_wait_early(const rtkv_early_stats* early_host, uint64_t seq, int64_t timeout_us) {
   RTKV_REQUIRE(early_host != nullptr, "null early-stats buffer");
   const auto t0 = std::chrono::steady_clock::now();

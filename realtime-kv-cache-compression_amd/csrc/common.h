@@ -279,6 +279,8 @@ int launch_quant(const QuantArgs& a, hipStream_t st);
 
 int launch_shard_ranges(const int32_t* kept_index, const int64_t* row_offset, const rtkv_layer_stats* stats, int64_t B,
                         int64_t cap, int64_t S_local, int nranks, int64_t* ranges, hipStream_t st);
+int launch_prefetch_rows(const rtkv_kv_desc* kv, const int32_t* kept_index, const rtkv_layer_stats* stats,
+                         int64_t max_bytes, hipStream_t st);
 int launch_gather(const void* src, int64_t B, int64_t S, int64_t row_bytes, const int32_t* kept_index, int64_t cap,
                   int64_t ssb, void* dst, int64_t dsb, int64_t sss, const rtkv_layer_stats* stats, hipStream_t st);
 int launch_unpack(const uint8_t* packed, const int64_t* row_offset, const float* scale_zp, int which,

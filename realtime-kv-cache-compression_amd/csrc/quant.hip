@@ -69,6 +69,52 @@ int launch_gather(const void* src, int64_t B, int64_t S, int64_t row_bytes, cons
   return RTKV_OK;
 }
 
+// ------------------------------------------------------------------------------------ prefetch
+// The first kept rows of K and V (K4's first tasks, in K4's task order) read with the default cache
+// policy and discarded, so that they sit in the Infinity Cache when K4 starts.  For the drop-in path:
+// between K2's early publication and the K4 launch the host allocates the outputs and the device idles
+// (~15-20 us per layer); this kernel, enqueued right after K2, uses that window.  Loads only.
+__global__ __launch_bounds__(256) void prefetch_rows_kernel(const uint8_t* __restrict__ k, const uint8_t* __restrict__ v,
+                                                            int64_t sss, int64_t row_bytes,
+                                                            const int32_t* __restrict__ kept_index, int64_t S,
+                                                            int64_t max_rows, const rtkv_layer_stats* __restrict__ stats) {
+  const int64_t kept = stats->max_kept < max_rows ? stats->max_kept : max_rows;
+  const int lane = threadIdx.x & 63;
+  const int64_t t = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  const int64_t r = t >> 1;
+  if (r >= kept) return;
+  const int64_t i = kept_index[r];
+  if (i < 0 || i >= S) return;
+  const uint8_t* src = ((t & 1) ? v : k) + i * sss;
+  uint32_t acc = 0;
+  for (int64_t o = (int64_t)lane * 16; o < row_bytes; o += 64 * 16) {
+    const uint4 x = *reinterpret_cast<const uint4*>(src + o);
+    acc ^= x.x ^ x.w;
+  }
+  asm volatile("" ::"v"(acc));  // keep the loads
+}
+
+int launch_prefetch_rows(const rtkv_kv_desc* kv, const int32_t* kept_index, const rtkv_layer_stats* stats,
+                         int64_t max_bytes, hipStream_t st) {
+  RTKV_REQUIRE(kv && kept_index && stats, "prefetch_kept_rows: null pointer");
+  const int esz = kv->dtype == RTKV_F32 ? 4 : 2;
+  const int64_t F = kv->H * kv->D;
+  const int64_t row_bytes = F * esz;
+  // one batch row with contiguous 16-byte aligned rows (every drop-in configuration); otherwise nothing
+  const bool ok = kv->B == 1 && (kv->H == 1 || kv->stride_h == kv->D) && (row_bytes % 16) == 0 &&
+                  ((kv->stride_s * esz) % 16) == 0 && (((uintptr_t)kv->k_dev | (uintptr_t)kv->v_dev) & 15) == 0;
+  if (!ok || max_bytes <= 0) return RTKV_OK;
+  int64_t rows = max_bytes / (2 * row_bytes);
+  if (rows > kv->S) rows = kv->S;
+  if (rows < 1) return RTKV_OK;
+  const int64_t blocks = (2 * rows + 3) / 4;
+  hipLaunchKernelGGL(prefetch_rows_kernel, dim3((unsigned)blocks), dim3(256), 0, st,
+                     static_cast<const uint8_t*>(kv->k_dev), static_cast<const uint8_t*>(kv->v_dev), kv->stride_s * esz,
+                     row_bytes, kept_index, kv->S, rows, stats);
+  RTKV_HIP_CHECK(hipGetLastError());
+  return RTKV_OK;
+}
+
 // ------------------------------------------------------------------------------------ shard ranges
 // ranges[b][j] = {first output row, first packed byte} of rank j's tokens [j*S_local, (j+1)*S_local)
 // (j = nranks: one past the last kept row of batch row b).  kept_index is ascending per batch row.

@@ -334,7 +334,7 @@ class LayerResult:
         self._final: Optional[LayerStats] = None
         # the layer's completion on the stream it was launched on: final_stats() waits for exactly that,
         # whatever stream is current when it is called
-        self.done = torch.cuda.Event()
+        self.done = torch.cuda.Event(enable_timing=True)  # also the end of the drop-in's processing_time
         if record:
             self._record(stream)
 
@@ -359,11 +359,15 @@ class LayerResult:
         return self._stats
 
     def final_stats(self) -> LayerStats:
+        return self._checked(self.final_stats_unchecked())
+
+    def final_stats_unchecked(self) -> LayerStats:
+        """The final statistics block (a stream sync), error flags included but not raised."""
         if self._final is None:
             self.done.synchronize()  # the layer's stream, not whichever stream is current here
             raw = self.bufs.stats.cpu().numpy().tobytes()
             self._final = decode_stats(raw, self.B)
-        return self._checked(self._final)
+        return self._final
 
     def kv(self):
         """Dequantized (K', V') as contiguous [B, S'_max, F] views (reference return value)."""
@@ -462,6 +466,10 @@ class PendingLayer(LayerResult):
         super().__init__(bufs, kd.B, early, seq, stream=stream, record=False)
         self._kd, self._params, self._wso, self._stream, self._out = kd, params, workspace, stream, out
         self._ws = workspace.buf
+        # finish()'s call, bound now: only out_rows is added after the publication
+        self._finish_args = (ctypes.byref(kd), ctypes.byref(params), ctypes.byref(out))
+        self._finish_tail = (self._ws.data_ptr(), self._ws.numel(), stream, early.ptr if early is not None else None,
+                             seq)
         self.k_out = self.v_out = self.packed_k = self.packed_v = None
         workspace.pending = self
         self.finished = False
@@ -515,10 +523,7 @@ class PendingLayer(LayerResult):
             out.packed_capacity = n
             self._codes = codes
         try:
-            L.check(L.lib().rtkv_compress_layer_finish(ctypes.byref(self._kd), ctypes.byref(self._params), ctypes.byref(out),
-                                                       max(Sp, 1), self._ws.data_ptr(), self._ws.numel(), self._stream,
-                                                       self._early.ptr if self._early is not None else None,
-                                                       self._seq),
+            L.check(L.lib().rtkv_compress_layer_finish(*self._finish_args, max(Sp, 1), *self._finish_tail),
                     "rtkv_compress_layer_finish")
         finally:
             self._wso.pending = None
@@ -532,10 +537,10 @@ class PendingLayer(LayerResult):
         self._record(self._stream)
         return self
 
-    def final_stats(self) -> LayerStats:
+    def final_stats_unchecked(self) -> LayerStats:
         if not self.finished and self._final is None:  # no completion event yet: K1+K2 on the layer's stream
             torch.cuda.ExternalStream(self._stream, device=self.bufs.device).synchronize()
-        return super().final_stats()
+        return super().final_stats_unchecked()
 
     def kv(self):
         return self.k_out, self.v_out

@@ -97,6 +97,8 @@ class RealTimePrefillCompressor:
         # next call on that device or by get_overall_compression_stats, without a stream sync
         self._unverified: Dict[torch.device, tuple] = {}
         self._test_flags = 0  # RTKV_TEST_* bits OR-ed into every layer's flags (tests only)
+        # bytes of kept K/V rows read into the Infinity Cache between K2 and K4 (rtkv_prefetch_kept_rows)
+        self.prefetch_bytes = int(float(os.environ.get("RTKV_DROPIN_PREFETCH_MB", "0")) * (1 << 20))
         self._packable: Dict[tuple, bool] = {}  # (dtype, bits) → whether the packed codes are emitted
 
     # ------------------------------------------------------------------ reference API
@@ -169,22 +171,38 @@ class RealTimePrefillCompressor:
                                        causal=causal, key_bias=key_padding_bias)
         else:
             res = compress_layer_begin(K, V, W, params, bufs, ws, early)
+        if self.prefetch_bytes > 0 and res._early is not None:
+            # the first kept rows into the Infinity Cache while the host waits and allocates (after K2)
+            L.check(L.lib().rtkv_prefetch_kept_rows(res._finish_args[0], res._finish_args[2], self.prefetch_bytes,
+                                                    res._stream), "rtkv_prefetch_kept_rows")
         # the one host wait of the layer: the device publishes S' and the counts as soon as K2 has its
         # thresholds; the exactly-sized outputs are allocated then and K4 is enqueued into them
+        prev, done = None, False
         try:
             flags = res.sizes()[2]  # the early publication's S', code bytes and flags (K2 still running)
-            self._verify_previous(K.device)  # the previous layer's K4 has run by now (stream order)
+            # the previous layer's K4 has started by now (stream order): its final flags, read before this
+            # layer's K4 overwrites them, are checked after the launch (off the path to it)
+            prev = self._unverified.pop(K.device, None)
+            prev_flags = prev[0].final_flags() if prev is not None else None
             if flags & L.FLAG_F16_QMAX_OVERFLOW:
                 raise RuntimeError(F16_OVERFLOW_MSG)
-            res.finish()
+            res.finish()  # between the publication and this launch the device only runs K2's tail
+            done = True
         finally:
             if ws.pending is res:  # an error before finish(): the workspace is free again
                 ws.pending = None
+            if prev is not None and not done:  # still to be checked (next call / overall stats)
+                self._unverified.setdefault(K.device, prev)
+        if prev is not None:
+            self._verify(prev, prev_flags)
         st = res.stats()
         if res._early is not None:
             self._unverified[K.device] = (res, layer_idx)
-        t_end = torch.cuda.Event(enable_timing=True)
-        t_end.record(stream)
+        # the layer's end: the completion event finish() recorded right after K4 (a timing event).  A
+        # second event recorded back to back with it cost ~9 µs of device idle per layer before the next
+        # K1 (profiles/r04d_dropin_gaps*.txt); one event on each side of the layer, as the raw driver
+        # records, costs nothing measurable
+        t_end = res.done
         selected_keys, selected_values = res.kv()
         Sp = st.max_kept
         scores = bufs.scores
@@ -259,15 +277,18 @@ class RealTimePrefillCompressor:
         buffers smaller than its sizes.  Reads the flags K4 published to the host mirror; waits for that
         layer only if its K4 has not published them yet."""
         prev = self._unverified.pop(device, None)
-        if prev is None:
-            return
+        if prev is not None:
+            self._verify(prev, prev[0].final_flags())
+
+    def _verify(self, prev, flags):
+        """_verify_previous for `prev` = (PendingLayer, layer_idx) with its final flags as read from the
+        host mirror (None: not published yet, or already overwritten by a later layer's K4)."""
         res, layer_idx = prev
-        flags = res.final_flags()
-        if flags is None:  # its K4 has not started (another stream): wait for the layer
+        if flags is None:  # its K4 has not started yet (another stream), or its word was overwritten
             res.done.synchronize()
             flags = res.final_flags()
             if flags is None:
-                flags = res.final_stats().error_flags
+                flags = res.final_stats_unchecked().error_flags
         if flags & (L.FLAG_SPIN_TIMEOUT | L.FLAG_OUTPUT_OVERFLOW):
             self.layer_states.pop(layer_idx, None)
             check_flags(flags, f"compress_layer_kv_cache (layer {layer_idx}, returned before its K4 ran)")

@@ -9,5 +9,5 @@ out=gpurun_out/dropin_gaps${DROPIN_OUT:+_$DROPIN_OUT}
 rm -rf "$out"; mkdir -p "$out"
 timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d "$out" -o trace -- python3 tools/dropin_profile.py \
   --layers 32 --reps 5 --no-cprofile ${DROPIN_ARGS:-} > "$out/run.log" 2>&1
-python3 tools/gap_summary.py "$out" > "$out/summary.txt"
+python3 tools/gap_summary.py "$out" --layers 32 --warmup 2 --reps 5 > "$out/summary.txt"
 cat "$out/run.log" | grep -v amdgpu.ids; cat "$out/summary.txt"

@@ -7,3 +7,4 @@ timeout -k 10 300 python -u -m pytest -x -v --timeout 120 --timeout-method threa
   tests/test_gpu_dropin_memory.py tests/test_gpu_stats.py tests/test_gpu_parity.py -m gpu > gpurun_out/r04d_tests.log 2>&1 || exit $?
 timeout -k 10 300 python tools/dropin_profile.py --layers 32 --reps 5 > gpurun_out/r04d_cprofile.txt 2>&1 || exit $?
 DROPIN_OUT=r04d bash tools/dropin_gaps.sh > gpurun_out/r04d_dropin_gaps.txt 2>&1 || exit $?
+RTKV_DROPIN_EVENTS=0 DROPIN_OUT=r04d_noev bash tools/dropin_gaps.sh > gpurun_out/r04d_dropin_gaps_noev.txt 2>&1 || exit $?
