@@ -136,13 +136,21 @@ __device__ __forceinline__ void codes_h2(const ChunkCodes<W>& x, H2 (&c)[4]) {
 #pragma unroll
       for (int p = 0; p < 4; ++p)  // byte p of r0 → bits 0..7, byte p of r1 → bits 16..23
         u[p] = __builtin_amdgcn_perm(x.r[1], x.r[0], 0x0c000c00u | (uint32_t)p | ((uint32_t)(4 + p) << 16));
-    } else if constexpr (W == 4) {
-#pragma unroll
-      for (int p = 0; p < 4; ++p) u[p] = (x.r[0] >> (4 * p)) & 0x000f000fu;
     } else {
-      const uint32_t y = __builtin_amdgcn_perm(0u, x.r[0], 0x0c010c00u);  // byte 1 → bits 16..23
+      // W = 4 / 2: (y >> W·p) & mask | 0x6400 in one v_and_or_b32 per pair (the compiler emits and + or).
+      // VOP3 takes no literal and one SGPR: the mask in a VGPR, the 0x6400 pair in an SGPR
+      const uint32_t y = W == 4 ? x.r[0] : __builtin_amdgcn_perm(0u, x.r[0], 0x0c010c00u);  // W = 2: byte 1 → bits 16..23
+      const uint32_t msk = W == 4 ? 0x000f000fu : 0x00030003u, one = 0x64006400u;
 #pragma unroll
-      for (int p = 0; p < 4; ++p) u[p] = (y >> (2 * p)) & 0x00030003u;
+      for (int p = 0; p < 4; ++p) {
+        uint32_t r;
+        asm("v_and_or_b32 %0, %1, %2, %3" : "=v"(r) : "v"(y >> (W * p)), "v"(msk), "s"(one));
+        u[p] = r;
+      }
+      const H2 k1024 = {(_Float16)1024.f, (_Float16)1024.f};
+#pragma unroll
+      for (int p = 0; p < 4; ++p) c[p] = __builtin_bit_cast(H2, u[p]) - k1024;
+      return;
     }
     const H2 k1024 = {(_Float16)1024.f, (_Float16)1024.f};
 #pragma unroll
@@ -228,14 +236,15 @@ __global__ __launch_bounds__(64 * kDW) void decode_split_kernel(DecodeArgs a) {
   const float qscale = a.scale;  // 1/sqrt(D) · log2(e): scores in the exp2 domain
   // one row of the chunk columns this lane owns: K' → dots → online softmax → V' → accumulators
   auto row = [&](auto wtag, const ChunkCodes<decltype(wtag)::value> (&xk)[NCH],
-                 const ChunkCodes<decltype(wtag)::value> (&xv)[NCH], const RowParams& rk, const RowParams& rv) {
+                 const ChunkCodes<decltype(wtag)::value> (&xv)[NCH], const RowParams& rk, const RowParams& rv,
+                 H2 zsk, H2 zsv) {  // fp16: {zp, scale} of K and V as halves (the other dtypes use rk / rv)
     constexpr int W = decltype(wtag)::value;
     float sc[NCH][GQ];
     // K' of each chunk (exactly dequant<DT>: each op rounded to the dtype) and the dots
 #pragma unroll
     for (int k = 0; k < NCH; ++k) {
       if constexpr (kH) {
-        const H2 zp2 = {(_Float16)rk.zp, (_Float16)rk.zp}, sc2 = {(_Float16)rk.scale, (_Float16)rk.scale};
+        const H2 zp2 = __builtin_shufflevector(zsk, zsk, 0, 0), sc2 = __builtin_shufflevector(zsk, zsk, 1, 1);
         H2 kh[4];
         codes_h2<W>(xk[k], kh);
 #pragma unroll
@@ -308,7 +317,7 @@ __global__ __launch_bounds__(64 * kDW) void decode_split_kernel(DecodeArgs a) {
       }
       // V' and the accumulators
       if constexpr (kH) {
-        const H2 zp2 = {(_Float16)rv.zp, (_Float16)rv.zp}, sc2 = {(_Float16)rv.scale, (_Float16)rv.scale};
+        const H2 zp2 = __builtin_shufflevector(zsv, zsv, 0, 0), sc2 = __builtin_shufflevector(zsv, zsv, 1, 1);
         H2 vh[4];
         codes_h2<W>(xv[k], vh);
 #pragma unroll
@@ -389,6 +398,9 @@ __global__ __launch_bounds__(64 * kDW) void decode_split_kernel(DecodeArgs a) {
     }
     if (jb + 64 * kDW < r1) meta(jb + 64 * kDW, m_off, m_offn, m_sz);  // the next batch, in flight meanwhile
     const uint32_t off_lo = (uint32_t)off, off_hi = (uint32_t)(off >> 32);
+    // fp16: {zp, scale} of K and V as half pairs (exact: K4 stores fp16-representable values)
+    const uint32_t zs_k = kH ? __builtin_bit_cast(uint32_t, H2{(_Float16)sz.y, (_Float16)sz.x}) : 0u;
+    const uint32_t zs_v = kH ? __builtin_bit_cast(uint32_t, H2{(_Float16)sz.w, (_Float16)sz.z}) : 0u;
     auto by_width = [&](auto wtag) {
       constexpr int W = decltype(wtag)::value;
       constexpr int PD = W <= 4 ? 8 : (W == 8 ? 4 : 2);  // rows in flight (≤ 32 VGPRs of codes at NCH 2)
@@ -428,9 +440,15 @@ __global__ __launch_bounds__(64 * kDW) void decode_split_kernel(DecodeArgs a) {
       auto compute = [&](int i) {
         const int t = tl[i];
         RowParams rk, rv;
-        rk.scale = lane_f(sz.x, t); rk.zp = lane_f(sz.y, t);
-        rv.scale = lane_f(sz.z, t); rv.zp = lane_f(sz.w, t);
-        row(wtag, bk[i], bv[i], rk, rv);
+        H2 zk = {}, zv = {};
+        if constexpr (kH) {  // the halves were packed once per 64-row batch: two readlanes per row
+          zk = __builtin_bit_cast(H2, __builtin_amdgcn_readlane((int)zs_k, t));
+          zv = __builtin_bit_cast(H2, __builtin_amdgcn_readlane((int)zs_v, t));
+        } else {
+          rk.scale = lane_f(sz.x, t); rk.zp = lane_f(sz.y, t);
+          rv.scale = lane_f(sz.z, t); rv.zp = lane_f(sz.w, t);
+        }
+        row(wtag, bk[i], bv[i], rk, rv, zk, zv);
       };
       int base = 0;
       for (; base + PD <= n; base += PD) {  // full rounds: straight-line, each slot refilled

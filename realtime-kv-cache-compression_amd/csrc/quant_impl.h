@@ -623,6 +623,93 @@ __global__ __launch_bounds__(256, (DT == RTKV_F32 && NCH == 8 && FULL && CONTIG)
   }
 }
 
+// Split-row K4 for short layers (one batch row, contiguous rows of NSPLIT·NCHW·512 elements, no
+// shards): one workgroup of NSPLIT waves per (kept row, tensor), wave q owning chunks
+// [q·NCHW·64, (q+1)·NCHW·64) of the row.  At S = 4096 quant_rows_kernel has ~1.2 waves of kept work
+// per wave slot, so its second, mostly empty round of whole-row waves (a full load → min/max →
+// store latency chain each) is a third of the kernel; here a task is NSPLIT times shorter.  The
+// row's min / max / min |x| / NaN flag are combined through LDS; fminf/fmaxf are order-independent
+// (a zero's sign reaches neither scale nor zero-point), so every output equals quant_rows_kernel's.
+template <int DT, int NCHW, int NSPLIT>
+__global__ __launch_bounds__(64 * NSPLIT) void quant_rows_split_kernel(QuantArgs a) {
+  using S_ = typename Dt<DT>::S;
+  const int lane = threadIdx.x & 63;
+  const int q = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int S = (int)a.kv.S;
+  const int cap = (int)a.out.row_capacity;
+  const int tasks = 2 * (a.kept_index ? (cap < S ? cap : S) : S);
+  const rtkv_batch_stats* bst = a.stats ? reinterpret_cast<const rtkv_batch_stats*>(a.stats + 1) : nullptr;
+  if (k4_layer_gate<DT>(a)) return;  // buffer sizes, final flags, a timed-out selection
+  const bool emit_deq = a.out.k_out_dev != nullptr;
+  const bool emit_pk = a.out.packed_k_dev != nullptr;
+  __shared__ float xch[NSPLIT][4];
+  float4* stage = nullptr;
+  if constexpr (DT == RTKV_F32) {
+    __shared__ float4 k4_stage[NSPLIT][128];
+    stage = k4_stage[q];
+  }
+  int off[NCHW];
+#pragma unroll
+  for (int k = 0; k < NCHW; ++k) off[k] = (k * 64 + lane) * 8;
+  const int qoff = q * NCHW * 512;  // this wave's first element of the row
+  for (int t = blockIdx.x; t < tasks; t += gridDim.x) {  // every condition below is uniform per task
+    const int which = t & 1;
+    const int r = t >> 1;
+    const int rs = r < cap ? r : cap - 1;
+    const int i_s = a.kept_index ? a.kept_index[rs] : r;
+    const int l_s = a.row_label ? (int)a.row_label[rs] : 0;
+    const int64_t roff = emit_pk ? a.out.row_offset_dev[rs] : 0;
+    const int kept_b = a.kept_index ? (int)bst[0].kept : S;
+    if (r >= kept_b) continue;
+    if ((unsigned)i_s >= (unsigned)S) continue;  // never read outside the layer (corrupt kept_index)
+    const int i = __builtin_amdgcn_readfirstlane(i_s);
+    const int lab = __builtin_amdgcn_readfirstlane(a.row_label ? l_s : (int)a.labels[i]);
+    S_* orow = emit_deq ? static_cast<S_*>(which ? a.out.v_out_dev : a.out.k_out_dev) +
+                              (int64_t)r * a.out.o_stride_s + qoff
+                        : nullptr;
+    const int64_t sz_idx = (int64_t)r * 4 + which * 2;
+    if (lab > 2) {  // zero row (caller classes outside {0,1,2})
+      if (emit_deq) {
+        const Chunk<DT> z = f32_to_chunk<DT>({0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f});
+#pragma unroll
+        for (int k = 0; k < NCHW; ++k) *reinterpret_cast<Chunk<DT>*>(orow + off[k]) = z;
+      }
+      if (q == 0 && a.out.scale_zp_dev && lane < 2) a.out.scale_zp_dev[sz_idx + lane] = 0.f;
+      continue;
+    }
+    const int bits = lab == 0 ? a.bits[0] : (lab == 1 ? a.bits[1] : a.bits[2]);
+    const int w = field_width(DT, bits);
+    const S_* src = static_cast<const S_*>(which ? a.kv.v_dev : a.kv.k_dev) + (int64_t)i * a.kv.stride_s + qoff;
+    Chunk<DT> raw[NCHW];
+#pragma unroll
+    for (int k = 0; k < NCHW; ++k) raw[k] = load_chunk_nt<DT>(src + off[k]);
+    float mn, mx, anz;
+    bool row_nan;
+    row_minmax<DT, NCHW, true>(raw, NCHW * 64, lane, mn, mx, anz, row_nan);
+    if (lane == 0) {
+      xch[q][0] = mn;
+      xch[q][1] = mx;
+      xch[q][2] = anz;
+      xch[q][3] = row_nan ? 1.f : 0.f;
+    }
+    __syncthreads();
+    bool nan_any = false;
+#pragma unroll
+    for (int p = 0; p < NSPLIT; ++p) {
+      mn = fminf(mn, xch[p][0]);
+      mx = fmaxf(mx, xch[p][1]);
+      anz = fminf(anz, xch[p][2]);
+      nan_any |= xch[p][3] != 0.f;
+    }
+    __syncthreads();  // xch is rewritten by the next task
+    const RowParams rp = row_params<DT>(mn, mx, bits, anz);
+    if (q == 0 && a.out.scale_zp_dev && lane < 2) a.out.scale_zp_dev[sz_idx + lane] = lane == 0 ? rp.scale : rp.zp;
+    uint8_t* pk = emit_pk ? (which ? a.out.packed_v_dev : a.out.packed_k_dev) + roff + (int64_t)q * NCHW * 64 * w
+                          : nullptr;
+    emit_row<DT, NCHW, true, true>(raw, rp, nan_any, w, orow, off, pk, NCHW * 64, lane, emit_deq, emit_pk, stage);
+  }
+}
+
 // Generic path: any D, any alignment, any F (scalar element access, partial last chunk).
 template <int DT>
 __global__ __launch_bounds__(256) void quant_rows_generic_kernel(QuantArgs a) {
@@ -754,6 +841,22 @@ int launch_quant_dt(const QuantArgs& a, hipStream_t st) {
     hipLaunchKernelGGL((quant_rows_generic_kernel<DT>), dim3((unsigned)blocks), dim3(256), 0, st, a);
     RTKV_HIP_CHECK(hipGetLastError());
     return RTKV_OK;
+  }
+  // short single-row layers: split rows (quant_rows_split_kernel); RTKV_K4_SPLIT_MAXS: token bound
+  static const int64_t split_maxs = [] {
+    const char* e = getenv("RTKV_K4_SPLIT_MAXS");
+    return e ? (int64_t)atol(e) : (int64_t)8192;
+  }();
+  if (contig && kv.B == 1 && a.S_glob == 0 && a.kept_index && Sg <= split_maxs && (nch % 64) == 0) {
+    const unsigned g = (unsigned)tasks;
+#define RTKV_QS(NCHT, NCHW, NSPLIT)                                                                       \
+    if (nch == (int64_t)NCHT * 64) {                                                                      \
+      hipLaunchKernelGGL((quant_rows_split_kernel<DT, NCHW, NSPLIT>), dim3(g), dim3(64 * NSPLIT), 0, st, a); \
+      RTKV_HIP_CHECK(hipGetLastError());                                                                  \
+      return RTKV_OK;                                                                                     \
+    }
+    RTKV_QS(8, 2, 4) RTKV_QS(10, 2, 5)  // Llama-7B / 13B rows
+#undef RTKV_QS
   }
   if (contig) return launch_quant_vec<DT, true>(a, nch, dim3((unsigned)blocks), st);
   return launch_quant_vec<DT, false>(a, nch, dim3((unsigned)blocks), st);

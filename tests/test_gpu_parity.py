@@ -579,3 +579,45 @@ def test_full_size_properties(S, dtype, ratio, H):
         _, ref = orc.fake_quant(K[0, i], synth.DTYPES[dtype], bits, sc, zp)
         assert np.array_equal(k2h[r], ref)
 
+
+
+@pytest.mark.parametrize("dtype,H", [("float32", 32), ("float16", 32), ("bfloat16", 32), ("float32", 40),
+                                     ("float16", 40)])
+def test_split_row_k4_matches_oracle(dtype, H):
+    """Short single-row layers (S <= 8192, F = 4096 / 5120) take quant_rows_split_kernel: each row is
+    quantized by 4 (5) waves that combine its min/max in LDS.  Dequantized rows, codes, scale/zp and
+    row offsets equal the oracle's, including the division-gate edge rows (NaN / ±inf rows: the
+    dual-vs-packed test above; their codes are platform-defined conversions)."""
+    import rtkv
+    from rtkv import _lib as L
+    D, S = 128, 1024 if H == 32 else 800
+    F = H * D
+    K, V = synth.kv(77 + H, 1, S, F, "float32")
+    edge = synth.to_f32(_division_edge_rows(dtype, F), dtype)[0]
+    K[0, 3:3 + edge.shape[0]] = edge
+    V[0, 50:50 + edge.shape[0]] = edge[::-1]
+    K, V = synth.cast(K, dtype), synth.cast(V, dtype)
+    P = rtkv.prompt_length(S)
+    W = synth.attention_slice(77 + H, 1, H, S, P, dtype)
+    dt = synth.DTYPES[dtype]
+    pr = COVERAGE
+    cfg = config(pr, 1)
+    ratio = 0.6
+    p = rtkv.params_from_config(cfg, 0, P, ratio, L.EMIT_DEQUANT | L.EMIT_PACKED)
+    bufs = rtkv.LayerBuffers(1, S, F, TD[dtype], "cuda", (2, 4, 8))
+    res = rtkv.compress_layer(dev(K, dtype), dev(V, dtype), dev(W, dtype), p, bufs, rtkv.Workspace("cuda"))
+    st = res.stats()
+    kk, vv = res.kv()
+    o = orc.compress_layer(K, V, dt, W, dt, P, pr["alpha"], pr["beta"], pr["gamma"], cfg.layer_weights[0],
+                           pr["theta_h"], pr["theta_m"], (2, 4, 8), ratio)
+    R = st.max_kept
+    assert 0 < R < S
+    n = st.total_packed_bytes
+    assert np.array_equal(bufs.packed_k[:n].cpu().numpy(), o["packed_k"][:n])
+    assert np.array_equal(bufs.packed_v[:n].cpu().numpy(), o["packed_v"][:n])
+    assert np.array_equal(bufs.row_offset[:, :R].cpu().numpy(), o["row_offset"])
+    assert np.array_equal(bufs.scale_zp[:, :R].cpu().numpy().view(np.int32), o["scale_zp"].view(np.int32))
+    for got, ref in ((host(kk), o["k_out"]), (host(vv), o["v_out"])):
+        nan_g, nan_r = np.isnan(synth.to_f32(got, dtype)), np.isnan(synth.to_f32(ref, dtype))
+        assert np.array_equal(nan_g, nan_r)
+        assert np.array_equal(got[~nan_g], ref[~nan_r])
