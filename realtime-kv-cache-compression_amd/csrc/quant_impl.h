@@ -842,11 +842,14 @@ int launch_quant_dt(const QuantArgs& a, hipStream_t st) {
     RTKV_HIP_CHECK(hipGetLastError());
     return RTKV_OK;
   }
-  // short single-row layers: split rows (quant_rows_split_kernel); RTKV_K4_SPLIT_MAXS: token bound
-  static const int64_t split_maxs = [] {
+  // short single-row layers: split rows (quant_rows_split_kernel) up to S = 8192 for fp32 (S = 4096:
+  // K4 50.5 -> 43.9 us, S = 8192: 90.3 -> 80.1 us), 4096 for the 2-byte dtypes (S = 8192 fp16: 49.9 ->
+  // 50.5 us, no gain; profiles/r04f_k4_split_ab.json).  RTKV_K4_SPLIT_MAXS overrides the token bound.
+  static const int64_t split_env = [] {
     const char* e = getenv("RTKV_K4_SPLIT_MAXS");
-    return e ? (int64_t)atol(e) : (int64_t)8192;
+    return e ? (int64_t)atol(e) : (int64_t)-1;
   }();
+  const int64_t split_maxs = split_env >= 0 ? split_env : (DT == RTKV_F32 ? 8192 : 4096);
   if (contig && kv.B == 1 && a.S_glob == 0 && a.kept_index && Sg <= split_maxs && (nch % 64) == 0) {
     const unsigned g = (unsigned)tasks;
 #define RTKV_QS(NCHT, NCHW, NSPLIT)                                                                       \

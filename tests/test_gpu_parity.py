@@ -616,7 +616,11 @@ def test_split_row_k4_matches_oracle(dtype, H):
     assert np.array_equal(bufs.packed_k[:n].cpu().numpy(), o["packed_k"][:n])
     assert np.array_equal(bufs.packed_v[:n].cpu().numpy(), o["packed_v"][:n])
     assert np.array_equal(bufs.row_offset[:, :R].cpu().numpy(), o["row_offset"])
-    assert np.array_equal(bufs.scale_zp[:, :R].cpu().numpy().view(np.int32), o["scale_zp"].view(np.int32))
+    # scale/zp bit for bit; a NaN (an edge row that overflows the dtype) by position: the sign of a
+    # generated NaN is platform-defined (x86's default NaN is negative, gfx950's positive)
+    sz_g, sz_r = bufs.scale_zp[:, :R].cpu().numpy(), o["scale_zp"]
+    assert np.array_equal(np.isnan(sz_g), np.isnan(sz_r))
+    assert np.array_equal(sz_g[~np.isnan(sz_g)].view(np.int32), sz_r[~np.isnan(sz_r)].view(np.int32))
     for got, ref in ((host(kk), o["k_out"]), (host(vv), o["v_out"])):
         nan_g, nan_r = np.isnan(synth.to_f32(got, dtype)), np.isnan(synth.to_f32(ref, dtype))
         assert np.array_equal(nan_g, nan_r)

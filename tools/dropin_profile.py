@@ -22,12 +22,63 @@ import bench  # noqa: E402
 import rtkv  # noqa: E402
 
 
+def host_timeline(comp, job, ids, layers, reps):
+    """Per layer, host time from the return of the K4 launch (finish) to the next layer's K1 launch
+    (begin), the begin call itself, the wait for the early statistics, and from the wait's return to
+    the K4 launch — the host's share of the device gaps in the kernel trace."""
+    from rtkv import _lib as L
+    from rtkv import engine
+    lib = L.lib()
+    t = {"begin0": [], "begin1": [], "wait1": [], "fin0": [], "fin1": []}
+    ob, of = lib.rtkv_compress_layer_begin, lib.rtkv_compress_layer_finish
+    ow = engine.EarlyStatsBuffer.wait
+
+    def begin(*x):
+        t["begin0"].append(time.perf_counter())
+        r = ob(*x)
+        t["begin1"].append(time.perf_counter())
+        return r
+
+    def fin(*x):
+        t["fin0"].append(time.perf_counter())
+        r = of(*x)
+        t["fin1"].append(time.perf_counter())
+        return r
+
+    def wait(self, *x, **k):
+        r = ow(self, *x, **k)
+        t["wait1"].append(time.perf_counter())
+        return r
+    lib.rtkv_compress_layer_begin, lib.rtkv_compress_layer_finish = begin, fin
+    engine.EarlyStatsBuffer.wait = wait
+    dev = job.device
+    for it in range(2 + reps):
+        for v in t.values():
+            v.clear()
+        comp.reset_compression_state()
+        torch.cuda.synchronize(dev)
+        for l in range(layers):
+            K, V, W = job.inputs[l]
+            comp.compress_layer_kv_cache(K, V, W, ids, l)
+        torch.cuda.synchronize(dev)
+    n = layers
+    us = lambda v: 1e6 * sum(v) / len(v)
+    post = [t["begin0"][i + 1] - t["fin1"][i] for i in range(n - 1)]
+    print(f"host per layer (us): K4 launch return -> next begin call {us(post):.1f}; begin call (K1+K2 launch) "
+          f"{us([t['begin1'][i] - t['begin0'][i] for i in range(n)]):.1f}; begin return -> wait return "
+          f"{us([t['wait1'][i] - t['begin1'][i] for i in range(n)]):.1f}; wait return -> finish call "
+          f"{us([t['fin0'][i] - t['wait1'][i] for i in range(n)]):.1f}; finish call (K4 launch) "
+          f"{us([t['fin1'][i] - t['fin0'][i] for i in range(n)]):.1f}", flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--dtype", default="float32")
     ap.add_argument("--layers", type=int, default=8)
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--no-cprofile", action="store_true", help="timings only (under a kernel trace)")
+    ap.add_argument("--host-timeline", action="store_true",
+                    help="host timestamps around the begin / wait / finish calls (wrappers add ~1 us each)")
     a = ap.parse_args()
     sys.argv = ["bench.py", "--dtype", a.dtype, "--layers", str(a.layers)]
     args = bench.resolve_config(bench.parse(), 1)
@@ -43,6 +94,9 @@ def main():
             comp.compress_layer_kv_cache(K, V, W, ids, l)
         torch.cuda.synchronize(dev)
 
+    if a.host_timeline:
+        host_timeline(comp, job, ids, args.layers, a.reps)
+        return
     for _ in range(2):
         run()
     t0 = time.perf_counter()
