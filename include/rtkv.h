@@ -350,13 +350,17 @@ int rtkv_wait_early(const rtkv_early_stats* early_host, uint64_t seq, int64_t ti
  * layer before it trusts the outputs without syncing the stream. */
 int rtkv_compress_layer_begin(const rtkv_kv_desc* kv, const rtkv_attn_desc* w, const rtkv_layer_params* p,
                               const rtkv_layer_out* out, void* workspace_dev, size_t workspace_bytes, void* stream,
-                              rtkv_early_stats* early_host, uint64_t seq, int32_t* published);
+                              rtkv_early_stats* early_host, uint64_t seq, int32_t* published, void* start_event);
 int rtkv_compress_layer_qk_begin(const rtkv_kv_desc* kv, const rtkv_qk_desc* q, const rtkv_layer_params* p,
                                  const rtkv_layer_out* out, void* workspace_dev, size_t workspace_bytes, void* stream,
-                                 rtkv_early_stats* early_host, uint64_t seq, int32_t* published);
+                                 rtkv_early_stats* early_host, uint64_t seq, int32_t* published, void* start_event);
 int rtkv_compress_layer_finish(const rtkv_kv_desc* kv, const rtkv_layer_params* p, const rtkv_layer_out* out,
                                int64_t out_rows, void* workspace_dev, size_t workspace_bytes, void* stream,
                                rtkv_early_stats* early_host, uint64_t seq);
+/* start_event (nullable, a hipEvent_t): recorded on the stream right before K1, in the same call —
+ * the start of the drop-in's processing_time.  (Recorded from the host separately before this call,
+ * the timing event cost ~4.5 us of device idle per layer; recorded here, as rtkv_compress_layer_events
+ * does, nothing measurable.) */
 /* Between begin and finish (drop-in path, no reference counterpart): read the first kept rows of K
  * and V — K4's first tasks — up to max_bytes in total, with the default cache policy, so that they are
  * in the Infinity Cache when K4 starts.  Enqueue right after begin, on its stream: it runs while the

@@ -335,18 +335,20 @@ int rtkv_compress_layer_qk_early(const rtkv_kv_desc* kv, const rtkv_qk_desc* q, 
 
 int rtkv_compress_layer_begin(const rtkv_kv_desc* kv, const rtkv_attn_desc* w, const rtkv_layer_params* p,
                               const rtkv_layer_out* out, void* workspace_dev, size_t workspace_bytes, void* stream,
-                              rtkv_early_stats* early_host, uint64_t seq, int32_t* published) {
+                              rtkv_early_stats* early_host, uint64_t seq, int32_t* published, void* start_event) {
   RTKV_REQUIRE(w != nullptr, "null attention descriptor");
-  return compress_layer_impl(kv, w, nullptr, p, out, workspace_dev, workspace_bytes, stream, nullptr, early_host, seq,
-                             published, true);
+  void* const ev[4] = {start_event, nullptr, nullptr, nullptr};
+  return compress_layer_impl(kv, w, nullptr, p, out, workspace_dev, workspace_bytes, stream, start_event ? ev : nullptr,
+                             early_host, seq, published, true);
 }
 
 int rtkv_compress_layer_qk_begin(const rtkv_kv_desc* kv, const rtkv_qk_desc* q, const rtkv_layer_params* p,
                                  const rtkv_layer_out* out, void* workspace_dev, size_t workspace_bytes, void* stream,
-                                 rtkv_early_stats* early_host, uint64_t seq, int32_t* published) {
+                                 rtkv_early_stats* early_host, uint64_t seq, int32_t* published, void* start_event) {
   RTKV_REQUIRE(q != nullptr, "null query descriptor");
-  return compress_layer_impl(kv, nullptr, q, p, out, workspace_dev, workspace_bytes, stream, nullptr, early_host, seq,
-                             published, true);
+  void* const ev[4] = {start_event, nullptr, nullptr, nullptr};
+  return compress_layer_impl(kv, nullptr, q, p, out, workspace_dev, workspace_bytes, stream, start_event ? ev : nullptr,
+                             early_host, seq, published, true);
 }
 
 int rtkv_compress_layer_finish(const rtkv_kv_desc* kv, const rtkv_layer_params* p, const rtkv_layer_out* out,

@@ -326,15 +326,17 @@ class LayerResult:
     kept_score_sum are NaN; ``final_stats()`` syncs the stream and reads them all."""
 
     def __init__(self, bufs: LayerBuffers, B: int, early: Optional[EarlyStatsBuffer] = None, seq: int = 0,
-                 stream: Optional[int] = None, record: bool = True):
+                 stream: Optional[int] = None, record: bool = True, done: Optional[torch.cuda.Event] = None):
         self.bufs = bufs
         self.B = B
         self._early, self._seq = early, seq
         self._stats: Optional[LayerStats] = None
         self._final: Optional[LayerStats] = None
         # the layer's completion on the stream it was launched on: final_stats() waits for exactly that,
-        # whatever stream is current when it is called
-        self.done = torch.cuda.Event(enable_timing=True)  # also the end of the drop-in's processing_time
+        # whatever stream is current when it is called.  A timing event (also the end of the drop-in's
+        # processing_time); `done` passes one in (the drop-in reuses its events: release_done())
+        self.done = done if done is not None else torch.cuda.Event(enable_timing=True)
+        self._done_released = False
         if record:
             self._record(stream)
 
@@ -364,10 +366,27 @@ class LayerResult:
     def final_stats_unchecked(self) -> LayerStats:
         """The final statistics block (a stream sync), error flags included but not raised."""
         if self._final is None:
-            self.done.synchronize()  # the layer's stream, not whichever stream is current here
+            self.wait_done()
             raw = self.bufs.stats.cpu().numpy().tobytes()
             self._final = decode_stats(raw, self.B)
         return self._final
+
+    def wait_done(self):
+        """Wait for the layer's kernels: its completion event (the layer's stream, not whichever stream
+        is current here), or its whole stream once that event went back to the caller's pool."""
+        if self._done_released:
+            s = getattr(self, "_stream", None)
+            if s is None:
+                torch.cuda.synchronize(self.bufs.device)
+            else:
+                torch.cuda.ExternalStream(s, device=self.bufs.device).synchronize()
+        else:
+            self.done.synchronize()
+
+    def release_done(self) -> torch.cuda.Event:
+        """Hand the completion event back for reuse (the layer has completed); later waits sync the stream."""
+        self._done_released = True
+        return self.done
 
     def kv(self):
         """Dequantized (K', V') as contiguous [B, S'_max, F] views (reference return value)."""
@@ -461,9 +480,9 @@ class PendingLayer(LayerResult):
     byte count (early publication, or a stream sync); finish() enqueues K4 into exactly-sized buffers."""
 
     def __init__(self, bufs: LayerBuffers, kd: L.KVDesc, params: L.LayerParams, workspace: "Workspace", stream: int,
-                 early: Optional[EarlyStatsBuffer], seq: int, out: L.LayerOut):
+                 early: Optional[EarlyStatsBuffer], seq: int, out: L.LayerOut, done: Optional[torch.cuda.Event] = None):
         # the completion event is recorded after K4 (finish()); until then final_stats() syncs the stream
-        super().__init__(bufs, kd.B, early, seq, stream=stream, record=False)
+        super().__init__(bufs, kd.B, early, seq, stream=stream, record=False, done=done)
         self._kd, self._params, self._wso, self._stream, self._out = kd, params, workspace, stream, out
         self._ws = workspace.buf
         # finish()'s call, bound now: only out_rows is added after the publication
@@ -548,9 +567,11 @@ class PendingLayer(LayerResult):
 
 def compress_layer_begin(K, V, W, params: L.LayerParams, bufs: LayerBuffers, workspace: Workspace,
                          early: Optional[EarlyStatsBuffer], layout: str = "bsf", Q=None, lse=None, causal: bool = True,
-                         stream: Optional[int] = None, key_bias: Optional[torch.Tensor] = None) -> PendingLayer:
+                         stream: Optional[int] = None, key_bias: Optional[torch.Tensor] = None,
+                         done: Optional[torch.cuda.Event] = None, start_event: Optional[int] = None) -> PendingLayer:
     """K1 + K2 of one layer (W, or Q + lse for the fused importance mode when W is None) into the
-    per-token buffers of `bufs` (LayerBuffers(..., outputs=False)); PendingLayer.finish() runs K4."""
+    per-token buffers of `bufs` (LayerBuffers(..., outputs=False)); PendingLayer.finish() runs K4.
+    start_event: a hipEvent_t handle (torch.cuda.Event.cuda_event) recorded right before K1."""
     L.require_device(K, V, *((Q, lse) if W is None else (W,)))
     kd = kv_desc(K, V, layout)
     if W is None:
@@ -568,6 +589,6 @@ def compress_layer_begin(K, V, W, params: L.LayerParams, bufs: LayerBuffers, wor
     st = L.stream_ptr(K.device) if stream is None else stream
     seq, pub = (early.next_seq(), ctypes.c_int32(0)) if early is not None else (0, ctypes.c_int32(0))
     L.check(fn(ctypes.byref(kd), ctypes.byref(xd), ctypes.byref(params), ctypes.byref(out), ws.data_ptr(), ws.numel(),
-               st, early.ptr if early is not None else None, seq, ctypes.byref(pub)), name)
-    return PendingLayer(bufs, kd, params, workspace, st, early if pub.value else None, seq, out)
+               st, early.ptr if early is not None else None, seq, ctypes.byref(pub), start_event), name)
+    return PendingLayer(bufs, kd, params, workspace, st, early if pub.value else None, seq, out, done=done)
 

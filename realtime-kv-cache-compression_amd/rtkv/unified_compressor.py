@@ -102,7 +102,10 @@ class RealTimePrefillCompressor:
         # drop-in step 7.99 -> 7.85 ms at cfg3 fp32 (profiles/r04f_dropin.json).  RTKV_DROPIN_PREFETCH_MB=0
         # turns it off.
         self.prefetch_bytes = int(float(os.environ.get("RTKV_DROPIN_PREFETCH_MB", "64")) * (1 << 20))
-        self._packable: Dict[tuple, bool] = {}  # (dtype, bits) → whether the packed codes are emitted
+        self._packable: Dict[tuple, bool] = {}
+        self._event_pool: Dict[torch.device, list] = {}  # free timing events (processing_time)
+        self._side_streams: Dict[torch.device, torch.cuda.Stream] = {}
+        self._timing: Dict[torch.device, tuple] = {}  # the last layer whose processing_time is still lazy  # (dtype, bits) → whether the packed codes are emitted
 
     # ------------------------------------------------------------------ reference API
     def identify_prompt_tokens(self, input_ids: torch.Tensor, special_tokens: Optional[List[int]] = None):
@@ -166,14 +169,21 @@ class RealTimePrefillCompressor:
         if early is None:
             early = self._early[K.device] = EarlyStatsBuffer()
         stream = torch.cuda.current_stream(K.device)  # the stream the layer's kernels run on
-        t_start = torch.cuda.Event(enable_timing=True)
-        t_start.record(stream)
+        # processing_time's two timing events come from a per-device pool: events created per call cost
+        # ~4.5 µs of device idle per layer before K1 (profiles/r04g_*); the previous layer's pair goes
+        # back to the pool once its time is read, at this layer's publication (below)
+        pool = self._event_pool.setdefault(K.device, [])
+        t_start = pool.pop() if pool else self._new_event(K.device)
+        done_ev = pool.pop() if pool else self._new_event(K.device)
+        # t_start is recorded by the begin call itself, right before K1 (recorded from here, ahead of the
+        # call, it cost ~4.5 µs of device idle before K1 per layer: profiles/r04h_*)
         if fused:
             Q = query_states if query_states.stride(-1) == 1 else query_states.contiguous()
             res = compress_layer_begin(K, V, None, params, bufs, ws, early, Q=Q, lse=attention_lse.contiguous(),
-                                       causal=causal, key_bias=key_padding_bias)
+                                       causal=causal, key_bias=key_padding_bias, done=done_ev,
+                                       start_event=t_start.cuda_event)
         else:
-            res = compress_layer_begin(K, V, W, params, bufs, ws, early)
+            res = compress_layer_begin(K, V, W, params, bufs, ws, early, done=done_ev, start_event=t_start.cuda_event)
         if self.prefetch_bytes > 0 and res._early is not None:
             # the first kept rows into the Infinity Cache while the host waits and allocates (after K2)
             L.check(L.lib().rtkv_prefetch_kept_rows(res._finish_args[0], res._finish_args[2], self.prefetch_bytes,
@@ -198,6 +208,9 @@ class RealTimePrefillCompressor:
                 self._unverified.setdefault(K.device, prev)
         if prev is not None:
             self._verify(prev, prev_flags)
+        timing = self._timing.pop(K.device, None)
+        if timing is not None:
+            self._resolve_timing(timing, pool)
         st = res.stats()
         if res._early is not None:
             self._unverified[K.device] = (res, layer_idx)
@@ -272,7 +285,32 @@ class RealTimePrefillCompressor:
             })
         res.k_out = res.v_out = None  # the caller owns K'/V'; nothing kept here pins them
         self.layer_states[layer_idx] = compression_info
+        self._timing[K.device] = (compression_info, t_start, res)
         return selected_keys, selected_values, compression_info
+
+    def _new_event(self, device) -> torch.cuda.Event:
+        """A timing event for the pool, its hipEvent_t created now (torch creates it at the first
+        record; done on a side stream that has no work, so nothing waits on it)."""
+        side = self._side_streams.get(device)
+        if side is None:
+            side = self._side_streams[device] = torch.cuda.Stream(device)
+        e = torch.cuda.Event(enable_timing=True)
+        e.record(side)
+        return e
+
+    @staticmethod
+    def _resolve_timing(timing, pool):
+        """Store a finished layer's processing_time and return its two events to the pool.  Called at
+        the next layer's early publication, which the device writes after that layer's completion event
+        (stream order), so no wait; a layer on another stream that has not completed keeps its lazy
+        value and its events."""
+        info, t0, res = timing
+        if not res.finished or not res.done.query():
+            return
+        if isinstance(dict.get(info, "processing_time"), _Lazy):
+            dict.__setitem__(info, "processing_time", t0.elapsed_time(res.done) / 1e3)
+        pool.append(t0)
+        pool.append(res.release_done())
 
     def _verify_previous(self, device):
         """Raise if the last layer returned on `device` turned out invalid after it was returned: a
@@ -288,7 +326,7 @@ class RealTimePrefillCompressor:
         host mirror (None: not published yet, or already overwritten by a later layer's K4)."""
         res, layer_idx = prev
         if flags is None:  # its K4 has not started yet (another stream), or its word was overwritten
-            res.done.synchronize()
+            res.wait_done()
             flags = res.final_flags()
             if flags is None:
                 flags = res.final_stats_unchecked().error_flags
@@ -336,6 +374,7 @@ class RealTimePrefillCompressor:
         self.layer_states = {}
         self.importance_tracker.layer_scores = {}
         self._unverified = {}
+        self._timing = {}  # (a pending layer keeps its lazy processing_time and its own events)
 
     def estimate_memory_usage(self) -> Dict[str, float]:
         try:
