@@ -174,9 +174,27 @@ typedef struct rtkv_layer_stats {
   /* followed by B x rtkv_batch_stats */
 } rtkv_layer_stats;
 
+/* After the B batch stats: the layer's device time span, read from the GPU's 100 MHz real-time counter
+ * (s_memrealtime; rtkv_wall_clock_khz gives its rate).  begin: when the first block of the layer's
+ * first kernel (K1 / K1') started; end: when the quantization kernel (K4) wrote its last row — the
+ * largest of end[16·k], k < RTKV_TIME_SLOTS (every K4 wave that wrote a row takes an atomic max on slot
+ * (its wave index mod RTKV_TIME_SLOTS), one 128-byte line per slot: on one address the atomics
+ * serialised and doubled K4).  begin is written by every fused call (rtkv_compress_layer*, _begin), end
+ * by rtkv_compress_layer_finish only (all slots 0 otherwise, or when K4 did not run).  The drop-in's
+ * processing_time comes from here, with no event on the stream (a timing event right before K1 cost
+ * ~4.6 us of device idle per layer). */
+#define RTKV_TIME_SLOTS 32
+typedef struct rtkv_layer_times {
+  uint64_t end[16 * RTKV_TIME_SLOTS];
+  uint64_t begin;
+} rtkv_layer_times;
+
 static inline size_t rtkv_stats_bytes(int64_t B) {
-  return sizeof(rtkv_layer_stats) + (size_t)B * sizeof(rtkv_batch_stats);
+  return sizeof(rtkv_layer_stats) + (size_t)B * sizeof(rtkv_batch_stats) + sizeof(rtkv_layer_times);
 }
+
+/* Rate of the device's real-time counter (rtkv_layer_times), kHz. */
+int64_t rtkv_wall_clock_khz(int32_t device);
 
 /* Outputs of one layer.  Any pointer may be NULL to skip that output (scores/labels/mask/kept_index
  * /stats are always needed by the fused driver and must be non-NULL there).

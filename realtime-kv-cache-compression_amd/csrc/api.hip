@@ -173,6 +173,19 @@ int rtkv_select_tokens(const float* scores_dev, const uint8_t* labels_dev, int64
   return launch_select(a, ws.sel, false, (hipStream_t)stream);
 }
 
+// the rtkv_layer_times trailer of a stats block (include/rtkv.h)
+static rtkv_layer_times* layer_times(rtkv_layer_stats* stats, int64_t B) {
+  if (!stats) return nullptr;
+  return reinterpret_cast<rtkv_layer_times*>(reinterpret_cast<char*>(stats) + rtkv_stats_bytes(B) -
+                                             sizeof(rtkv_layer_times));
+}
+
+int64_t rtkv_wall_clock_khz(int32_t device) {
+  int v = 0;
+  if (hipDeviceGetAttribute(&v, hipDeviceAttributeWallClockRate, device) != hipSuccess) return 0;
+  return v;
+}
+
 static QuantArgs make_quant_args(const rtkv_kv_desc* kv, const uint8_t* labels_dev, const int32_t* kept_index_dev,
                                  const rtkv_layer_params* p, const rtkv_layer_out* out, const uint8_t* row_label) {
   QuantArgs q;
@@ -253,7 +266,9 @@ static int compress_layer_impl(const rtkv_kv_desc* kv, const rtkv_attn_desc* w, 
   x.zero0_bytes = (select_fast_shape(kv->B, kv->S) && !(p->flags & RTKV_SELECT_PIPELINE)) ? select_fast_zero_bytes()
                                                                                          : select_zero_bytes(kv->B);
   x.zero1 = out->stats_dev;
-  x.zero1_bytes = rtkv_stats_bytes(kv->B);
+  // everything but rtkv_layer_times.begin, which the first block stamps meanwhile (end starts at 0)
+  x.zero1_bytes = rtkv_stats_bytes(kv->B) - sizeof(uint64_t);
+  x.t_begin = out->stats_dev ? reinterpret_cast<unsigned long long*>(&layer_times(out->stats_dev, kv->B)->begin) : nullptr;
   if (w) {
     rc = launch_aggregation(*w, p->prompt_len, ws.A, st, x);
   } else {
@@ -296,6 +311,7 @@ static int compress_layer_impl(const rtkv_kv_desc* kv, const rtkv_attn_desc* w, 
     if (rc) return rc;
     return mark(2);
   }
+  // (the one-call driver leaves rtkv_layer_times.end at 0: callers that time it use events)
   const QuantArgs q = make_quant_args(kv, out->labels_dev, out->kept_index_dev, p, out, row_labels ? ws.labels : nullptr);
   rc = launch_select(a, ws.sel, true, st);
   if (rc) return rc;
@@ -378,6 +394,7 @@ int rtkv_compress_layer_finish(const rtkv_kv_desc* kv, const rtkv_layer_params* 
   if (!(p->flags & RTKV_EMIT_PACKED)) q.out.packed_capacity = (int64_t)1 << 62;
   q.final_host = early_host;
   q.final_seq = seq;
+  q.t_end = reinterpret_cast<unsigned long long*>(layer_times(out->stats_dev, kv->B)->end);
   return launch_quant(q, (hipStream_t)stream);
 }
 

@@ -172,7 +172,9 @@ __global__ __launch_bounds__(256) void attn_lse_f32_kernel(LseF32Args g) {
 // Head-major K1' (as qk_head_kernel): a workgroup owns ONE head and 4·rpw query rows; the head's
 // P ≤ 128 prompt keys stay in LDS (64 KiB); each wave walks its rows in 16-row tiles and writes the
 // per-head prompt mass of each row to part[b][h][i] (qk_head_reduce_kernel sums the heads in order).
-__global__ __launch_bounds__(256) void qk_head_f32_kernel(rtkv_qk_desc q, int P, float* __restrict__ part, int rpw) {
+__global__ __launch_bounds__(256) void qk_head_f32_kernel(rtkv_qk_desc q, int P, float* __restrict__ part, int rpw,
+                                                          unsigned long long* t_begin) {
+  stamp_begin(t_begin);
   constexpr int PT = 128;
   constexpr int KEY_BYTES = PT * kRB;
   constexpr int KI = KEY_BYTES / 1024 / 4;
@@ -272,7 +274,7 @@ int launch_attention_lse_f32(const rtkv_qk_desc& q, float* lse, hipStream_t st) 
   return RTKV_OK;
 }
 
-int launch_qk_head_f32(const rtkv_qk_desc& q, int P, float* part, hipStream_t st) {
+int launch_qk_head_f32(const rtkv_qk_desc& q, int P, float* part, hipStream_t st, unsigned long long* t_begin) {
   RTKV_REQUIRE(q.D == kD, "importance_qk_lse (fp32): head_dim must be 128");
   RTKV_REQUIRE(q.q_stride_s % 4 == 0 && q.q_stride_h % 4 == 0 && q.q_stride_b % 4 == 0 && q.k_stride_s % 4 == 0 &&
                    q.k_stride_h % 4 == 0 && q.k_stride_b % 4 == 0 && ((uintptr_t)q.q_dev % 16) == 0 &&
@@ -288,7 +290,7 @@ int launch_qk_head_f32(const rtkv_qk_desc& q, int P, float* part, hipStream_t st
   int rpw = 256;
   while (rpw > 16 && (q.S + 4 * rpw - 1) / (4 * rpw) * q.H * q.B < 2048) rpw /= 2;
   const dim3 grid((unsigned)((q.S + 4 * rpw - 1) / (4 * rpw)), (unsigned)q.H, (unsigned)q.B);
-  hipLaunchKernelGGL(qk_head_f32_kernel, grid, dim3(256), lds, st, q, P, part, rpw);
+  hipLaunchKernelGGL(qk_head_f32_kernel, grid, dim3(256), lds, st, q, P, part, rpw, t_begin);
   RTKV_HIP_CHECK(hipGetLastError());
   return RTKV_OK;
 }

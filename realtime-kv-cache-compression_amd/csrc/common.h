@@ -181,9 +181,18 @@ struct AggExtras {
   // Only the position of the reduction-order boundary (cascade_limit) depends on it.
   int64_t row0 = 0;
   int64_t S_total = 0;
+  // device time stamp of the layer's start (rtkv_layer_times.begin, s_memrealtime), written by the
+  // first block of the layer's first kernel
+  unsigned long long* t_begin = nullptr;
 };
+// rtkv_layer_times.begin: the 100 MHz real-time counter when the layer's first block starts
+__device__ __forceinline__ void stamp_begin(unsigned long long* t) {
+  if (t && blockIdx.x == 0 && blockIdx.y == 0 && blockIdx.z == 0 && threadIdx.x == 0)
+    *t = (unsigned long long)__builtin_amdgcn_s_memrealtime();
+}
 // The K1 grid clears the selection scratch of the next kernels (4-byte words, grid-strided).
 __device__ __forceinline__ void zero_regions(const AggExtras& x) {
+  stamp_begin(x.t_begin);
   const int64_t nb = (int64_t)gridDim.x * gridDim.y;
   const int64_t id = (int64_t)blockIdx.y * gridDim.x + blockIdx.x;
   for (int r = 0; r < 2; ++r) {
@@ -198,7 +207,7 @@ int launch_aggregation(const rtkv_attn_desc& w, int P, float* A, hipStream_t st,
 size_t qk_scratch_bytes(int64_t B, int64_t H, int64_t S);
 // fp32 states on the f32 MFMA (attn_f32.hip): the row LSE and the head-major K1' per-head masses
 int launch_attention_lse_f32(const rtkv_qk_desc& q, float* lse, hipStream_t st);
-int launch_qk_head_f32(const rtkv_qk_desc& q, int P, float* part, hipStream_t st);
+int launch_qk_head_f32(const rtkv_qk_desc& q, int P, float* part, hipStream_t st, unsigned long long* t_begin);
 // an additive key bias in raw dot-product units (bias / scale), -inf for a padding key (< -1e30)
 __device__ __forceinline__ float key_bias_raw(const rtkv_qk_desc& q, int64_t b, int64_t j, float inv_scale) {
   const float v = q.kbias_dev[b * q.kbias_stride_b + j];
@@ -273,7 +282,18 @@ struct QuantArgs {
   int64_t out_rows;
   rtkv_early_stats* final_host;
   uint64_t final_seq;
+  // rtkv_layer_times.end of the fused driver's layer (atomic max over K4's workgroups), or null
+  unsigned long long* t_end;
 };
+// rtkv_layer_times.end: every wave of K4 that wrote a row stamps its end into slot (wave index mod
+// RTKV_TIME_SLOTS), the largest stays.  Per wave, no barrier (a workgroup-end barrier held finished
+// waves' slots: K4 +7 %); spread over 128-byte lines (one address: the atomics serialised, K4 x2).
+// Waves without a row end within their dispatch, before the last row is written.
+__device__ __forceinline__ void stamp_end(unsigned long long* t, bool wrote) {
+  if (!t || !wrote || (threadIdx.x & 63) != 0) return;
+  const unsigned slot = ((unsigned)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) % RTKV_TIME_SLOTS;
+  atomicMax(t + 16 * slot, (unsigned long long)__builtin_amdgcn_s_memrealtime());
+}
 int launch_quant(const QuantArgs& a, hipStream_t st);
 
 

@@ -251,6 +251,7 @@ __global__ __launch_bounds__(256, QK_HEAD_WPE) void qk_head_kernel(QKArgs g, flo
   const int c16 = lane & 15, kg = lane >> 4;
   const int h = blockIdx.y, b = blockIdx.z;
   const int S = (int)q.S, grp = (int)(q.H / q.Hkv), P = g.P;
+  stamp_begin(g.ex.t_begin);
   const int wrow = (blockIdx.x * 4 + wave) * rpw;  // this wave's first row
   const float l2e = 1.4426950408889634f;
   const float sc = q.scale * l2e;
@@ -424,7 +425,9 @@ static int launch_qk_head(const QKArgs& a, float* part, hipStream_t st, int* npa
   const dim3 grid((unsigned)((S + 4 * rpw - 1) / (4 * rpw)), (unsigned)a.q.H, (unsigned)a.q.B);
   hipLaunchKernelGGL((qk_head_kernel<DT, NT, KS>), grid, dim3(256), lds, st, a, part, rpw);
   RTKV_HIP_CHECK(hipGetLastError());
-  return launch_qk_head_reduce(a, part, st, nparts);
+  QKArgs r = a;
+  r.ex.t_begin = nullptr;  // the layer started with the head kernel
+  return launch_qk_head_reduce(r, part, st, nparts);
 }
 
 template <int DT, int NT, int KS>
@@ -479,9 +482,11 @@ int launch_qk_importance(const rtkv_qk_desc& q, int P, float* A, hipStream_t st,
   if (q.dtype == RTKV_F32) {  // fp32 states: the head-major kernel on the f32 MFMA (attn_f32.hip)
     RTKV_REQUIRE(head_ok, "importance_qk_lse (fp32): needs head_dim 128 and the head-major scratch "
                           "(rtkv_importance_qk_lse_ws / rtkv_workspace_size_qk)");
-    const int rc = launch_qk_head_f32(q, P, scratch, st);
+    const int rc = launch_qk_head_f32(q, P, scratch, st, a.ex.t_begin);
     if (rc) return rc;
-    return launch_qk_head_reduce(a, scratch, st, nparts);
+    QKArgs r = a;
+    r.ex.t_begin = nullptr;  // the layer started with the head kernel
+    return launch_qk_head_reduce(r, scratch, st, nparts);
   }
   RTKV_REQUIRE(q.q_stride_s % 8 == 0 && q.q_stride_h % 8 == 0 && q.q_stride_b % 8 == 0 && q.k_stride_s % 8 == 0 &&
                    q.k_stride_h % 8 == 0 && q.k_stride_b % 8 == 0 && ((uintptr_t)q.q_dev % 16) == 0 &&

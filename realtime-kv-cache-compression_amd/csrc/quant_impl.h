@@ -558,6 +558,7 @@ __global__ __launch_bounds__(256, (DT == RTKV_F32 && NCH == 8 && FULL && CONTIG)
     __shared__ float4 k4_stage[4][128];  // 256-thread workgroups: 4 waves × 2 KiB
     stage = k4_stage[wave & 3];
   }
+  bool wrote = false;
   for (int t = blockIdx.x * (blockDim.x >> 6) + wave; t < tasks; t += nw) {
     const int which = t & 1;
     const int rr = t >> 1;
@@ -620,7 +621,9 @@ __global__ __launch_bounds__(256, (DT == RTKV_F32 && NCH == 8 && FULL && CONTIG)
     if (emit_pk && !one_row) roff = a.out.row_offset_dev[(int64_t)b * cap + r];
     uint8_t* pk = emit_pk ? (which ? a.out.packed_v_dev : a.out.packed_k_dev) + roff : nullptr;
     emit_row<DT, NCH, CONTIG, FULL>(raw, rp, row_nan, w, orow, out_off, pk, nch, lane, emit_deq, emit_pk, stage);
+    wrote = true;
   }
+  stamp_end(a.t_end, wrote);
 }
 
 // Split-row K4 for short layers (one batch row, contiguous rows of NSPLIT·NCHW·512 elements, no
@@ -652,6 +655,7 @@ __global__ __launch_bounds__(64 * NSPLIT) void quant_rows_split_kernel(QuantArgs
 #pragma unroll
   for (int k = 0; k < NCHW; ++k) off[k] = (k * 64 + lane) * 8;
   const int qoff = q * NCHW * 512;  // this wave's first element of the row
+  bool wrote = false;
   for (int t = blockIdx.x; t < tasks; t += gridDim.x) {  // every condition below is uniform per task
     const int which = t & 1;
     const int r = t >> 1;
@@ -707,7 +711,9 @@ __global__ __launch_bounds__(64 * NSPLIT) void quant_rows_split_kernel(QuantArgs
     uint8_t* pk = emit_pk ? (which ? a.out.packed_v_dev : a.out.packed_k_dev) + roff + (int64_t)q * NCHW * 64 * w
                           : nullptr;
     emit_row<DT, NCHW, true, true>(raw, rp, nan_any, w, orow, off, pk, NCHW * 64, lane, emit_deq, emit_pk, stage);
+    wrote = true;
   }
+  stamp_end(a.t_end, wrote);
 }
 
 // Generic path: any D, any alignment, any F (scalar element access, partial last chunk).
@@ -779,6 +785,7 @@ __global__ __launch_bounds__(256) void quant_rows_generic_kernel(QuantArgs a) {
       }
     }
   }
+  stamp_end(a.t_end, true);
 }
 
 template <int DT, bool CONTIG>

@@ -78,8 +78,25 @@ class EarlyStats(ctypes.Structure):
                 ("batch", BatchStats), ("final_seq", ctypes.c_uint64), ("final_flags", c_i32), ("reserved2", c_i32)]
 
 
+_WALL_KHZ = {}
+
+
+def wall_clock_khz(device) -> int:
+    """Rate of the device's real-time counter (rtkv_layer_times), kHz; cached per device."""
+    idx = torch.device(device).index or 0
+    v = _WALL_KHZ.get(idx)
+    if v is None:
+        v = _WALL_KHZ[idx] = int(lib().rtkv_wall_clock_khz(idx))
+    return v
+
+
+TIME_SLOTS = 32  # RTKV_TIME_SLOTS
+TIMES_BYTES = (16 * TIME_SLOTS + 1) * 8  # sizeof(rtkv_layer_times): end[16 * slots], begin
+
+
 def stats_bytes(B: int) -> int:
-    return ctypes.sizeof(LayerStatsHeader) + B * ctypes.sizeof(BatchStats)
+    """rtkv_stats_bytes: header, B batch rows, the rtkv_layer_times trailer."""
+    return ctypes.sizeof(LayerStatsHeader) + B * ctypes.sizeof(BatchStats) + TIMES_BYTES
 
 
 _SIGS = {
@@ -122,6 +139,7 @@ _SIGS = {
     "rtkv_compress_layer_qk_begin": ([c_p, c_p, c_p, c_p, c_p, c_sz, c_p, c_p, ctypes.c_uint64, c_p, c_p], c_i32),
     "rtkv_compress_layer_finish": ([c_p, c_p, c_p, c_i64, c_p, c_sz, c_p, c_p, ctypes.c_uint64], c_i32),
     "rtkv_prefetch_kept_rows": ([c_p, c_p, c_i64, c_p], c_i32),
+    "rtkv_wall_clock_khz": ([c_i32], c_i64),
     "rtkv_mask_key_padding": ([c_p, c_i32, c_i64, c_i64, c_i64, c_i64, c_i64, c_f, c_p, c_i64, c_p, c_p], c_i32),
     "rtkv_host_alloc": ([c_sz], c_p),
     "rtkv_host_free": ([c_p], None),

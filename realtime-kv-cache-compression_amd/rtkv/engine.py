@@ -9,6 +9,7 @@ import ctypes
 from dataclasses import dataclass
 from typing import Optional
 
+import numpy as np
 import torch
 
 from . import _lib as L
@@ -326,17 +327,16 @@ class LayerResult:
     kept_score_sum are NaN; ``final_stats()`` syncs the stream and reads them all."""
 
     def __init__(self, bufs: LayerBuffers, B: int, early: Optional[EarlyStatsBuffer] = None, seq: int = 0,
-                 stream: Optional[int] = None, record: bool = True, done: Optional[torch.cuda.Event] = None):
+                 stream: Optional[int] = None, record: bool = True):
         self.bufs = bufs
         self.B = B
         self._early, self._seq = early, seq
         self._stats: Optional[LayerStats] = None
         self._final: Optional[LayerStats] = None
         # the layer's completion on the stream it was launched on: final_stats() waits for exactly that,
-        # whatever stream is current when it is called.  A timing event (also the end of the drop-in's
-        # processing_time); `done` passes one in (the drop-in reuses its events: release_done())
-        self.done = done if done is not None else torch.cuda.Event(enable_timing=True)
-        self._done_released = False
+        # whatever stream is current when it is called (no timing: the layer's time span comes from the
+        # kernels' own stamps, device_seconds())
+        self.done = torch.cuda.Event()
         if record:
             self._record(stream)
 
@@ -367,26 +367,27 @@ class LayerResult:
         """The final statistics block (a stream sync), error flags included but not raised."""
         if self._final is None:
             self.wait_done()
-            raw = self.bufs.stats.cpu().numpy().tobytes()
-            self._final = decode_stats(raw, self.B)
+            self._final = decode_stats(self.bufs.stats.cpu().numpy().tobytes(), self.B)
         return self._final
 
-    def wait_done(self):
-        """Wait for the layer's kernels: its completion event (the layer's stream, not whichever stream
-        is current here), or its whole stream once that event went back to the caller's pool."""
-        if self._done_released:
-            s = getattr(self, "_stream", None)
-            if s is None:
-                torch.cuda.synchronize(self.bufs.device)
-            else:
-                torch.cuda.ExternalStream(s, device=self.bufs.device).synchronize()
-        else:
-            self.done.synchronize()
+    def device_seconds(self) -> float:
+        """The layer's device time span (rtkv_layer_times: the first K1 block's start to the last K4
+        workgroup's end on the GPU's real-time counter), after a wait for the layer; NaN when K4 did not
+        run (or the call did not stamp it)."""
+        if not getattr(self, "finished", True):  # a pending layer whose K4 was never enqueued
+            return float("nan")
+        self.wait_done()  # (a statistics block read before K4 — the synchronised path — has no end yet)
+        t = self.bufs.stats[-L.TIMES_BYTES:].cpu().numpy().view(np.uint64)
+        end, begin = int(t[:-1:16].max()), int(t[-1])
+        khz = L.wall_clock_khz(self.bufs.device)
+        if end == 0 or end < begin or khz <= 0:
+            return float("nan")
+        return (end - begin) / (khz * 1e3)
 
-    def release_done(self) -> torch.cuda.Event:
-        """Hand the completion event back for reuse (the layer has completed); later waits sync the stream."""
-        self._done_released = True
-        return self.done
+    def wait_done(self):
+        """Wait for the layer's kernels (its completion event: the layer's stream, not whichever stream
+        is current here)."""
+        self.done.synchronize()
 
     def kv(self):
         """Dequantized (K', V') as contiguous [B, S'_max, F] views (reference return value)."""
@@ -480,9 +481,9 @@ class PendingLayer(LayerResult):
     byte count (early publication, or a stream sync); finish() enqueues K4 into exactly-sized buffers."""
 
     def __init__(self, bufs: LayerBuffers, kd: L.KVDesc, params: L.LayerParams, workspace: "Workspace", stream: int,
-                 early: Optional[EarlyStatsBuffer], seq: int, out: L.LayerOut, done: Optional[torch.cuda.Event] = None):
+                 early: Optional[EarlyStatsBuffer], seq: int, out: L.LayerOut):
         # the completion event is recorded after K4 (finish()); until then final_stats() syncs the stream
-        super().__init__(bufs, kd.B, early, seq, stream=stream, record=False, done=done)
+        super().__init__(bufs, kd.B, early, seq, stream=stream, record=False)
         self._kd, self._params, self._wso, self._stream, self._out = kd, params, workspace, stream, out
         self._ws = workspace.buf
         # finish()'s call, bound now: only out_rows is added after the publication
@@ -568,7 +569,7 @@ class PendingLayer(LayerResult):
 def compress_layer_begin(K, V, W, params: L.LayerParams, bufs: LayerBuffers, workspace: Workspace,
                          early: Optional[EarlyStatsBuffer], layout: str = "bsf", Q=None, lse=None, causal: bool = True,
                          stream: Optional[int] = None, key_bias: Optional[torch.Tensor] = None,
-                         done: Optional[torch.cuda.Event] = None, start_event: Optional[int] = None) -> PendingLayer:
+                         start_event: Optional[int] = None) -> PendingLayer:
     """K1 + K2 of one layer (W, or Q + lse for the fused importance mode when W is None) into the
     per-token buffers of `bufs` (LayerBuffers(..., outputs=False)); PendingLayer.finish() runs K4.
     start_event: a hipEvent_t handle (torch.cuda.Event.cuda_event) recorded right before K1."""
@@ -590,5 +591,5 @@ def compress_layer_begin(K, V, W, params: L.LayerParams, bufs: LayerBuffers, wor
     seq, pub = (early.next_seq(), ctypes.c_int32(0)) if early is not None else (0, ctypes.c_int32(0))
     L.check(fn(ctypes.byref(kd), ctypes.byref(xd), ctypes.byref(params), ctypes.byref(out), ws.data_ptr(), ws.numel(),
                st, early.ptr if early is not None else None, seq, ctypes.byref(pub), start_event), name)
-    return PendingLayer(bufs, kd, params, workspace, st, early if pub.value else None, seq, out, done=done)
+    return PendingLayer(bufs, kd, params, workspace, st, early if pub.value else None, seq, out)
 

@@ -72,11 +72,6 @@ class _LazyDict(dict):
         return repr(self.copy())
 
 
-def _synced(ev):
-    ev.synchronize()
-    return ev
-
-
 class RealTimePrefillCompressor:
     """Prompt-guided importance → dynamic precision → selective propagation, per layer."""
 
@@ -103,9 +98,7 @@ class RealTimePrefillCompressor:
         # turns it off.
         self.prefetch_bytes = int(float(os.environ.get("RTKV_DROPIN_PREFETCH_MB", "64")) * (1 << 20))
         self._packable: Dict[tuple, bool] = {}
-        self._event_pool: Dict[torch.device, list] = {}  # free timing events (processing_time)
-        self._side_streams: Dict[torch.device, torch.cuda.Stream] = {}
-        self._timing: Dict[torch.device, tuple] = {}  # the last layer whose processing_time is still lazy  # (dtype, bits) → whether the packed codes are emitted
+  # (dtype, bits) → whether the packed codes are emitted
 
     # ------------------------------------------------------------------ reference API
     def identify_prompt_tokens(self, input_ids: torch.Tensor, special_tokens: Optional[List[int]] = None):
@@ -169,21 +162,12 @@ class RealTimePrefillCompressor:
         if early is None:
             early = self._early[K.device] = EarlyStatsBuffer()
         stream = torch.cuda.current_stream(K.device)  # the stream the layer's kernels run on
-        # processing_time's two timing events come from a per-device pool: events created per call cost
-        # ~4.5 µs of device idle per layer before K1 (profiles/r04g_*); the previous layer's pair goes
-        # back to the pool once its time is read, at this layer's publication (below)
-        pool = self._event_pool.setdefault(K.device, [])
-        t_start = pool.pop() if pool else self._new_event(K.device)
-        done_ev = pool.pop() if pool else self._new_event(K.device)
-        # t_start is recorded by the begin call itself, right before K1 (recorded from here, ahead of the
-        # call, it cost ~4.5 µs of device idle before K1 per layer: profiles/r04h_*)
         if fused:
             Q = query_states if query_states.stride(-1) == 1 else query_states.contiguous()
             res = compress_layer_begin(K, V, None, params, bufs, ws, early, Q=Q, lse=attention_lse.contiguous(),
-                                       causal=causal, key_bias=key_padding_bias, done=done_ev,
-                                       start_event=t_start.cuda_event)
+                                       causal=causal, key_bias=key_padding_bias)
         else:
-            res = compress_layer_begin(K, V, W, params, bufs, ws, early, done=done_ev, start_event=t_start.cuda_event)
+            res = compress_layer_begin(K, V, W, params, bufs, ws, early)
         if self.prefetch_bytes > 0 and res._early is not None:
             # the first kept rows into the Infinity Cache while the host waits and allocates (after K2)
             L.check(L.lib().rtkv_prefetch_kept_rows(res._finish_args[0], res._finish_args[2], self.prefetch_bytes,
@@ -208,17 +192,9 @@ class RealTimePrefillCompressor:
                 self._unverified.setdefault(K.device, prev)
         if prev is not None:
             self._verify(prev, prev_flags)
-        timing = self._timing.pop(K.device, None)
-        if timing is not None:
-            self._resolve_timing(timing, pool)
         st = res.stats()
         if res._early is not None:
             self._unverified[K.device] = (res, layer_idx)
-        # the layer's end: the completion event finish() recorded right after K4 (a timing event).  A
-        # second event recorded back to back with it cost ~9 µs of device idle per layer before the next
-        # K1 (profiles/r04d_dropin_gaps*.txt); one event on each side of the layer, as the raw driver
-        # records, costs nothing measurable
-        t_end = res.done
         selected_keys, selected_values = res.kv()
         Sp = st.max_kept
         scores = bufs.scores
@@ -249,14 +225,16 @@ class RealTimePrefillCompressor:
             m2 = res.final_stats().score_m2
             return (m2 / (n - 1)) ** 0.5 if n > 1 else float("nan")
         host_time = time.time() - start_time
-        # processing_time: the layer's device time, K1 start to K4 end (HIP events on the layer's stream;
-        # read, with its wait, on first access).  The reference's is the host wall time of its synchronous
+        # processing_time: the layer's device time, K1's first block start to K4's last workgroup end (the
+        # GPU's real-time counter, stamped by the kernels: rtkv_layer_times; read, with its wait, on first
+        # access — no events on the stream: a timing event before K1 cost ~4.6 µs of device idle per
+        # layer, profiles/r04i_*).  The reference's is the host wall time of its synchronous
         # call (unified_compressor.py:118,148), which on the device path is exactly that span plus its
         # Python overhead; the device span is what this call costs the caller's stream.  host_return_time:
         # when this call returned (K4 still running).
         compression_info = _LazyDict({
             "layer_idx": layer_idx,
-            "processing_time": _Lazy(lambda: t_start.elapsed_time(_synced(t_end)) / 1e3),
+            "processing_time": _Lazy(res.device_seconds),
             "host_return_time": host_time,
             "original_shape": key_states.shape,
             "compressed_shape": selected_keys.shape,
@@ -285,32 +263,7 @@ class RealTimePrefillCompressor:
             })
         res.k_out = res.v_out = None  # the caller owns K'/V'; nothing kept here pins them
         self.layer_states[layer_idx] = compression_info
-        self._timing[K.device] = (compression_info, t_start, res)
         return selected_keys, selected_values, compression_info
-
-    def _new_event(self, device) -> torch.cuda.Event:
-        """A timing event for the pool, its hipEvent_t created now (torch creates it at the first
-        record; done on a side stream that has no work, so nothing waits on it)."""
-        side = self._side_streams.get(device)
-        if side is None:
-            side = self._side_streams[device] = torch.cuda.Stream(device)
-        e = torch.cuda.Event(enable_timing=True)
-        e.record(side)
-        return e
-
-    @staticmethod
-    def _resolve_timing(timing, pool):
-        """Store a finished layer's processing_time and return its two events to the pool.  Called at
-        the next layer's early publication, which the device writes after that layer's completion event
-        (stream order), so no wait; a layer on another stream that has not completed keeps its lazy
-        value and its events."""
-        info, t0, res = timing
-        if not res.finished or not res.done.query():
-            return
-        if isinstance(dict.get(info, "processing_time"), _Lazy):
-            dict.__setitem__(info, "processing_time", t0.elapsed_time(res.done) / 1e3)
-        pool.append(t0)
-        pool.append(res.release_done())
 
     def _verify_previous(self, device):
         """Raise if the last layer returned on `device` turned out invalid after it was returned: a
@@ -374,7 +327,6 @@ class RealTimePrefillCompressor:
         self.layer_states = {}
         self.importance_tracker.layer_scores = {}
         self._unverified = {}
-        self._timing = {}  # (a pending layer keeps its lazy processing_time and its own events)
 
     def estimate_memory_usage(self) -> Dict[str, float]:
         try:
