@@ -93,10 +93,11 @@ class RealTimePrefillCompressor:
         self._unverified: Dict[torch.device, tuple] = {}
         self._test_flags = 0  # RTKV_TEST_* bits OR-ed into every layer's flags (tests only)
         # bytes of kept K/V rows read into the Infinity Cache between K2 and K4 (rtkv_prefetch_kept_rows),
-        # in the window where the host allocates the outputs: 64 MB measured K4 163 -> 156 us and the
-        # drop-in step 7.99 -> 7.85 ms at cfg3 fp32 (profiles/r04f_dropin.json).  RTKV_DROPIN_PREFETCH_MB=0
-        # turns it off.
-        self.prefetch_bytes = int(float(os.environ.get("RTKV_DROPIN_PREFETCH_MB", "64")) * (1 << 20))
+        # in the window where the host allocates the outputs.  Drop-in step at cfg3 fp32 by size (one box,
+        # profiles/r04k_dropin_prefetch_sweep.json): 0 MB 7.59 ms, 24 MB 7.56, 40 MB 7.49, 64 MB 7.59
+        # (past ~40 MB the read outlasts the host's reaction and delays K4).  RTKV_DROPIN_PREFETCH_MB
+        # overrides (0: off).
+        self.prefetch_bytes = int(float(os.environ.get("RTKV_DROPIN_PREFETCH_MB", "40")) * (1 << 20))
         self._packable: Dict[tuple, bool] = {}
   # (dtype, bits) → whether the packed codes are emitted
 
