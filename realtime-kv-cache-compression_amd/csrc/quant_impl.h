@@ -59,6 +59,8 @@ template <int DT> __device__ __forceinline__ Chunk<DT> f32_to_chunk(const float 
 typedef unsigned int nt_u32x2 __attribute__((ext_vector_type(2)));
 typedef unsigned int nt_u32x4 __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ void nt_store16(void* dst, uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
+  // (write-through sc1 stores instead: K4 170 -> 186 us, and the K4 -> K1 gap unchanged;
+  // profiles/r04l_k4_sc1_ab.json)
   __builtin_nontemporal_store(nt_u32x4{a, b, c, d}, reinterpret_cast<nt_u32x4*>(dst));
 }
 template <int DT> __device__ __forceinline__ void store_chunk_nt(Chunk<DT>* dst, const Chunk<DT>& c) {
