@@ -867,6 +867,8 @@ int launch_quant_dt(const QuantArgs& a, hipStream_t st) {
       RTKV_HIP_CHECK(hipGetLastError());                                                                  \
       return RTKV_OK;                                                                                     \
     }
+    // 4 waves per F = 4096 row; 8 waves of one chunk each measured slower (s4096 K4 43.7 -> 48.9 us,
+    // profiles/r04m_k4_split8_ab.json)
     RTKV_QS(8, 2, 4) RTKV_QS(10, 2, 5)  // Llama-7B / 13B rows
 #undef RTKV_QS
   }
