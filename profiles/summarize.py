@@ -43,7 +43,7 @@ def main():
     sys.path.insert(0, os.path.dirname(here))
     import bench
     saved, sys.argv = sys.argv, ["bench.py"] + bench_args
-    workload = bench.workload_key(bench.parse())
+    workload = bench.workload_key(bench.resolve_config(bench.parse(), 1))  # the config's shape filled in
     sys.argv = saved
     shutil.copy(os.path.join(src, "prof", "run_kernel_stats.csv"), os.path.join(here, f"{tag}_kernel_stats.csv"))
     fetch, n = per_kernel(os.path.join(src, "pmc", "fetch_counter_collection.csv"), "FETCH_SIZE")
