@@ -252,3 +252,48 @@ def test_finish_with_undersized_outputs_writes_nothing():
         assert bool((kv == 7.0).all()) and bool((codes == 0xAB).all())
         with pytest.raises(RuntimeError, match="RTKV_FLAG_OUTPUT_OVERFLOW"):
             res.final_stats()
+
+
+def test_prefetch_and_start_event_leave_the_outputs_unchanged():
+    """The drop-in's kept-row prefetch (loads only, any size, a no-op for B > 1) and the begin call's
+    optional start event do not change a byte of the layer's outputs; the event is recorded (its
+    elapsed time to the completion event is positive)."""
+    import rtkv
+    from rtkv import _lib as L
+    from rtkv.engine import EarlyStatsBuffer, compress_layer_begin
+    S, F = 2048, 1024
+    g = torch.Generator(device="cuda").manual_seed(3)
+    P = rtkv.prompt_length(S)
+    cfg = rtkv.CompressionConfig(alpha=0.8, beta=0.1, gamma=0.1, theta_h=0.4, theta_m=0.25, num_hidden_layers=4,
+                                 high_precision_bits=8, medium_precision_bits=4, low_precision_bits=2)
+    outs = []
+    for B, pf in ((1, 0), (1, 1 << 40), (2, 0), (2, 1 << 40)):
+        K = torch.randn(B, S, F, device="cuda", generator=g)
+        V = torch.randn(B, S, F, device="cuda", generator=g)
+        W = torch.rand(B, 8, S, P, device="cuda", generator=g)
+        if pf:  # same inputs as the previous case
+            K, V, W = prev
+        prev = (K, V, W)
+        comp = rtkv.RealTimePrefillCompressor(cfg)
+        comp.prefetch_bytes = pf
+        ids = torch.zeros(B, S, dtype=torch.long, device="cuda")
+        k, v, info = comp.compress_layer_kv_cache(K, V, W, ids, 1)
+        outs.append((k.clone(), v.clone(), info["packed"]["codes_k"].clone(), info["packed"]["codes_v"].clone()))
+    for a, b in ((0, 1), (2, 3)):
+        for x, y in zip(outs[a], outs[b]):
+            assert torch.equal(x.view(torch.uint8) if x.dtype != torch.uint8 else x,
+                               y.view(torch.uint8) if y.dtype != torch.uint8 else y)
+    # the start event: recorded by rtkv_compress_layer_begin right before K1
+    K, V, W = prev[0][:1].contiguous(), prev[1][:1].contiguous(), prev[2][:1].contiguous()
+    p = rtkv.params_from_config(cfg, 1, P, 0.6, L.EMIT_DEQUANT | L.EMIT_PACKED)
+    bufs = rtkv.LayerBuffers(1, S, F, torch.float32, "cuda", (2, 4, 8), outputs=False)
+    ev = torch.cuda.Event(enable_timing=True)
+    ev.record()  # creates the hipEvent_t (torch makes it at the first record)
+    early = EarlyStatsBuffer()
+    res = compress_layer_begin(K, V, W, p, bufs, rtkv.Workspace("cuda"), early, start_event=ev.cuda_event)
+    res.finish()
+    res.done.synchronize()
+    end = torch.cuda.Event(enable_timing=True)
+    end.record()
+    end.synchronize()
+    assert ev.elapsed_time(end) > 0 and 0 < res.device_seconds() < ev.elapsed_time(end) / 1e3 + 1e-5
