@@ -22,6 +22,38 @@ import bench  # noqa: E402
 import rtkv  # noqa: E402
 
 
+def device_stamps(comp, job, ids, layers, reps):
+    """Without a profiler: each layer's device span (first K1 block start to last K4 row) and the idle
+    time from one layer's last K4 row to the next layer's first K1 block, from rtkv_layer_times."""
+    from rtkv import _lib as L
+    khz = L.wall_clock_khz(job.device)
+    spans, gaps, walls = [], [], []
+    for it in range(2 + reps):
+        comp.reset_compression_state()
+        torch.cuda.synchronize(job.device)
+        t0 = time.perf_counter()
+        res = []
+        for l in range(layers):
+            K, V, W = job.inputs[l]
+            comp.compress_layer_kv_cache(K, V, W, ids, l)
+            res.append(comp._unverified.get(job.device, (None,))[0])
+        torch.cuda.synchronize(job.device)
+        wall = time.perf_counter() - t0
+        if it < 2 or any(r is None for r in res):
+            continue
+        walls.append(wall)
+        be = []
+        for r in res:
+            t = r.bufs.stats[-L.TIMES_BYTES:].cpu().numpy().view("uint64")
+            be.append((int(t[-1]), int(t[:-1:16].max())))
+        spans += [(e - b) / khz * 1e3 for b, e in be]
+        gaps += [(be[i + 1][0] - be[i][1]) / khz * 1e3 for i in range(len(be) - 1)]
+    m = lambda v: sum(v) / len(v)
+    print(f"stamps: wall {m(walls) * 1e3:.3f} ms per {layers} layers; device span per layer {m(spans):.1f} us; "
+          f"idle between layers (last K4 row -> next K1 block) {m(gaps):.1f} us (p50 {sorted(gaps)[len(gaps) // 2]:.1f})",
+          flush=True)
+
+
 def host_timeline(comp, job, ids, layers, reps):
     """Per layer, host time from the return of the K4 launch (finish) to the next layer's K1 launch
     (begin), the begin call itself, the wait for the early statistics, and from the wait's return to
@@ -77,6 +109,9 @@ def main():
     ap.add_argument("--layers", type=int, default=8)
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--no-cprofile", action="store_true", help="timings only (under a kernel trace)")
+    ap.add_argument("--stamps", action="store_true",
+                    help="per-layer device spans and inter-layer gaps from the kernels' own time stamps "
+                         "(rtkv_layer_times; no profiler)")
     ap.add_argument("--host-timeline", action="store_true",
                     help="host timestamps around the begin / wait / finish calls (wrappers add ~1 us each)")
     a = ap.parse_args()
@@ -94,6 +129,9 @@ def main():
             comp.compress_layer_kv_cache(K, V, W, ids, l)
         torch.cuda.synchronize(dev)
 
+    if a.stamps:
+        device_stamps(comp, job, ids, args.layers, a.reps)
+        return
     if a.host_timeline:
         host_timeline(comp, job, ids, args.layers, a.reps)
         return

@@ -1,0 +1,9 @@
+#!/bin/bash
+# round 4 (p): new early/drop-in tests; bench line picks up profiles/r04_pmc.json
+set -o pipefail
+mkdir -p gpurun_out
+export PYTHONUNBUFFERED=1
+timeout -k 10 300 python -u -m pytest -x -v --timeout 120 --timeout-method thread tests/test_gpu_early.py tests/test_gpu_dropin_memory.py -m gpu > gpurun_out/r04p_tests.log 2>&1 || exit $?
+timeout -k 10 300 python bench.py --legs none --steps 10 --warmup 3 > gpurun_out/r04p_bench.json 2> gpurun_out/r04p_bench.err || exit $?
+timeout -k 10 300 python tools/dropin_profile.py --layers 32 --reps 5 --stamps > gpurun_out/r04p_stamps.txt 2>&1 || exit $?
+RTKV_DROPIN_PREFETCH_MB=0 timeout -k 10 300 python tools/dropin_profile.py --layers 32 --reps 5 --stamps > gpurun_out/r04p_stamps_pf0.txt 2>&1 || exit $?
