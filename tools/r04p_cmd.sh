@@ -14,3 +14,7 @@ RTKV_K1_HB16=8 timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeo
 for hb in 0 8 4; do
   RTKV_K1_HB16=$hb timeout -k 10 300 python bench.py --dtype float16 --legs none --steps 10 --warmup 3 --cpu-baseline-seconds 0 > gpurun_out/r04p_k1hb$hb.json 2>/dev/null || exit $?
 done
+RTKV_QK_NWV=8 timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gpu_qk.py -m gpu > gpurun_out/r04p_qk8_tests.log 2>&1 || exit $?
+for nw in 4 8; do
+  RTKV_QK_NWV=$nw timeout -k 10 300 python bench.py --importance qk --dtype float16 --legs none --steps 5 --warmup 2 --cpu-baseline-seconds 0 > gpurun_out/r04p_qk_nwv$nw.json 2>/dev/null || exit $?
+done
