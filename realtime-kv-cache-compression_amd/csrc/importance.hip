@@ -330,18 +330,6 @@ __global__ __launch_bounds__(BT, SPLIT ? 2 * BT / 256 : 1) void aggregation_shfl
       a0[0] = u.x; a0[1] = u.y; a0[2] = u.z; a0[3] = u.w; a0[4] = w.x; a0[5] = w.y; a0[6] = w.z; a0[7] = w.w;
     }
     h = HC;
-  } else if constexpr (PF && HC > 0) {
-    // compile-time head count (H == HC): the batches fully unrolled, the next one in flight while this
-    // one is summed; the cascade steps fold to constants (a2, a3 never used for HC <= 256)
-    constexpr int NB = HC / HB;
-    V v[2][HB];
-    load_batch(v[0], 0);
-#pragma unroll
-    for (int bi = 0; bi < NB; ++bi) {
-      if (bi + 1 < NB) load_batch(v[(bi + 1) & 1], (bi + 1) * HB);
-      consume(v[bi & 1], bi * HB);
-    }
-    h = NB * HB;
   } else if constexpr (!PF) {
     while (h + HB <= H) {
       V v[HB];
@@ -691,17 +679,7 @@ static int launch_agg_dt(const rtkv_attn_desc& w, int P, float* A, hipStream_t s
       const int tt = bt / 16;
       dim3 grid((unsigned)((w.S + tt - 1) / tt), (unsigned)w.B);
       if (x.nparts) *x.nparts = (int)grid.x;
-      static const int hb_env = [] {  // RTKV_K1_HB16=8 / 4: 8- or 4-head batches, next in flight (A/B)
-        const char* e = getenv("RTKV_K1_HB16");
-        return e ? atoi(e) : 0;
-      }();
-      if (bt == 1024 && H == 32 && hb_env == 8)
-        hipLaunchKernelGGL((aggregation_shfl_kernel<DT, 16, 8, true, 1024, false, 32>), grid, dim3(1024), 0, st, W,
-                           H, w.S, w.stride_b, w.stride_h, w.stride_s, lim, A, x);
-      else if (bt == 1024 && H == 32 && hb_env == 4)
-        hipLaunchKernelGGL((aggregation_shfl_kernel<DT, 16, 4, true, 1024, false, 32>), grid, dim3(1024), 0, st, W,
-                           H, w.S, w.stride_b, w.stride_h, w.stride_s, lim, A, x);
-      else if (bt == 1024)
+      if (bt == 1024)
         hipLaunchKernelGGL((aggregation_shfl_kernel<DT, 16, 16, false, 1024>), grid, dim3(1024), 0, st, W, H, w.S,
                            w.stride_b, w.stride_h, w.stride_s, lim, A, x);
       else if (bt == 512)

@@ -234,9 +234,8 @@ __global__ __launch_bounds__(256) void qk_importance_kernel(QKArgs g) {
 #ifndef QK_HEAD_WPE
 #define QK_HEAD_WPE 4
 #endif
-template <int DT, int NT, int KS, int NWV = 4>
-__global__ __launch_bounds__(64 * NWV, QK_HEAD_WPE) void qk_head_kernel(QKArgs g, float* __restrict__ part,
-                                                                                  int rpw) {
+template <int DT, int NT, int KS>
+__global__ __launch_bounds__(256, QK_HEAD_WPE) void qk_head_kernel(QKArgs g, float* __restrict__ part, int rpw) {
   using FT = typename Frag<DT>::T;
   using S_ = typename Dt<DT>::S;
   constexpr int D = 32 * KS;
@@ -245,8 +244,7 @@ __global__ __launch_bounds__(64 * NWV, QK_HEAD_WPE) void qk_head_kernel(QKArgs g
   constexpr int CH = RB / 16;
   constexpr int RPI = 1024 / RB;
   constexpr int KEY_BYTES = PT * RB;
-  constexpr int KI = KEY_BYTES / 1024 / NWV;
-  static_assert(KI >= 1, "key tile too small for NWV waves");
+  constexpr int KI = KEY_BYTES / 1024 / 4;
   extern __shared__ __attribute__((aligned(1024))) uint8_t lds[];  // KEY_BYTES
   const rtkv_qk_desc& q = g.q;
   const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -254,7 +252,7 @@ __global__ __launch_bounds__(64 * NWV, QK_HEAD_WPE) void qk_head_kernel(QKArgs g
   const int h = blockIdx.y, b = blockIdx.z;
   const int S = (int)q.S, grp = (int)(q.H / q.Hkv), P = g.P;
   stamp_begin(g.ex.t_begin);
-  const int wrow = (blockIdx.x * NWV + wave) * rpw;  // this wave's first row
+  const int wrow = (blockIdx.x * 4 + wave) * rpw;  // this wave's first row
   const float l2e = 1.4426950408889634f;
   const float sc = q.scale * l2e;
   const S_* Qh = static_cast<const S_*>(q.q_dev) + b * q.q_stride_b + (int64_t)h * q.q_stride_h;
@@ -418,23 +416,17 @@ static int launch_qk_head(const QKArgs& a, float* part, hipStream_t st, int* npa
   constexpr size_t lds = (size_t)(16 * NT) * (64 * KS);
   const int64_t S = a.q.S;
   // rows per wave: 16-row tiles, enough workgroups to fill the chip (>= 1024 with the heads)
-  static const int target = [] {  // RTKV_QK_WGS: measurement knob (workgroups to aim for)
+  // RTKV_QK_WGS: workgroups to aim for.  1024 (128 rows per wave: the head's 32 KB of keys staged once per
+  // 512 rows) measured 47.3 us per cfg3 f16 layer against 49.8 for 2048 and 53.2 for 4096; 8-wave
+  // workgroups (the keys once per 8 waves) 54.4 (profiles/r04p_qk_grid_ab.json)
+  static const int target = [] {
     const char* e = getenv("RTKV_QK_WGS");
-    return e ? atoi(e) : 2048;
+    return e ? atoi(e) : 1024;
   }();
   int rpw = 256;
-  static const int nwv_env = [] {  // RTKV_QK_NWV=8: 8-wave workgroups (the keys staged once per 8 waves; A/B)
-    const char* e = getenv("RTKV_QK_NWV");
-    return e && atoi(e) == 8 ? 8 : 4;
-  }();
-  constexpr bool can8 = (16 * NT) * (64 * KS) >= 8 * 1024;  // >= one 1 KiB key DMA piece per wave
-  const int nwv = (nwv_env == 8 && can8) ? 8 : 4;
-  while (rpw > 16 && (S + nwv * rpw - 1) / (nwv * rpw) * a.q.H * a.q.B < target) rpw /= 2;
-  const dim3 grid((unsigned)((S + nwv * rpw - 1) / (nwv * rpw)), (unsigned)a.q.H, (unsigned)a.q.B);
-  if constexpr (can8) {
-    if (nwv == 8) hipLaunchKernelGGL((qk_head_kernel<DT, NT, KS, 8>), grid, dim3(512), lds, st, a, part, rpw);
-  }
-  if (nwv == 4) hipLaunchKernelGGL((qk_head_kernel<DT, NT, KS>), grid, dim3(256), lds, st, a, part, rpw);
+  while (rpw > 16 && (S + 4 * rpw - 1) / (4 * rpw) * a.q.H * a.q.B < target) rpw /= 2;
+  const dim3 grid((unsigned)((S + 4 * rpw - 1) / (4 * rpw)), (unsigned)a.q.H, (unsigned)a.q.B);
+  hipLaunchKernelGGL((qk_head_kernel<DT, NT, KS>), grid, dim3(256), lds, st, a, part, rpw);
   RTKV_HIP_CHECK(hipGetLastError());
   QKArgs r = a;
   r.ex.t_begin = nullptr;  // the layer started with the head kernel
