@@ -84,15 +84,21 @@ def host_timeline(comp, job, ids, layers, reps):
     lib.rtkv_compress_layer_begin, lib.rtkv_compress_layer_finish = begin, fin
     engine.EarlyStatsBuffer.wait = wait
     dev = job.device
+    edges = []
     for it in range(2 + reps):
         for v in t.values():
             v.clear()
         comp.reset_compression_state()
         torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
         for l in range(layers):
             K, V, W = job.inputs[l]
             comp.compress_layer_kv_cache(K, V, W, ids, l)
+        t1 = time.perf_counter()
         torch.cuda.synchronize(dev)
+        t2 = time.perf_counter()
+        if it >= 2:
+            edges.append((t["begin0"][0] - t0, t1 - t["fin1"][-1], t2 - t1, t2 - t0))
     n = layers
     us = lambda v: 1e6 * sum(v) / len(v)
     post = [t["begin0"][i + 1] - t["fin1"][i] for i in range(n - 1)]
@@ -101,6 +107,9 @@ def host_timeline(comp, job, ids, layers, reps):
           f"{us([t['wait1'][i] - t['begin1'][i] for i in range(n)]):.1f}; wait return -> finish call "
           f"{us([t['fin0'][i] - t['wait1'][i] for i in range(n)]):.1f}; finish call (K4 launch) "
           f"{us([t['fin1'][i] - t['fin0'][i] for i in range(n)]):.1f}", flush=True)
+    e = [sum(x[k] for x in edges) / len(edges) * 1e6 for k in range(4)]
+    print(f"edges (us): loop start -> first begin call {e[0]:.1f}; last K4 launch -> last call returns {e[1]:.1f}; "
+          f"final sync {e[2]:.1f}; wall {e[3]:.1f}", flush=True)
 
 
 def main():
