@@ -77,6 +77,9 @@ def resolve_config(args, world: int):
         if c["seq_total"] % world:
             raise SystemExit(f"bench.py: {args.config}'s S = {c['seq_total']} does not split over {world} ranks")
         args.seq = c["seq_total"] // world
+    # a shape override makes it another workload: label it as the config it was derived from
+    args.config_label = args.config if (args.layers, args.heads, args.head_dim, args.seq * world) == (
+        c["layers"], c["heads"], c["head_dim"], c["seq_total"]) else f"{args.config}-derived"
     return args
 
 
@@ -720,7 +723,7 @@ def main():
             "vs_baseline": None,
             "dtype": {"float16": "f16", "bfloat16": "bf16", "float32": "f32"}[args.dtype],
             "data": "synthetic (seeded torch RNG; K,V ~ N(0,1), W = causal u^4-softmax-like prompt slice)",
-            "config": {"workload": f"{args.config}: {args.model} prefill KV compression"
+            "config": {"workload": f"{args.config_label}: {args.model} prefill KV compression"
                                    f"{' (fused Q/LSE importance)' if args.importance == 'qk' else ''}, {args.layers} layers, "
                                    f"S={job.S * world} ({job.S}/rank), {args.heads}x{args.head_dim}, {args.dtype}, "
                                    f"P={job.P}, bits 8/4/2, ratios .8/.6/.4, {outs} outputs"
