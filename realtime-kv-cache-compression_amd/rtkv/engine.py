@@ -521,23 +521,12 @@ class PendingLayer(LayerResult):
         not (yet) available: no early buffer, K4 not started, or overwritten by a later layer's K4."""
         return self._early.final_flags(self._seq) if self._early is not None and self.finished else None
 
-    def finish(self, pool=None) -> "PendingLayer":
+    def finish(self) -> "PendingLayer":
         """Allocate K'/V' [B, S', F] and the packed codes at their exact sizes and enqueue K4 into them.
         Between the early statistics and this launch the device only runs K2's tail, so this path is
         kept short: one allocation for K'+V', one for both code planes, the begin call's LayerOut patched."""
         Sp, pb, flags = self.sizes()
         check_flags(flags)
-        ctx = torch.cuda.use_mem_pool(pool) if pool is not None else None
-        if ctx is not None:
-            ctx.__enter__()
-        try:
-            self._alloc_outputs(Sp, pb)
-        finally:
-            if ctx is not None:
-                ctx.__exit__(None, None, None)
-        return self._launch_finish(Sp)
-
-    def _alloc_outputs(self, Sp, pb):
         b = self.bufs
         dev = b.device
         out = self._out
@@ -553,9 +542,6 @@ class PendingLayer(LayerResult):
             out.packed_k_dev, out.packed_v_dev = cp, cp + n
             out.packed_capacity = n
             self._codes = codes
-
-    def _launch_finish(self, Sp) -> "PendingLayer":
-        b = self.bufs
         try:
             L.check(L.lib().rtkv_compress_layer_finish(*self._finish_args, max(Sp, 1), *self._finish_tail),
                     "rtkv_compress_layer_finish")

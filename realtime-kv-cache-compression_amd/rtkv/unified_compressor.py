@@ -72,9 +72,6 @@ class _LazyDict(dict):
         return repr(self.copy())
 
 
-_OUT_POOL = os.environ.get("RTKV_DROPIN_POOL") == "1"  # experiment knob
-
-
 class RealTimePrefillCompressor:
     """Prompt-guided importance → dynamic precision → selective propagation, per layer."""
 
@@ -102,7 +99,6 @@ class RealTimePrefillCompressor:
         # overrides (0: off).
         self.prefetch_bytes = int(float(os.environ.get("RTKV_DROPIN_PREFETCH_MB", "40")) * (1 << 20))
         self._packable: Dict[tuple, bool] = {}
-        self._pools: Dict[torch.device, object] = {}
   # (dtype, bits) → whether the packed codes are emitted
 
     # ------------------------------------------------------------------ reference API
@@ -188,7 +184,7 @@ class RealTimePrefillCompressor:
             prev_flags = prev[0].final_flags() if prev is not None else None
             if flags & L.FLAG_F16_QMAX_OVERFLOW:
                 raise RuntimeError(F16_OVERFLOW_MSG)
-            res.finish(self._out_pool(K.device))  # between the publication and this launch the device only runs K2's tail
+            res.finish()  # between the publication and this launch the device only runs K2's tail
             done = True
         finally:
             if ws.pending is res:  # an error before finish(): the workspace is free again
@@ -269,15 +265,6 @@ class RealTimePrefillCompressor:
         res.k_out = res.v_out = None  # the caller owns K'/V'; nothing kept here pins them
         self.layer_states[layer_idx] = compression_info
         return selected_keys, selected_values, compression_info
-
-    def _out_pool(self, device):
-        """The private allocator pool of this compressor's K'/V' and codes (RTKV_DROPIN_POOL=1, A/B)."""
-        if not _OUT_POOL:
-            return None
-        p = self._pools.get(device)
-        if p is None:
-            p = self._pools[device] = torch.cuda.MemPool()
-        return p
 
     def _verify_previous(self, device):
         """Raise if the last layer returned on `device` turned out invalid after it was returned: a
