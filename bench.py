@@ -607,12 +607,15 @@ def roofline_objects(args, job, kus, k4_bytes):
     k4_ach = k4_alg / (k4_us / 1e6) / 1e9
     k4_traffic = None
     name = "quant_rows_kernel"
-    if pmc:
-        k4_traffic = next((round(v["hbm_bytes"]) for k, v in pmc.items() if name in k), None)
+    if pmc:  # the whole-row or the split-row K4 (quant_rows_split_kernel), whichever the workload ran
+        hit = next(((k, v) for k, v in pmc.items() if "quant_rows_" in k), None)
+        if hit:
+            k4_traffic = round(hit[1]["hbm_bytes"])
+            name = "quant_rows_split_kernel" if "quant_rows_split_kernel" in hit[0] else name
     k4 = {"bound": "hbm", "achieved": round(k4_ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
           "frac": round(k4_ach / HBM_PEAK_GBS, 4), "traffic": k4_traffic, "traffic_source": src,
           "algorithmic_bytes_per_launch": round(k4_alg),
-          "kernel": "quant_rows_kernel (K4), K4's read + write bytes",
+          "kernel": f"{name} (K4), K4's read + write bytes",
           "avg_launch_us": round(k4_us, 2)}
     return path, k4
 

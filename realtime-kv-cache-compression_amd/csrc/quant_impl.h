@@ -851,14 +851,17 @@ int launch_quant_dt(const QuantArgs& a, hipStream_t st) {
     RTKV_HIP_CHECK(hipGetLastError());
     return RTKV_OK;
   }
-  // short single-row layers: split rows (quant_rows_split_kernel) up to S = 8192 for fp32 (S = 4096:
-  // K4 50.5 -> 43.9 us, S = 8192: 90.3 -> 80.1 us), 4096 for the 2-byte dtypes (S = 8192 fp16: 49.9 ->
-  // 50.5 us, no gain; profiles/r04f_k4_split_ab.json).  RTKV_K4_SPLIT_MAXS overrides the token bound.
+  // single-row layers: split rows (quant_rows_split_kernel) at every S for fp32 with the dequantized
+  // outputs (S = 4096: K4 50.5 -> 43.9 us, 8192: 90.3 -> 80.1, 16384 (cfg3): 168.6 -> 155.4, 65536:
+  // 635 -> 608; profiles/r04f_k4_split_ab.json, r04ab/r04ac), up to S = 8192 for fp32 packed-only
+  // (cfg3 packed-only: 96.4 -> 103.0 us, slower) and up to S = 4096 for the 2-byte dtypes (fp16 S = 8192:
+  // 49.9 -> 50.5 us, 16384: 89.6 -> 94.7, slower).  RTKV_K4_SPLIT_MAXS overrides the token bound.
   static const int64_t split_env = [] {
     const char* e = getenv("RTKV_K4_SPLIT_MAXS");
     return e ? (int64_t)atol(e) : (int64_t)-1;
   }();
-  const int64_t split_maxs = split_env >= 0 ? split_env : (DT == RTKV_F32 ? 8192 : 4096);
+  const int64_t split_maxs = split_env >= 0 ? split_env
+                               : (DT == RTKV_F32 ? (a.out.k_out_dev ? INT64_MAX : (int64_t)8192) : (int64_t)4096);
   if (contig && kv.B == 1 && a.S_glob == 0 && a.kept_index && Sg <= split_maxs && (nch % 64) == 0) {
     const unsigned g = (unsigned)tasks;
 #define RTKV_QS(NCHT, NCHW, NSPLIT)                                                                       \
