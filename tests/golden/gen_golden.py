@@ -54,6 +54,9 @@ PUBLISHED = dict(alpha=0.6, beta=0.2, gamma=0.2, theta_h=0.6, theta_m=0.2, high_
                  medium_precision_bits=4, low_precision_bits=2, early_layer_ratio=0.8,
                  middle_layer_ratio=0.6, later_layer_ratio=0.4)
 COVERAGE = dict(PUBLISHED, alpha=0.8, beta=0.1, gamma=0.1, theta_h=0.4, theta_m=0.25)
+# the second published run: same parameters at the CompressionConfig default widths 16/8/4
+# (experiments/results/compression_exp_20251020_225951/config.json:50-52, configs/base_config.py:33-35)
+PUB16 = dict(PUBLISHED, high_precision_bits=16, medium_precision_bits=8, low_precision_bits=4)
 DEFAULT = {}  # CompressionConfig defaults: 16/8/4 bits, .4/.3/.3, θ .7/.3
 
 
@@ -294,6 +297,13 @@ LAYER_CASES = [
     ("cfg4_s65536_l31", COVERAGE, 32, 31, 1, 32, 32, 128, 65536, "float32"),
     ("cfg4_s65536_l0", PUBLISHED, 32, 0, 1, 32, 32, 128, 65536, "float16"),
     ("cfg4_s65536_l31", PUBLISHED, 32, 31, 1, 32, 32, 128, 65536, "float16"),
+    # round 5: the default / second published widths 16/8/4 at full size (16-bit packing at F = 4096, the
+    # {0.5, 1, 2} cost units of selective_propagation.py:54-66, K2 quotas in 16-bit units); bf16 cannot
+    # hold 2^16-1, so its HIGH rows take 17-bit fields (rtkv_field_width)
+    ("cfg3_b16_l0", PUB16, 32, 0, 1, 32, 32, 128, 16384, "float32"),
+    ("cfg3_b16_l25", PUB16, 32, 25, 1, 32, 32, 128, 16384, "float32"),
+    ("cfg3_b16_l12", PUB16, 32, 12, 1, 32, 32, 128, 16384, "bfloat16"),
+    ("cfg4_s65536_b16_l20", PUB16, 32, 20, 1, 32, 32, 128, 65536, "float32"),
 ]
 
 
