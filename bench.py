@@ -64,6 +64,38 @@ CONFIGS = {
 }
 
 
+# Compression parameters of a workload.  "coverage": SURVEY §8d's coverage set (all three classes populated and
+# tokens dropped in every layer group) at the reference tests' 8/4/2 bits — the main line and most legs;
+# "pub16": the reference's second published run, alpha/beta/gamma .6/.2/.2, theta .6/.2, ratios .8/.6/.4 at the
+# CompressionConfig default widths 16/8/4 (experiments/results/compression_exp_20251020_225951/config.json,
+# configs/base_config.py:33-35).
+PARAM_SETS = {
+    "coverage": dict(alpha=0.8, beta=0.1, gamma=0.1, theta_h=0.4, theta_m=0.25, high_precision_bits=8,
+                     medium_precision_bits=4, low_precision_bits=2, early_layer_ratio=0.8, middle_layer_ratio=0.6,
+                     later_layer_ratio=0.4),
+    "pub16": dict(alpha=0.6, beta=0.2, gamma=0.2, theta_h=0.6, theta_m=0.2, high_precision_bits=16,
+                  medium_precision_bits=8, low_precision_bits=4, early_layer_ratio=0.8, middle_layer_ratio=0.6,
+                  later_layer_ratio=0.4),
+}
+
+
+def metric_label(args, world: int) -> str:
+    """BASELINE.json's metric string for the headline (cfg3 on 1 GPU); other configs / N get their own."""
+    if world == 1 and args.config == "cfg3":
+        return "prefill KV-compress GB/s + TTFT, Llama-2-7B S=16k, 1 GPU"
+    S_total = args.seq * world
+    return (f"prefill KV-compress GB/s + TTFT, {args.model} S={S_total // 1024}k, "
+            f"{world} GPU{'s' if world > 1 else ''}")
+
+
+def scaling_fields(ms_per_step: float, single_ms: float, world: int, how: str) -> dict:
+    """The N > 1 line's same-workload single-GPU reference: the SAME S_total prefill (same inputs) through
+    the single-GPU driver on rank 0's GPU, so a 1 -> N curve never mixes workloads."""
+    speedup = single_ms / ms_per_step
+    return {"single_gpu_ms_same_workload": round(single_ms, 4), "speedup": round(speedup, 4),
+            "strong_scaling_efficiency": round(speedup / world, 4), "how": how}
+
+
 def resolve_config(args, world: int):
     """Fill --layers/--heads/--head-dim/--seq from --config (default: cfg3 at N = 1, cfg4 at N > 1)."""
     if args.config is None:
@@ -83,17 +115,62 @@ def resolve_config(args, world: int):
     return args
 
 
+def visible_gpu_count(dri: str = "/dev/dri", env=None) -> int:
+    """GPUs this process could use, counted WITHOUT initialising HIP (the launcher runs before any GPU
+    call, and a HIP-initialised parent must not spawn the ranks): the DRM render nodes this process can
+    open (a container maps only its own GPUs' nodes, and the device cgroup refuses the others), limited
+    by the visibility masks HIP honours (ROCR_VISIBLE_DEVICES, then HIP_VISIBLE_DEVICES /
+    CUDA_VISIBLE_DEVICES).  Raises RuntimeError when the count cannot be determined (e.g. /dev/dri
+    unreadable); no /dev/dri at all means no GPU."""
+    env = os.environ if env is None else env
+    if not os.path.exists(dri):
+        n = 0
+    else:
+        try:
+            nodes = sorted(x for x in os.listdir(dri) if x.startswith("renderD"))
+        except OSError as e:
+            raise RuntimeError(f"cannot list {dri}: {e}") from e
+        n = 0
+        for x in nodes:
+            try:
+                fd = os.open(os.path.join(dri, x), os.O_RDWR | os.O_CLOEXEC)
+            except OSError:
+                continue  # not this process's GPU (device cgroup / permissions)
+            os.close(fd)
+            n += 1
+    for var in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        v = env.get(var)
+        if v is None:
+            continue
+        ids = [t for t in v.split(",") if t.strip() != ""]
+        if any(not t.strip().lstrip("-").isdigit() for t in ids):
+            raise RuntimeError(f"{var}={v!r}: cannot count the GPUs it selects (UUIDs are not supported here)")
+        picked = []
+        for t in ids:  # HIP stops at the first invalid ordinal
+            i = int(t)
+            if i < 0 or i >= n:
+                break
+            picked.append(i)
+        n = len(picked)
+    return n
+
+
 def launch(args) -> int:
     """--gpus N > 1 without a torch.distributed environment: run this script under
-    torch.distributed.run as a CHILD process (nothing here touches a GPU: device_count() does not
-    initialise HIP), relay its exit code.  Fails fast when fewer than N GPUs are visible."""
+    torch.distributed.run as a CHILD process (nothing here touches a GPU: visible_gpu_count() opens
+    DRM render nodes only, no HIP call), relay its exit code.  Fails fast when fewer than N GPUs are
+    visible or the count cannot be determined."""
     with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as so:
         so.bind(("127.0.0.1", 0))
         port = so.getsockname()[1]
     rest = [a for a in sys.argv[1:] if a != "--launch-dry-run"]
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
            "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + rest
-    visible = torch.cuda.device_count()
+    try:
+        visible = visible_gpu_count()
+    except RuntimeError as e:
+        print(f"bench.py: cannot determine the visible GPUs ({e}); not running", file=sys.stderr, flush=True)
+        return 2
     if args.launch_dry_run:
         print(json.dumps({"launch": cmd, "visible_gpus": visible}), flush=True)
         return 0
@@ -121,12 +198,18 @@ def parse():
                     help="--gpus N > 1 without WORLD_SIZE: print the torch.distributed.run command line and exit")
     ap.add_argument("--dtype", default="float32", choices=["float16", "bfloat16", "float32"],
                     help="K/V/attention dtype (default: the reference model's fp32)")
+    ap.add_argument("--params", default="coverage", choices=sorted(PARAM_SETS),
+                    help="compression parameters: coverage (8/4/2 bits, the default workload) or pub16 (the "
+                         "reference's published 16/8/4 run)")
+    ap.add_argument("--no-same-workload", action="store_true",
+                    help="N > 1: skip the same-workload single-GPU reference on rank 0")
     ap.add_argument("--no-packed", action="store_true", help="skip the packed-code output")
     ap.add_argument("--no-dequant", action="store_true", help="skip the dequantized K'/V' output (packed only)")
-    ap.add_argument("--legs", default="f16,packed_only,drop_in,s4096,cfg2_s4096_quant,s65536,independent_layers,"
-                                      "prefill_7b,prefill_7b_f32",
-                    help="extra single-GPU legs after the main line: comma list of f16, packed_only, drop_in, "
-                         "s4096, cfg2_s4096_quant, s65536, independent_layers, prefill_7b, prefill_7b_f32 (or 'none')")
+    ap.add_argument("--legs", default="f16,packed_only,f16_packed_only,bits16,drop_in,s4096,cfg2_s4096_quant,s65536,"
+                                      "independent_layers,prefill_7b,prefill_7b_f32",
+                    help="extra single-GPU legs after the main line: comma list of f16, packed_only, f16_packed_only, "
+                         "bits16, drop_in, s4096, cfg2_s4096_quant, s65536, independent_layers, prefill_7b, "
+                         "prefill_7b_f32 (or 'none')")
     ap.add_argument("--prefill-dtype", default="float16", choices=["float16", "bfloat16", "float32"],
                     help="dtype of the prefill_7b leg's random-init model")
     ap.add_argument("--prefill-modes", default="none,fused,eager",
@@ -196,10 +279,11 @@ class Job:
     another job's resident inputs instead of generating new ones."""
 
     def __init__(self, args, device, rank, world, dtype=None, emit_dequant=None, emit_packed=None, inputs=None,
-                 seq=None, slots=None, quant_only=False):
+                 seq=None, slots=None, quant_only=False, param_set=None):
         """seq: tokens (default --seq); slots: distinct input/output sets, layer l uses slot l % slots
-        (bounds the memory of long-sequence legs; default one per layer); quant_only: every token kept
-        (RTKV_NO_SELECTION: BASELINE config 2, quantization without propagation)."""
+        (bounds the memory of long-sequence legs; default one per layer); ``inputs`` given: layer l reads
+        inputs[l % len(inputs)] and only the outputs cycle over ``slots``; quant_only: every token kept
+        (RTKV_NO_SELECTION: BASELINE config 2, quantization without propagation); param_set: PARAM_SETS key."""
         import rtkv
         from rtkv import _lib as L
         self.args, self.device, self.rank, self.world = args, device, rank, world
@@ -209,11 +293,9 @@ class Job:
         self.S_total = self.S * world
         self.P = rtkv.prompt_length(self.S_total)
         self.quant_only = quant_only
-        self.cfg = rtkv.CompressionConfig(alpha=0.8, beta=0.1, gamma=0.1, theta_h=0.4, theta_m=0.25,
-                                          high_precision_bits=8, medium_precision_bits=4, low_precision_bits=2,
-                                          early_layer_ratio=0.8, middle_layer_ratio=0.6, later_layer_ratio=0.4,
-                                          num_hidden_layers=args.layers)
-        self.bits = (2, 4, 8)
+        self.param_set = param_set = param_set or getattr(args, "params", "coverage")
+        self.cfg = rtkv.CompressionConfig(**PARAM_SETS[param_set], num_hidden_layers=args.layers)
+        self.bits = (self.cfg.low_precision_bits, self.cfg.medium_precision_bits, self.cfg.high_precision_bits)
         self.emit_packed = (not args.no_packed) if emit_packed is None else emit_packed
         self.emit_dequant = (not args.no_dequant) if emit_dequant is None else emit_dequant
         if not (self.emit_packed or self.emit_dequant):
@@ -224,7 +306,7 @@ class Job:
         gen = torch.Generator(device=device)
         gen.manual_seed(1234 + 7919 * rank)
         self.slots = min(args.layers, slots or args.layers)
-        self.inputs = inputs if inputs is not None else []
+        self.inputs = list(inputs) if inputs is not None else []
         self.bufs, self.params = [], []
         for l in range(args.layers):
             if inputs is None and l < self.slots:
@@ -240,6 +322,7 @@ class Job:
                                                    emit_dequant=self.emit_dequant, emit_packed=self.emit_packed))
             ratio = 1.0 if quant_only else prop.get_layer_propagation_ratio(l)
             self.params.append(rtkv.params_from_config(self.cfg, l, self.P, ratio, flags))
+        self.in_slots = len(self.inputs)
         self._acct = None
         self.ws = rtkv.Workspace(device)
         self.ws.get(1, self.S)
@@ -268,26 +351,26 @@ class Job:
             for st in self.streams[1:]:
                 st.wait_stream(main)
         for l in range(self.args.layers):
-            sl = l % self.slots
+            sl, si = l % self.slots, l % self.in_slots
             if n > 1:
                 st = self.streams[l % n]
                 with torch.cuda.stream(st if st is not None else torch.cuda.current_stream(self.device)):
                     if qk:
-                        K, V, Q, lse = self.inputs[sl]
+                        K, V, Q, lse = self.inputs[si]
                         rtkv.compress_layer_qk(K, V, Q, lse, self.params[l], self.bufs[sl], self.wss[l % n])
                     else:
-                        K, V, W = self.inputs[sl]
+                        K, V, W = self.inputs[si]
                         rtkv.compress_layer(K, V, W, self.params[l], self.bufs[sl], self.wss[l % n])
                 continue
             if qk:
-                K, V, Q, lse = self.inputs[sl]
+                K, V, Q, lse = self.inputs[si]
                 if events is None:
                     rtkv.compress_layer_qk(K, V, Q, lse, self.params[l], self.bufs[sl], self.ws)
                     continue
                 kd, wd = rtkv.engine.kv_desc(K, V), rtkv.engine.qk_desc(Q, K, lse)
                 fn = L.lib().rtkv_compress_layer_qk_events
             else:
-                K, V, W = self.inputs[sl]
+                K, V, W = self.inputs[si]
                 if events is None:
                     rtkv.compress_layer(K, V, W, self.params[l], self.bufs[sl], self.ws)
                     continue
@@ -330,12 +413,12 @@ class Job:
 
     def _step_one(self, l):
         import rtkv
-        sl = l % self.slots
+        sl, si = l % self.slots, l % self.in_slots
         if self.args.importance == "qk":
-            K, V, Q, lse = self.inputs[sl]
+            K, V, Q, lse = self.inputs[si]
             rtkv.compress_layer_qk(K, V, Q, lse, self.params[l], self.bufs[sl], self.ws)
         else:
-            K, V, W = self.inputs[sl]
+            K, V, W = self.inputs[si]
             rtkv.compress_layer(K, V, W, self.params[l], self.bufs[sl], self.ws)
 
     def layer_bytes(self):
@@ -388,32 +471,65 @@ class Job:
 
 def drop_in_leg(args, job, steps, warmup):
     """The reference caller's path (modified_llama.py:113-117): RealTimePrefillCompressor.
-    compress_layer_kv_cache per layer, with its host sync for the output shape.  TTFT is the
-    reference's definition, Σ processing_time over the layers (longbench_eval.py:160)."""
+    compress_layer_kv_cache per layer, with its host sync for the output shape.
+
+    Two TTFTs: ``ttft_ms`` is what the caller sees — the wall time of the 32 calls plus the final
+    sync, the reference's definition (Σ processing_time, longbench_eval.py:160, where each
+    processing_time is the host wall time of a synchronous call, unified_compressor.py:118,148);
+    ``ttft_device_span_ms`` is Σ processing_time as rtkv reports it (each layer's device span stamped
+    by its kernels).  Measured for the default strict mode (each call waits for K4's start, so a late
+    selection failure raises in its own layer) and for strict=False."""
     import rtkv
-    comp = rtkv.RealTimePrefillCompressor(job.cfg, emit_packed=job.emit_packed)
     ids = torch.zeros(1, job.S, dtype=torch.long, device=job.device)
-    ttft, wall = [], []
     # the raw driver on the same inputs right before, in the same device state (legs that ran before
     # this one leave the device warmer: the drop-in's margin is measured against this, not the main line)
     raw_ms, _ = job.timed(steps, 1)
-    for it in range(warmup + steps):
-        comp.reset_compression_state()
-        torch.cuda.synchronize(job.device)
-        t0 = time.perf_counter()
-        for l in range(args.layers):
-            K, V, W = job.inputs[l]
-            comp.compress_layer_kv_cache(K, V, W, ids, l)
-        torch.cuda.synchronize(job.device)
-        if it >= warmup:
-            wall.append((time.perf_counter() - t0) * 1e3)
-            ttft.append(comp.get_overall_compression_stats()["total_processing_time"] * 1e3)
-    ms = sum(ttft) / len(ttft)
-    return {"ttft_ms": round(ms, 4), "ms_per_layer": round(ms / args.layers, 4),
-            "raw_driver_ms_per_step_same_state": round(raw_ms, 4),
-            "wall_ms_per_step": round(sum(wall) / len(wall), 4), "steps": steps,
-            "path": "rtkv.RealTimePrefillCompressor.compress_layer_kv_cache (dequant + packed, one host sync "
-                    "per layer for the output shape)"}
+    out = {}
+    for strict in (True, False):
+        comp = rtkv.RealTimePrefillCompressor(job.cfg, emit_packed=job.emit_packed, strict=strict)
+        span, wall = [], []
+        for it in range(warmup + steps):
+            comp.reset_compression_state()
+            torch.cuda.synchronize(job.device)
+            t0 = time.perf_counter()
+            for l in range(args.layers):
+                K, V, W = job.inputs[l % job.in_slots]
+                comp.compress_layer_kv_cache(K, V, W, ids, l)
+            torch.cuda.synchronize(job.device)
+            if it >= warmup:
+                wall.append((time.perf_counter() - t0) * 1e3)
+                span.append(comp.get_overall_compression_stats()["total_processing_time"] * 1e3)
+        w, d = sum(wall) / len(wall), sum(span) / len(span)
+        out["strict" if strict else "non_strict"] = {
+            "ttft_ms": round(w, 4), "wall_ms_per_layer": round(w / args.layers, 4),
+            "ttft_device_span_ms": round(d, 4), "over_raw_driver_ms": round(w - raw_ms, 4)}
+        del comp
+    s_ = out["strict"]
+    return {"ttft_ms": s_["ttft_ms"], "ms_per_layer": s_["wall_ms_per_layer"],
+            "ttft_device_span_ms": s_["ttft_device_span_ms"], "wall_ms_per_step": s_["ttft_ms"],
+            "raw_driver_ms_per_step_same_state": round(raw_ms, 4), "modes": out, "steps": steps,
+            "path": "rtkv.RealTimePrefillCompressor.compress_layer_kv_cache (dequant + packed, one host wait "
+                    "per layer for the output shape; strict = the default)"}
+
+
+def union_inputs(args, device, world, dtype):
+    """The inputs of every layer of a sharded job's WHOLE prefill on one device: rank j's chunks drawn
+    exactly as ShardedJob draws them (generator seed 1234 + 7919*j, row0 = j*S_local), concatenated in
+    token order — the single-GPU reference of an N-rank line computes the same bytes."""
+    import rtkv
+    S_local, H, D = args.seq, args.heads, args.head_dim
+    P = rtkv.prompt_length(S_local * world)
+    gens = []
+    for j in range(world):
+        g = torch.Generator(device=device)
+        g.manual_seed(1234 + 7919 * j)
+        gens.append(g)
+    inputs = []
+    for l in range(args.layers):
+        parts = [synth_layer(l, S_local, H, D, P, dtype, device, gens[j], row0=j * S_local) for j in range(world)]
+        inputs.append(tuple(torch.cat([p[k] for p in parts], dim=2 if k == 2 else 1) for k in range(3)))
+        del parts
+    return inputs
 
 
 class ShardedJob:
@@ -431,10 +547,7 @@ class ShardedJob:
         self.F = self.H * self.D
         self.S_total = self.S * world
         self.P = rtkv.prompt_length(self.S_total)
-        self.cfg = rtkv.CompressionConfig(alpha=0.8, beta=0.1, gamma=0.1, theta_h=0.4, theta_m=0.25,
-                                          high_precision_bits=8, medium_precision_bits=4, low_precision_bits=2,
-                                          early_layer_ratio=0.8, middle_layer_ratio=0.6, later_layer_ratio=0.4,
-                                          num_hidden_layers=args.layers)
+        self.cfg = rtkv.CompressionConfig(**PARAM_SETS["coverage"], num_hidden_layers=args.layers)
         self.bits = (2, 4, 8)
         self.comp = ShardedPrefillCompressor(self.cfg, emit_packed=not args.no_packed, emit_dequant=True,
                                              device=device, overlap=not args.no_overlap,
@@ -527,9 +640,12 @@ class ShardedJob:
 
 def workload_key(args):
     """Identifies the workload a committed PMC summary was collected on (profiles/*_pmc.json)."""
-    return {"seq": args.seq, "layers": args.layers, "heads": args.heads, "head_dim": args.head_dim,
-            "dtype": args.dtype, "packed": not args.no_packed, "dequant": not args.no_dequant,
-            "importance": args.importance}
+    key = {"seq": args.seq, "layers": args.layers, "heads": args.heads, "head_dim": args.head_dim,
+           "dtype": args.dtype, "packed": not args.no_packed, "dequant": not args.no_dequant,
+           "importance": args.importance}
+    if getattr(args, "params", "coverage") != "coverage":  # summaries before round 5 are all "coverage"
+        key["params"] = args.params
+    return key
 
 
 def pmc_kernels(args):
@@ -620,14 +736,23 @@ def roofline_objects(args, job, kus, k4_bytes):
     return path, k4
 
 
+def job_args(args, job):
+    """args as they would read for a bench run of exactly `job`'s workload (the PMC summary key)."""
+    a = argparse.Namespace(**vars(args))
+    a.seq, a.dtype, a.params = job.S, str(job.dtype).split(".")[-1], job.param_set
+    a.no_dequant, a.no_packed = not job.emit_dequant, not job.emit_packed
+    return a
+
+
 def leg_summary(args, job, ms, kus):
     tot, k4 = job.layer_bytes()
-    path, _ = roofline_objects(args, job, kus, k4)
+    path, k4r = roofline_objects(job_args(args, job), job, kus, k4)
     return {"value": round(sum(tot) / (ms / 1e3) / 1e9, 2), "unit": "GB/s", "ms_per_step": round(ms, 4),
             "dtype": {"float16": "f16", "bfloat16": "bf16", "float32": "f32"}[str(job.dtype).split(".")[-1]],
             "outputs": "+".join(x for x, on in (("dequant", job.emit_dequant), ("packed", job.emit_packed)) if on),
+            "bits": "/".join(map(str, job.bits[::-1])), "params": job.param_set,
             "kernel_us_per_layer": kernel_us(job, kus),
-            "path_read_roofline_frac": path["frac"], "layer_us": round(sum(kus), 2)}
+            "path_read_roofline_frac": path["frac"], "layer_us": round(sum(kus), 2), "roofline": k4r}
 
 
 def kernel_us(job, kus):
@@ -713,10 +838,24 @@ def main():
                   **split)
         ranks = [None] * world
         dist.all_gather_object(ranks, me)
+    single = None
+    if sharded and world > 1 and rank == 0 and not args.no_same_workload:
+        # the SAME S_total prefill through the single-GPU driver on this GPU (the other ranks wait in the
+        # final barrier): the per-N lines of a 1 -> N curve then each carry their own same-workload time
+        ref = Job(args, device, 0, 1, inputs=union_inputs(args, device, world, job.dtype), seq=args.seq * world,
+                  slots=8)
+        single_ms, _ = ref.timed(args.steps, args.warmup)
+        single = scaling_fields(ms_per_step, single_ms, world,
+                                f"the same {args.config_label} prefill (S={args.seq * world}, same inputs: every rank's "
+                                f"chunks concatenated) through the single-GPU driver (rtkv_compress_layer; "
+                                f"{'pipeline' if args.seq * world > 32768 else 'one-launch'} K2) on rank 0's GPU, "
+                                f"{args.steps} timed steps, outputs cycled over 8 buffers")
+        del ref
+        torch.cuda.empty_cache()
     if rank == 0:
         outs = "+".join(x for x, on in (("dequant", not args.no_dequant), ("packed", not args.no_packed)) if on)
         line = {
-            "metric": "prefill KV-compress GB/s + TTFT, Llama-2-7B S=16k, 1 GPU",
+            "metric": metric_label(args, world),
             "value": round(value, 2),
             "unit": "GB/s",
             "n_gpus": world,
@@ -733,14 +872,17 @@ def main():
             "config": {"workload": f"{args.config_label}: {args.model} prefill KV compression"
                                    f"{' (fused Q/LSE importance)' if args.importance == 'qk' else ''}, {args.layers} layers, "
                                    f"S={job.S * world} ({job.S}/rank), {args.heads}x{args.head_dim}, {args.dtype}, "
-                                   f"P={job.P}, bits 8/4/2, ratios .8/.6/.4, {outs} outputs"
-                                   + (f", {job.slots} distinct layer inputs cycled" if getattr(job, "slots", args.layers) < args.layers else ""),
+                                   f"P={job.P}, bits {'/'.join(map(str, job.bits[::-1]))}, {getattr(job, 'param_set', 'coverage')} "
+                                   f"parameters, ratios .8/.6/.4, {outs} outputs"
+                                   + (f", {job.in_slots} distinct layer inputs cycled" if getattr(job, "in_slots", args.layers) < args.layers else ""),
                        "model": f"{args.model} (KV shapes only)", "global_batch": 1, "seq_len": job.S * world,
                        "parallelism": f"sequence-shard x{world}" if world > 1 else "single GPU",
                        "layer_streams": 1 if sharded else max(1, args.streams)},
         }
         if sharded:
             line["world_size"] = world
+            if single is not None:
+                line.update(single)
             line["ranks"] = ranks
             line["exchange"] = {"received_bytes_per_rank_per_step": job.exchanged_bytes(),
                                 "kind": ("grouped RCCL send/recv per layer of packed K/V codes + scale/zp (exact byte "
@@ -762,14 +904,27 @@ def main():
                                    "hbm_GBs": round((job.H * job.S * job.D * 2 + 4 * job.H * job.S) / (kus[0] / 1e6) / 1e9, 1)}
             legs = {}
             wanted = [x for x in args.legs.split(",") if x and x != "none"] if args.importance == "w" else []
+            wanted = sorted(wanted, key=lambda x: x not in ("f16", "f16_packed_only"))  # share the fp16 inputs
+            f16_inputs = None
             for name in wanted:
-                if name == "f16" and args.dtype != "float16":
-                    leg = Job(args, device, rank, world, dtype="float16")
-                    legs["f16"] = leg_summary(args, leg, *leg.timed(args.leg_steps, 2))
+                if name in ("f16", "f16_packed_only") and args.dtype != "float16":
+                    # the workload in fp16, with dequantized + packed outputs or packed only (the north star's
+                    # 60 % is defined on packed KV; SURVEY §8d's worked example is fp16)
+                    packed_only = name == "f16_packed_only"
+                    leg = Job(args, device, rank, world, dtype="float16", inputs=f16_inputs,
+                              emit_dequant=not packed_only, emit_packed=True)
+                    f16_inputs = leg.inputs
+                    legs[name] = leg_summary(args, leg, *leg.timed(args.leg_steps, 2))
                     del leg
                 elif name == "packed_only":
                     leg = Job(args, device, rank, world, emit_dequant=False, emit_packed=True, inputs=job.inputs)
                     legs["packed_only"] = leg_summary(args, leg, *leg.timed(args.leg_steps, 2))
+                    del leg
+                elif name == "bits16" and job.param_set != "pub16":
+                    # the reference's default / second published widths 16/8/4 with the published run's
+                    # parameters, on the main line's inputs
+                    leg = Job(args, device, rank, world, inputs=job.inputs, param_set="pub16")
+                    legs["bits16"] = leg_summary(args, leg, *leg.timed(args.leg_steps, 2))
                     del leg
                 elif name == "independent_layers":
                     # NOT the reference caller's order: consecutive layers on 4 streams (layer l on stream
@@ -783,6 +938,9 @@ def main():
                         "path": "layer l on stream l % 4 (cross-layer overlap of one layer's selection with its "
                                 "neighbours' kernels; not reachable from the reference's sequential prefill)"}
                 elif name in ("s4096", "cfg2_s4096_quant", "s65536"):
+                    if f16_inputs is not None:
+                        f16_inputs = None
+                        torch.cuda.empty_cache()
                     # BASELINE configs: cfg2 (7B, S=4096, quantization only), the north star's S in {4k, 64k}
                     seq = 65536 if name == "s65536" else 4096
                     leg = Job(args, device, rank, world, seq=seq, slots=8 if seq > 16384 else None,

@@ -375,6 +375,12 @@ int rtkv_compress_layer_qk_begin(const rtkv_kv_desc* kv, const rtkv_qk_desc* q, 
 int rtkv_compress_layer_finish(const rtkv_kv_desc* kv, const rtkv_layer_params* p, const rtkv_layer_out* out,
                                int64_t out_rows, void* workspace_dev, size_t workspace_bytes, void* stream,
                                rtkv_early_stats* early_host, uint64_t seq);
+/* Spin until early_host->final_seq == seq, i.e. until the finish call's K4 has started and published
+ * the layer's final flags (RTKV_OK; read final_flags then), or timeout_us passes (RTKV_ERR_TIMEOUT).
+ * The drop-in's strict mode (RealTimePrefillCompressor(strict=True)) waits here before it returns, so a
+ * selection that timed out after the early publication raises in the layer's own call — where the
+ * reference caller's try/except falls back for that layer (modified_llama.py:144-149). */
+int rtkv_wait_final(const rtkv_early_stats* early_host, uint64_t seq, int64_t timeout_us);
 /* start_event (nullable, a hipEvent_t): recorded on the stream right before K1, in the same call —
  * the start of the drop-in's processing_time.  (Recorded from the host separately before this call,
  * the timing event cost ~4.5 us of device idle per layer; recorded here, as rtkv_compress_layer_events

@@ -418,6 +418,21 @@ int rtkv_wait_early(const rtkv_early_stats* early_host, uint64_t seq, int64_t ti
   }
 }
 
+int rtkv_wait_final(const rtkv_early_stats* early_host, uint64_t seq, int64_t timeout_us) {
+  RTKV_REQUIRE(early_host != nullptr, "null early-stats buffer");
+  const auto t0 = std::chrono::steady_clock::now();
+  for (uint32_t it = 0;; ++it) {
+    if (__atomic_load_n(&early_host->final_seq, __ATOMIC_ACQUIRE) == seq) return RTKV_OK;
+    if ((it & 255u) == 255u &&
+        std::chrono::duration_cast<std::chrono::microseconds>(std::chrono::steady_clock::now() - t0).count() >
+            timeout_us) {
+      set_error("rtkv: wait_final: the layer's K4 did not publish its final flags in time");
+      return RTKV_ERR_TIMEOUT;
+    }
+    __builtin_ia32_pause();
+  }
+}
+
 void* rtkv_host_alloc(size_t bytes) {
   void* p = nullptr;
   if (hipHostMalloc(&p, bytes, hipHostMallocCoherent | hipHostMallocMapped) != hipSuccess) return nullptr;

@@ -135,6 +135,7 @@ _SIGS = {
     "rtkv_compress_layer_early": ([c_p, c_p, c_p, c_p, c_p, c_sz, c_p, c_p, ctypes.c_uint64, c_p], c_i32),
     "rtkv_compress_layer_qk_early": ([c_p, c_p, c_p, c_p, c_p, c_sz, c_p, c_p, ctypes.c_uint64, c_p], c_i32),
     "rtkv_wait_early": ([c_p, ctypes.c_uint64, c_i64], c_i32),
+    "rtkv_wait_final": ([c_p, ctypes.c_uint64, c_i64], c_i32),
     "rtkv_compress_layer_begin": ([c_p, c_p, c_p, c_p, c_p, c_sz, c_p, c_p, ctypes.c_uint64, c_p, c_p], c_i32),
     "rtkv_compress_layer_qk_begin": ([c_p, c_p, c_p, c_p, c_p, c_sz, c_p, c_p, ctypes.c_uint64, c_p, c_p], c_i32),
     "rtkv_compress_layer_finish": ([c_p, c_p, c_p, c_i64, c_p, c_sz, c_p, c_p, ctypes.c_uint64], c_i32),

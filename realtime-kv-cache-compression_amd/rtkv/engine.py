@@ -198,6 +198,18 @@ class EarlyStatsBuffer:
             return None
         return int(e.final_flags)
 
+    def wait_final(self, seq: int, device=None) -> int:
+        """The final RTKV_FLAG_* word of call `seq` once its K4 has started and published it
+        (rtkv_wait_final); past the timeout the device is synchronised and the mirror re-read."""
+        rc = self._lib.rtkv_wait_final(self.ptr, seq, self.TIMEOUT_US)
+        if rc == L.ERR_TIMEOUT:
+            torch.cuda.synchronize(device)
+            flags = self.final_flags(seq)
+            if flags is not None:
+                return flags
+        L.check(rc, "rtkv_wait_final")
+        return int(self._view.final_flags)
+
     def wait(self, seq: int, device=None) -> L.EarlyStats:
         """The statistics of call `seq` once the device has published them.  A queue slower than the
         spin timeout (a long backlog, preemption) is not an error: the device that runs the layer is
@@ -520,6 +532,13 @@ class PendingLayer(LayerResult):
         """The layer's complete RTKV_FLAG_* word as K4 published it (no stream sync), or None when it is
         not (yet) available: no early buffer, K4 not started, or overwritten by a later layer's K4."""
         return self._early.final_flags(self._seq) if self._early is not None and self.finished else None
+
+    def wait_final_flags(self) -> int:
+        """Wait (host spin, no stream sync) until this layer's K4 has started and published the layer's
+        final flags, and return them; a layer without an early buffer syncs its stream instead."""
+        if self._early is None or not self.finished:
+            return self.final_stats_unchecked().error_flags
+        return self._early.wait_final(self._seq, self.bufs.device)
 
     def finish(self) -> "PendingLayer":
         """Allocate K'/V' [B, S', F] and the packed codes at their exact sizes and enqueue K4 into them.

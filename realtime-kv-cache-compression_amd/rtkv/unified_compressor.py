@@ -75,7 +75,14 @@ class _LazyDict(dict):
 class RealTimePrefillCompressor:
     """Prompt-guided importance → dynamic precision → selective propagation, per layer."""
 
-    def __init__(self, config, model_config=None, emit_packed: bool = True):
+    def __init__(self, config, model_config=None, emit_packed: bool = True, strict: Optional[bool] = None):
+        """strict (extension): wait in each call until the layer's K4 has published the final flags
+        (rtkv_wait_final: K2's end, no stream sync) and raise in THAT call when its selection failed after
+        the early statistics — the reference's synchronous call fails in the failing layer, where the
+        caller's try/except falls back for that layer (modified_llama.py:144-149).  strict=False returns
+        on the early statistics and reports such a layer at the next call on the device, in
+        get_overall_compression_stats, reset_compression_state or verify_pending_layers.  Default:
+        RTKV_STRICT (1 unless set to 0)."""
         self.config = config
         self.model_config = model_config
         self.importance_tracker = LayerWiseImportanceTracker(config)
@@ -98,8 +105,8 @@ class RealTimePrefillCompressor:
         # (past ~40 MB the read outlasts the host's reaction and delays K4).  RTKV_DROPIN_PREFETCH_MB
         # overrides (0: off).
         self.prefetch_bytes = int(float(os.environ.get("RTKV_DROPIN_PREFETCH_MB", "40")) * (1 << 20))
-        self._packable: Dict[tuple, bool] = {}
-  # (dtype, bits) → whether the packed codes are emitted
+        self._packable: Dict[tuple, bool] = {}  # (dtype, bits, emit_packed) → whether the codes are emitted
+        self.strict = (os.environ.get("RTKV_STRICT", "1") != "0") if strict is None else bool(strict)
 
     # ------------------------------------------------------------------ reference API
     def identify_prompt_tokens(self, input_ids: torch.Tensor, special_tokens: Optional[List[int]] = None):
@@ -169,14 +176,14 @@ class RealTimePrefillCompressor:
                                        causal=causal, key_bias=key_padding_bias)
         else:
             res = compress_layer_begin(K, V, W, params, bufs, ws, early)
-        if self.prefetch_bytes > 0 and res._early is not None:
-            # the first kept rows into the Infinity Cache while the host waits and allocates (after K2)
-            L.check(L.lib().rtkv_prefetch_kept_rows(res._finish_args[0], res._finish_args[2], self.prefetch_bytes,
-                                                    res._stream), "rtkv_prefetch_kept_rows")
         # the one host wait of the layer: the device publishes S' and the counts as soon as K2 has its
         # thresholds; the exactly-sized outputs are allocated then and K4 is enqueued into them
         prev, done = None, False
         try:
+            if self.prefetch_bytes > 0 and res._early is not None:
+                # the first kept rows into the Infinity Cache while the host waits and allocates (after K2)
+                L.check(L.lib().rtkv_prefetch_kept_rows(res._finish_args[0], res._finish_args[2], self.prefetch_bytes,
+                                                        res._stream), "rtkv_prefetch_kept_rows")
             flags = res.sizes()[2]  # the early publication's S', code bytes and flags (K2 still running)
             # the previous layer's K4 has started by now (stream order): its final flags, read before this
             # layer's K4 overwrites them, are checked after the launch (off the path to it)
@@ -195,7 +202,10 @@ class RealTimePrefillCompressor:
             self._verify(prev, prev_flags)
         st = res.stats()
         if res._early is not None:
-            self._unverified[K.device] = (res, layer_idx)
+            if self.strict:  # K2's end (K4's first wave publishes the final flags): raise in this call
+                check_flags(res.wait_final_flags(), f"compress_layer_kv_cache (layer {layer_idx})")
+            else:
+                self._unverified[K.device] = (res, layer_idx)
         selected_keys, selected_values = res.kv()
         Sp = st.max_kept
         scores = bufs.scores
@@ -290,8 +300,7 @@ class RealTimePrefillCompressor:
 
     def get_overall_compression_stats(self) -> Dict:
         """Aggregate of every processed layer (unified_compressor.py:174-230)."""
-        for device in list(self._unverified):
-            self._verify_previous(device)
+        self.verify_pending_layers()
         if not self.layer_states:
             return {}
         states = list(self.layer_states.values())
@@ -324,10 +333,22 @@ class RealTimePrefillCompressor:
             },
         }
 
+    def verify_pending_layers(self):
+        """Raise now if a layer returned before its K4 ran (strict=False) turned out invalid: a selection
+        that timed out after the early statistics (its K'/V' are NaN rows) or undersized outputs.  Call
+        it when a forward ends if the compressor is not strict; get_overall_compression_stats and
+        reset_compression_state call it too."""
+        for device in list(self._unverified):
+            self._verify_previous(device)
+
     def reset_compression_state(self):
+        """unified_compressor.py:232-235.  A pending layer that failed after it was returned (strict=False)
+        is raised here, after the state is cleared, rather than dropped with it."""
+        pending, self._unverified = self._unverified, {}
         self.layer_states = {}
         self.importance_tracker.layer_scores = {}
-        self._unverified = {}
+        for device, prev in pending.items():
+            self._verify(prev, prev[0].final_flags())
 
     def estimate_memory_usage(self) -> Dict[str, float]:
         try:

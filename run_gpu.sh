@@ -18,11 +18,12 @@ for s in ${STEPS:-smoke pytest bench}; do
     smoke)  step smoke 300 python -c "import __graft_entry__ as g; g.build(); g.smoke()" ;;
     pytest) step pytest_gpu 1200 python -u -m pytest tests -m gpu -q -x -p no:cacheprovider --timeout 120 --timeout-method thread ;;
     shardp) step shardp 900 python -u -m pytest tests/test_gpu_shard_procs.py tests/test_gpu_shard.py -q -x -p no:cacheprovider --timeout 300 --timeout-method thread ;;
-    fused)  step fused 600 python -u -m pytest tests/test_gpu_fused.py tests/test_gpu_early.py -q -x -p no:cacheprovider --timeout 120 --timeout-method thread ;;
+    early)  step early 600 python -u -m pytest tests/test_gpu_early.py -q -x -p no:cacheprovider --timeout 120 --timeout-method thread ;;
     targ)   step targ 900 python -u -m pytest ${TESTS:-tests/test_gpu_f32_masks.py} -q -x -p no:cacheprovider --timeout 120 --timeout-method thread ;;
     profprefill) step profprefill 900 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/profprefill -o run -- python3 bench.py --steps 1 --warmup 1 --legs prefill_7b --prefill-modes ${PREFILL_MODES:-none,fused} --cpu-baseline-seconds 0 ;;
     pytestall) step pytest_gpu 1200 python -m pytest tests -m gpu -q -p no:cacheprovider ;;
     bench)  step bench 600 python bench.py ${BENCH_ARGS:-} ;;
+    gpucount) step gpucount 120 python -c "import bench, json; print(json.dumps({'visible_gpu_count': bench.visible_gpu_count()}))" ;;
     prof)   step rocprof 900 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python3 bench.py --steps 5 --warmup 1 --legs none --cpu-baseline-seconds 0 ;;
     pmc)    step pmc 900 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmc -o fetch -- python3 bench.py --steps 2 --warmup 1 --legs none --cpu-baseline-seconds 0 ;;
     shard1) step shard1 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29512 bench.py --sharded --steps 3 --warmup 1 --legs none --cpu-baseline-seconds 0 ;;

@@ -81,7 +81,8 @@ def test_early_stats_equal_the_final_block(dtype, B, S, H, D, ratio, expect):
     assert torch.equal(bufs_e.packed_v[: ref.total_packed_bytes], bufs_r.packed_v[: ref.total_packed_bytes])
 
 
-def test_drop_in_returns_before_the_layer_finishes_and_stays_correct():
+@pytest.mark.parametrize("strict", [True, False])
+def test_drop_in_returns_before_the_layer_finishes_and_stays_correct(strict):
     """The drop-in over consecutive layers (one early-stats buffer, rising sequence numbers): every
     layer's K'/V' and lazily read statistics equal a run that synchronises after each layer."""
     import rtkv
@@ -96,7 +97,7 @@ def test_drop_in_returns_before_the_layer_finishes_and_stays_correct():
         W = synth.attention_slice(70 + l, 1, H, S, P, dtype)
         ins.append((_dev(K, dtype), _dev(V, dtype), _dev(W, dtype)))
     ids = torch.zeros(1, S, dtype=torch.long, device="cuda")
-    a, b = rtkv.RealTimePrefillCompressor(cfg), rtkv.RealTimePrefillCompressor(cfg)
+    a, b = rtkv.RealTimePrefillCompressor(cfg, strict=strict), rtkv.RealTimePrefillCompressor(cfg)
     got = [a.compress_layer_kv_cache(K, V, W, ids, l) for l, (K, V, W) in enumerate(ins)]
     torch.cuda.synchronize()
     for l, (K, V, W) in enumerate(ins):
@@ -186,16 +187,80 @@ def test_lookback_timeout_after_the_early_publication_is_caught():
         res.final_stats()
 
 
+def test_strict_drop_in_raises_a_late_timeout_in_the_failing_layer():
+    """strict (the default): the call whose selection fails after the early statistics raises itself,
+    so the reference caller's try/except (modified_llama.py:144-149) falls back for THAT layer: its
+    uncompressed K/V are used, nothing NaN reaches attention, layer_states holds only the good layers
+    and the next layers compress normally."""
+    import rtkv
+    from rtkv import _lib as L
+    S, F, P, cfg, Kd, Vd, Wd = _lookback_inputs()
+    ids = torch.zeros(1, S, dtype=torch.long, device="cuda")
+    comp = rtkv.RealTimePrefillCompressor(cfg, strict=True)
+    assert rtkv.RealTimePrefillCompressor(cfg).strict  # the default
+
+    def caller(layer_idx):
+        """modified_llama.py:102-149 in outline: compress, or print and keep the full K/V on any error."""
+        try:
+            k, v, _ = comp.compress_layer_kv_cache(Kd, Vd, Wd, ids, layer_idx)
+            return k, v, False
+        except Exception as e:  # noqa: BLE001 — the reference's catch-all
+            print(f"Compression failed for layer {layer_idx}: {e}")
+            return Kd, Vd, True
+
+    outs = []
+    for layer in range(4):
+        comp._test_flags = L.TEST_WITHHOLD_LOOKBACK if layer == 1 else 0
+        outs.append(caller(layer))
+    comp._test_flags = 0
+    torch.cuda.synchronize()
+    assert [o[2] for o in outs] == [False, True, False, False]
+    assert outs[1][0] is Kd
+    for k, v, _ in outs:
+        assert not torch.isnan(k.float()).any() and not torch.isnan(v.float()).any()
+    assert sorted(comp.layer_states) == [0, 2, 3]
+    ref = rtkv.RealTimePrefillCompressor(cfg, strict=False)
+    r2, _, _ = ref.compress_layer_kv_cache(Kd, Vd, Wd, ids, 2)
+    torch.cuda.synchronize()
+    assert torch.equal(outs[2][0].view(torch.int16), r2.view(torch.int16))
+    assert comp.get_overall_compression_stats()["total_layers_processed"] == 3
+
+
+def test_non_strict_late_timeout_of_the_last_layer_raises_at_reset():
+    """strict=False: a failing LAST layer of a forward must not vanish with reset_compression_state()
+    (ADVICE r4): reset clears the state and then raises; verify_pending_layers() raises the same way
+    before any reset."""
+    import rtkv
+    from rtkv import _lib as L
+    S, F, P, cfg, Kd, Vd, Wd = _lookback_inputs()
+    ids = torch.zeros(1, S, dtype=torch.long, device="cuda")
+    for hook in ("reset", "verify"):
+        comp = rtkv.RealTimePrefillCompressor(cfg, strict=False)
+        comp.compress_layer_kv_cache(Kd, Vd, Wd, ids, 0)
+        comp._test_flags = L.TEST_WITHHOLD_LOOKBACK
+        comp.compress_layer_kv_cache(Kd, Vd, Wd, ids, 1)  # returns on its clean early statistics
+        comp._test_flags = 0
+        with pytest.raises(RuntimeError, match="layer 1"):
+            comp.reset_compression_state() if hook == "reset" else comp.verify_pending_layers()
+        if hook == "reset":
+            assert comp.layer_states == {} and comp.importance_tracker.layer_scores == {}
+        else:
+            assert sorted(comp.layer_states) == [0]
+        comp.reset_compression_state()  # nothing pending any more
+        torch.cuda.synchronize()
+
+
 def test_drop_in_reports_a_late_timeout_at_the_next_call():
-    """The drop-in returns on the early statistics; a layer whose selection failed after them is
-    reported by the next call on the device (and by get_overall_compression_stats) from K4's host
-    flags, without a stream sync per layer, and the layer is dropped from layer_states.  The layers
-    after it are unaffected."""
+    """strict=False: the drop-in returns on the early statistics; a layer whose selection failed after
+    them is reported by the next call on the device (and by get_overall_compression_stats) from K4's
+    host flags, without a stream sync per layer, and the layer is dropped from layer_states.  The
+    layers after it are unaffected.  (A documented deviation from the reference's synchronous call,
+    INTEGRATION.md §4; strict=True, the default, raises in the failing layer.)"""
     import rtkv
     S, F, P, cfg, Kd, Vd, Wd = _lookback_inputs()
     ids = torch.zeros(1, S, dtype=torch.long, device="cuda")
     from rtkv import _lib as L
-    comp = rtkv.RealTimePrefillCompressor(cfg)
+    comp = rtkv.RealTimePrefillCompressor(cfg, strict=False)
     k0, v0, _ = comp.compress_layer_kv_cache(Kd, Vd, Wd, ids, 0)  # good layer
     comp._test_flags = L.TEST_WITHHOLD_LOOKBACK
     k1, v1, _ = comp.compress_layer_kv_cache(Kd, Vd, Wd, ids, 1)  # returns on its (clean) early statistics
@@ -206,7 +271,7 @@ def test_drop_in_reports_a_late_timeout_at_the_next_call():
     assert torch.isnan(k1.float()).all()
     k3, v3, _ = comp.compress_layer_kv_cache(Kd, Vd, Wd, ids, 3)
     torch.cuda.synchronize()
-    ref = rtkv.RealTimePrefillCompressor(cfg)
+    ref = rtkv.RealTimePrefillCompressor(cfg, strict=False)
     r3, _, _ = ref.compress_layer_kv_cache(Kd, Vd, Wd, ids, 3)
     assert torch.equal(k3.view(torch.int16), r3.view(torch.int16))
     assert sorted(comp.layer_states) == [0, 3]

@@ -15,10 +15,6 @@
 
 namespace rtkv {
 void set_error(const std::string& m) { fprintf(stderr, "%s\n", m.c_str()); }
-// the fused launch (fused_*.hip) is not part of this probe
-int launch_fused_f32(const FinalizeArgs&, void*, const QuantArgs&, hipStream_t) { return RTKV_ERR_UNSUPPORTED; }
-int launch_fused_f16(const FinalizeArgs&, void*, const QuantArgs&, hipStream_t) { return RTKV_ERR_UNSUPPORTED; }
-int launch_fused_bf16(const FinalizeArgs&, void*, const QuantArgs&, hipStream_t) { return RTKV_ERR_UNSUPPORTED; }
 }  // namespace rtkv
 
 #define CK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { printf("%s: %s\n", #x, hipGetErrorString(e_)); return 1; } } while (0)
