@@ -201,6 +201,8 @@ def parse():
     ap.add_argument("--params", default="coverage", choices=sorted(PARAM_SETS),
                     help="compression parameters: coverage (8/4/2 bits, the default workload) or pub16 (the "
                          "reference's published 16/8/4 run)")
+    ap.add_argument("--quant-only", action="store_true",
+                    help="every token kept (RTKV_NO_SELECTION): BASELINE config 2's quantization-only path")
     ap.add_argument("--no-same-workload", action="store_true",
                     help="N > 1: skip the same-workload single-GPU reference on rank 0")
     ap.add_argument("--no-packed", action="store_true", help="skip the packed-code output")
@@ -279,7 +281,7 @@ class Job:
     another job's resident inputs instead of generating new ones."""
 
     def __init__(self, args, device, rank, world, dtype=None, emit_dequant=None, emit_packed=None, inputs=None,
-                 seq=None, slots=None, quant_only=False, param_set=None):
+                 seq=None, slots=None, quant_only=None, param_set=None):
         """seq: tokens (default --seq); slots: distinct input/output sets, layer l uses slot l % slots
         (bounds the memory of long-sequence legs; default one per layer); ``inputs`` given: layer l reads
         inputs[l % len(inputs)] and only the outputs cycle over ``slots``; quant_only: every token kept
@@ -292,7 +294,7 @@ class Job:
         self.F = self.H * self.D
         self.S_total = self.S * world
         self.P = rtkv.prompt_length(self.S_total)
-        self.quant_only = quant_only
+        self.quant_only = quant_only = getattr(args, "quant_only", False) if quant_only is None else quant_only
         self.param_set = param_set = param_set or getattr(args, "params", "coverage")
         self.cfg = rtkv.CompressionConfig(**PARAM_SETS[param_set], num_hidden_layers=args.layers)
         self.bits = (self.cfg.low_precision_bits, self.cfg.medium_precision_bits, self.cfg.high_precision_bits)
@@ -484,6 +486,17 @@ def drop_in_leg(args, job, steps, warmup):
     # the raw driver on the same inputs right before, in the same device state (legs that ran before
     # this one leave the device warmer: the drop-in's margin is measured against this, not the main line)
     raw_ms, _ = job.timed(steps, 1)
+    # ... and timed like the drop-in: one prefill per timed region (sync, 32 layers, sync), so both pay the
+    # same per-prefill start (the first launch after an idle device) and end (the final sync)
+    raw_sample = []
+    for it in range(warmup + steps):
+        torch.cuda.synchronize(job.device)
+        t0 = time.perf_counter()
+        job.step()
+        torch.cuda.synchronize(job.device)
+        if it >= warmup:
+            raw_sample.append((time.perf_counter() - t0) * 1e3)
+    raw_sample_ms = sum(raw_sample) / len(raw_sample)
     out = {}
     for strict in (True, False):
         comp = rtkv.RealTimePrefillCompressor(job.cfg, emit_packed=job.emit_packed, strict=strict)
@@ -502,12 +515,17 @@ def drop_in_leg(args, job, steps, warmup):
         w, d = sum(wall) / len(wall), sum(span) / len(span)
         out["strict" if strict else "non_strict"] = {
             "ttft_ms": round(w, 4), "wall_ms_per_layer": round(w / args.layers, 4),
-            "ttft_device_span_ms": round(d, 4), "over_raw_driver_ms": round(w - raw_ms, 4)}
+            "ttft_device_span_ms": round(d, 4), "over_raw_driver_ms": round(w - raw_ms, 4),
+            "over_raw_driver_per_prefill_ms": round(w - raw_sample_ms, 4)}
         del comp
     s_ = out["strict"]
     return {"ttft_ms": s_["ttft_ms"], "ms_per_layer": s_["wall_ms_per_layer"],
             "ttft_device_span_ms": s_["ttft_device_span_ms"], "wall_ms_per_step": s_["ttft_ms"],
-            "raw_driver_ms_per_step_same_state": round(raw_ms, 4), "modes": out, "steps": steps,
+            "raw_driver_ms_per_step_same_state": round(raw_ms, 4),
+            "raw_driver_ms_per_prefill_same_state": round(raw_sample_ms, 4),
+            "raw_driver_note": "ms_per_step: steps back to back (the main line's timing); per_prefill: each step "
+                               "alone between two syncs, as the drop-in's wall time is taken",
+            "modes": out, "steps": steps,
             "path": "rtkv.RealTimePrefillCompressor.compress_layer_kv_cache (dequant + packed, one host wait "
                     "per layer for the output shape; strict = the default)"}
 
@@ -645,6 +663,8 @@ def workload_key(args):
            "importance": args.importance}
     if getattr(args, "params", "coverage") != "coverage":  # summaries before round 5 are all "coverage"
         key["params"] = args.params
+    if getattr(args, "quant_only", False):
+        key["quant_only"] = True
     return key
 
 
@@ -654,11 +674,10 @@ def pmc_kernels(args):
     WRITE_SIZE passes of `bench.py --legs none`), or (None, None)."""
     import glob
     want = workload_key(args)
-    legacy = dict(want, dtype="float16")  # round-1 summaries predate the workload key (f16 default)
     for path in sorted(glob.glob(os.path.join(REPO, "profiles", "*_pmc.json")), reverse=True):
         with open(path) as f:
             doc = json.load(f)
-        if doc.get("workload", legacy if "workload" not in doc else None) == want:
+        if doc.get("workload") == want:  # round-1 summaries carry no workload key: never matched
             return doc["kernels"], os.path.relpath(path, REPO)
     return None, None
 
@@ -739,7 +758,7 @@ def roofline_objects(args, job, kus, k4_bytes):
 def job_args(args, job):
     """args as they would read for a bench run of exactly `job`'s workload (the PMC summary key)."""
     a = argparse.Namespace(**vars(args))
-    a.seq, a.dtype, a.params = job.S, str(job.dtype).split(".")[-1], job.param_set
+    a.seq, a.dtype, a.params, a.quant_only = job.S, str(job.dtype).split(".")[-1], job.param_set, job.quant_only
     a.no_dequant, a.no_packed = not job.emit_dequant, not job.emit_packed
     return a
 
@@ -873,7 +892,8 @@ def main():
                                    f"{' (fused Q/LSE importance)' if args.importance == 'qk' else ''}, {args.layers} layers, "
                                    f"S={job.S * world} ({job.S}/rank), {args.heads}x{args.head_dim}, {args.dtype}, "
                                    f"P={job.P}, bits {'/'.join(map(str, job.bits[::-1]))}, {getattr(job, 'param_set', 'coverage')} "
-                                   f"parameters, ratios .8/.6/.4, {outs} outputs"
+                                   f"parameters, {'no selection (every token kept)' if getattr(job, 'quant_only', False) else 'ratios .8/.6/.4'}, "
+                                   f"{outs} outputs"
                                    + (f", {job.in_slots} distinct layer inputs cycled" if getattr(job, "in_slots", args.layers) < args.layers else ""),
                        "model": f"{args.model} (KV shapes only)", "global_batch": 1, "seq_len": job.S * world,
                        "parallelism": f"sequence-shard x{world}" if world > 1 else "single GPU",

@@ -334,7 +334,7 @@ __device__ __forceinline__ void row_minmax(const Chunk<DT> (&raw)[NCH], int nch,
 // per chunk each cover every other 16 B of the wave's 2 KiB span — partial 128-byte lines, which the
 // memory side counted as ~8 % extra write and ~5 % extra read traffic (profiles/r03_k4_traffic_split.json).
 // Through the stage, each store instruction writes 1 KiB contiguous (lane l: bytes 16l..16l+15).
-template <int DT, int NCH, bool CONTIG, bool FULL>
+template <int DT, int NCH, bool CONTIG, bool FULL, bool PK_ONLY = false>
 __device__ __forceinline__ void emit_row(const Chunk<DT> (&raw)[NCH], const RowParams& rp, bool row_nan, int w,
                                        typename Dt<DT>::S* orow, const int (&out_off)[NCH], uint8_t* pk, int nch,
                                        int lane, bool emit_deq, bool emit_pk, float4* stage = nullptr) {
@@ -406,7 +406,8 @@ __device__ __forceinline__ void emit_row(const Chunk<DT> (&raw)[NCH], const RowP
   };
   auto by_width = [&](auto ftag) {
     auto go = [&](auto wtag) {
-      if (emit_deq) process(wtag, ftag, std::true_type{});
+      if constexpr (PK_ONLY) process(wtag, ftag, std::false_type{});
+      else if (emit_deq) process(wtag, ftag, std::true_type{});
       else process(wtag, ftag, std::false_type{});
     };
     switch (w) {
@@ -443,7 +444,8 @@ __device__ __forceinline__ void emit_row(const Chunk<DT> (&raw)[NCH], const RowP
           default: native(std::integral_constant<int, 16>{}, dtag); break;
         }
       };
-      if (emit_deq) by_w(std::true_type{});
+      if constexpr (PK_ONLY) by_w(std::false_type{});
+      else if (emit_deq) by_w(std::true_type{});
       else by_w(std::false_type{});
       return;
     }
@@ -507,8 +509,11 @@ __device__ __forceinline__ bool k4_layer_gate(const QuantArgs& a) {
 // Row geometry shared by every task of a launch: element f of a row lives at (f / D) * stride_h + f % D.
 // CONTIG (stride_h == D on input and output) makes that plain f.  FULL: the row is exactly NCH*64
 // chunks of 8 (F a multiple of 512), so no lane is idle and packed rows stay 16-byte aligned.
-template <int DT, int NCH, bool CONTIG, bool FULL>
-__global__ __launch_bounds__(256, (DT == RTKV_F32 && NCH == 8 && FULL && CONTIG) ? 4 : 2) void quant_rows_kernel(QuantArgs a) {
+// PKW > 0 (compile time): packed codes + scale/zero-point only (no dequantized K'/V': the decode and packed
+// consumers' mode), the dequantization path compiled out, at a launch bound of PKW waves per SIMD.
+template <int DT, int NCH, bool CONTIG, bool FULL, int PKW = 0>
+__global__ __launch_bounds__(256, PKW ? PKW : ((DT == RTKV_F32 && NCH == 8 && FULL && CONTIG) ? 4 : 2)) void quant_rows_kernel(QuantArgs a) {
+  constexpr bool PK_ONLY = PKW > 0;
   using S_ = typename Dt<DT>::S;
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -537,8 +542,8 @@ __global__ __launch_bounds__(256, (DT == RTKV_F32 && NCH == 8 && FULL && CONTIG)
   }
   const rtkv_batch_stats* bst = a.stats ? reinterpret_cast<const rtkv_batch_stats*>(a.stats + 1) : nullptr;
   if (k4_layer_gate<DT>(a)) return;  // buffer sizes, final flags, a timed-out selection
-  const bool emit_deq = a.out.k_out_dev != nullptr;
-  const bool emit_pk = a.out.packed_k_dev != nullptr;
+  const bool emit_deq = !PK_ONLY && a.out.k_out_dev != nullptr;
+  const bool emit_pk = PK_ONLY || a.out.packed_k_dev != nullptr;
   // per-lane in-row offsets of each chunk (task independent)
   int in_off[NCH], out_off[NCH];
 #pragma unroll
@@ -556,7 +561,7 @@ __global__ __launch_bounds__(256, (DT == RTKV_F32 && NCH == 8 && FULL && CONTIG)
   }
   auto valid = [&](int k) { return FULL || (k * 64 + lane) < nch; };
   float4* stage = nullptr;  // fp32 dequantized rows go out through a wave-private LDS stage (emit_row)
-  if constexpr (DT == RTKV_F32 && CONTIG && FULL) {
+  if constexpr (DT == RTKV_F32 && CONTIG && FULL && !PK_ONLY) {
     __shared__ float4 k4_stage[4][128];  // 256-thread workgroups: 4 waves × 2 KiB
     stage = k4_stage[wave & 3];
   }
@@ -622,7 +627,8 @@ __global__ __launch_bounds__(256, (DT == RTKV_F32 && NCH == 8 && FULL && CONTIG)
     if (a.out.scale_zp_dev && lane < 2) a.out.scale_zp_dev[sz_idx + lane] = lane == 0 ? rp.scale : rp.zp;
     if (emit_pk && !one_row) roff = a.out.row_offset_dev[(int64_t)b * cap + r];
     uint8_t* pk = emit_pk ? (which ? a.out.packed_v_dev : a.out.packed_k_dev) + roff : nullptr;
-    emit_row<DT, NCH, CONTIG, FULL>(raw, rp, row_nan, w, orow, out_off, pk, nch, lane, emit_deq, emit_pk, stage);
+    emit_row<DT, NCH, CONTIG, FULL, PK_ONLY>(raw, rp, row_nan, w, orow, out_off, pk, nch, lane, emit_deq, emit_pk,
+                                             stage);
     wrote = true;
   }
   stamp_end(a.t_end, wrote);
@@ -793,6 +799,21 @@ __global__ __launch_bounds__(256) void quant_rows_generic_kernel(QuantArgs a) {
 template <int DT, bool CONTIG>
 static int launch_quant_vec(const QuantArgs& a, int64_t nch, dim3 grid, hipStream_t st) {
   const int per_lane = (int)((nch + 63) / 64);
+  // packed-only: 0 = the runtime-mode kernel, else the compiled-out variant at that wave bound (A/B knob)
+  static const int pk_waves = [] {
+    const char* e = getenv("RTKV_K4_PK_WAVES");
+    return e ? atoi(e) : 4;
+  }();
+  if (!a.out.k_out_dev && a.out.packed_k_dev && pk_waves > 0 && DT != RTKV_F32) {
+#define RTKV_QP(N, WV)                                                                             \
+    if (nch == (int64_t)N * 64 && pk_waves == WV) {                                                \
+      hipLaunchKernelGGL((quant_rows_kernel<DT, N, CONTIG, true, WV>), grid, dim3(256), 0, st, a); \
+      RTKV_HIP_CHECK(hipGetLastError());                                                           \
+      return RTKV_OK;                                                                              \
+    }
+    RTKV_QP(8, 4) RTKV_QP(10, 4) RTKV_QP(8, 5)
+#undef RTKV_QP
+  }
 #define RTKV_Q(N)                                                                              \
   if (nch == (int64_t)N * 64) {                                                                \
     hipLaunchKernelGGL((quant_rows_kernel<DT, N, CONTIG, true>), grid, dim3(256), 0, st, a);   \

@@ -78,6 +78,7 @@ struct FastHead {                  // zeroed before the launch (K1 or a memset):
 struct FastPartial {               // phase 1, per workgroup (complete before its counts word)
   double ssum;
   uint32_t kmn, kmx;               // score key range
+  double m2;                       // quantization-only kernel: Σ (s - workgroup mean)^2
 };
 struct FastLayout {
   FastHead* head;                  // zeroed
@@ -1059,6 +1060,143 @@ __device__ __forceinline__ void k2_body(const FastArgs& g, uint32_t* hist_lds) {
   K2_WG(5);
   compact_phase(g, s, l, i, valid, s_selw);
   K2_WG(8);
+}
+
+// ------------------------------------------------------------------------------------ quantization only
+// RTKV_NO_SELECTION (BASELINE config 2: the quantizer alone, dynamic_quantization.py:128-196, every token
+// kept): no thresholds, no ranking.  Kept row = token index, so the only exchange between workgroups is
+// the exclusive prefix of packed row bytes, which follows from the predecessors' class counts — published
+// straight from registers right after the scores (one tagged word per workgroup, one look-back round
+// trip).  The last workgroup also gathers every workgroup's partials (score sum, range and Σ(s - mean_j)^2,
+// combined exactly in double: M2 = Σ M2_j + n_j·(mean_j − mean)^2) for the layer statistics and the
+// early host mirror.  Chain: min/max partials → scores → counts word → look-back → stores (about three
+// round trips, against the selection kernel's seven).
+template <bool HAS_T2, int DT>
+__global__ __launch_bounds__(kST) void fsel_quant_kernel(FastArgs g) {
+  const FinalizeArgs& a = g.f;
+  __shared__ uint32_t s_f3[3][kSW];
+  __shared__ double s_d[kSW];
+  __shared__ uint32_t s_k[2][kSW];
+  __shared__ uint64_t s_base;
+  const int t = threadIdx.x, lane = t & (kWave - 1), wid = t / kWave;
+  const int S = (int)a.S;
+  const int G = (S + kST - 1) / kST;
+  const int blk = blockIdx.x;
+  const int i = blk * kST + t;
+  const bool valid = i < S;
+  const float Ai = valid ? a.A[i] : 0.f;
+  const float T2i = (HAS_T2 && valid) ? a.T2[i] : 0.f;
+  float mn, mx;
+  amin_amax(a, mn, mx);
+  const float den = Dt<DT>::rnd(mx - mn), eps = Dt<DT>::rnd(1e-8f);
+  float s = 0.f;
+  int l = 0;
+  if (valid) {
+    s = token_score<DT, HAS_T2>(a, i, Ai, T2i, mn, den, eps);
+    l = class_of(s, a.p);
+  }
+  // ---- per-class ranks in token order and the workgroup's class counts, published at once
+  bool f3[3];
+#pragma unroll
+  for (int c = 0; c < 3; ++c) f3[c] = valid & (l == c);
+  uint32_t r3[3], t3[3];
+  block_flag_ranks<3>(f3, r3, t3, s_f3);
+  if (t == 0) st_sc1(&g.L.head->part[blk], kTag | (uint64_t)t3[0] | ((uint64_t)t3[1] << 11) | ((uint64_t)t3[2] << 22));
+  // ---- the predecessors' counts (wave 0) while the others store the per-token outputs
+  if (wid == 0) {
+    const uint64_t w = poll_tagged(g.L.head->part, 1, blk, g.spin_limit, a.stats);
+    const uint64_t ps = wave_sum(lane < blk ? from11(w & ~kTag, 3) : 0ull);
+    if (lane == 0) s_base = ps;
+  }
+  if (valid) {
+    a.scores[i] = s;
+    a.labels[i] = (uint8_t)l;
+    a.mask[i] = 1;
+    if (i < a.row_capacity) {
+      a.kept_index[i] = i;
+      if (a.row_label) a.row_label[i] = (uint8_t)l;
+    }
+  }
+  // ---- workgroup partials: score sum and key range, then Σ (s - workgroup mean)^2
+  const int nb = min(kST, S - blk * kST);
+  {
+    const double sw = wave_sum(valid ? (double)s : 0.0);
+    uint32_t kmn = valid ? score_key(s) : 0xffffffffu, kmx = valid ? score_key(s) : 0u;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      kmn = min(kmn, (uint32_t)__shfl_xor((int)kmn, o, kWave));
+      kmx = max(kmx, (uint32_t)__shfl_xor((int)kmx, o, kWave));
+    }
+    if (lane == 0) { s_d[wid] = sw; s_k[0][wid] = kmn; s_k[1][wid] = kmx; }
+  }
+  __syncthreads();
+  double bsum = s_d[lane & (kSW - 1)];
+  uint32_t bmn = s_k[0][lane & (kSW - 1)], bmx = s_k[1][lane & (kSW - 1)];
+#pragma unroll
+  for (int o = kSW / 2; o > 0; o >>= 1) {
+    bsum += __shfl_xor(bsum, o, kWave);
+    bmn = min(bmn, (uint32_t)__shfl_xor((int)bmn, o, kWave));
+    bmx = max(bmx, (uint32_t)__shfl_xor((int)bmx, o, kWave));
+  }
+  const double bmean = bsum / (double)nb;
+  const double dl = (double)s - bmean;
+  const double m2w = wave_sum(valid ? dl * dl : 0.0);
+  int64_t rb[3];  // (s_base: wave 0's look-back, published by the barrier above)
+#pragma unroll
+  for (int q = 0; q < 3; ++q) rb[q] = row_bytes(a, q);
+  __syncthreads();
+  if (lane == 0) s_d[wid] = m2w;
+  if (valid && a.row_offset && i < a.row_capacity)
+    a.row_offset[i] = ((int64_t)r3[0] + fld(s_base, 0)) * rb[0] + ((int64_t)r3[1] + fld(s_base, 1)) * rb[1] +
+                      ((int64_t)r3[2] + fld(s_base, 2)) * rb[2];
+  __syncthreads();
+  if (wid == 0) {
+    double m2 = s_d[lane & (kSW - 1)];
+#pragma unroll
+    for (int o = kSW / 2; o > 0; o >>= 1) m2 += __shfl_xor(m2, o, kWave);
+    if (lane == 0) {
+      FastPartial* pp = g.L.part + blk;
+      st_sc1(&pp->ssum, bsum);
+      st_sc1(&pp->m2, m2);
+      st_sc1(&pp->kmn, bmn);
+      st_sc1(&pp->kmx, bmx);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      st_sc1(&g.L.head->ready[blk], kTag);
+    }
+  }
+  if (blk != G - 1 || wid != 0) return;
+  // ---- the last workgroup: every workgroup's counts and partials → the layer statistics
+  const uint64_t wc = poll_tagged(g.L.head->part, 1, G, g.spin_limit, a.stats);
+  const uint64_t cnt = wave_sum(lane < G ? from11(wc & ~kTag, 3) : 0ull);
+  (void)poll_tagged(g.L.head->ready, 1, G, g.spin_limit, a.stats);
+  double ps = 0.0, pm2 = 0.0;
+  uint32_t pmn = 0xffffffffu, pmx = 0u;
+  int nj = 0;
+  if (lane < G) {
+    const FastPartial* pp = g.L.part + lane;
+    ps = ld_sc1(&pp->ssum);
+    pm2 = ld_sc1(&pp->m2);
+    pmn = ld_sc1(&pp->kmn);
+    pmx = ld_sc1(&pp->kmx);
+    nj = min(kST, S - lane * kST);
+  }
+  double ssum = ps;
+#pragma unroll
+  for (int o = kWave / 2; o > 0; o >>= 1) {
+    ssum += __shfl_xor(ssum, o, kWave);
+    pmn = min(pmn, (uint32_t)__shfl_xor((int)pmn, o, kWave));
+    pmx = max(pmx, (uint32_t)__shfl_xor((int)pmx, o, kWave));
+  }
+  const double mean = ssum / (double)S;
+  const double dj = nj ? ps / (double)nj - mean : 0.0;
+  const double M2 = wave_sum(lane < G ? pm2 + (double)nj * dj * dj : 0.0);
+  if (lane != 0) return;
+  rtkv_layer_stats* hs = a.stats;
+  rtkv_batch_stats* bs = reinterpret_cast<rtkv_batch_stats*>(hs + 1);
+  const int64_t ccount[3] = {(int64_t)fld(cnt, 0), (int64_t)fld(cnt, 1), (int64_t)fld(cnt, 2)};
+  publish_stats(g, false, ssum, pmn, pmx, ccount, ccount);
+  hs->score_m2 = M2;
+  bs->kept_score_sum = ssum;
 }
 
 template <int TPT, bool HAS_T2, int DT>

@@ -31,6 +31,16 @@ template <int TPT, bool HAS_T2, int DT> static int launch_fsel(const FastArgs& g
   return RTKV_OK;
 }
 
+template <bool HAS_T2> static int launch_fsel_quant(const FastArgs& g, int G, hipStream_t st) {
+  switch (g.f.a_dtype) {
+    case RTKV_F16: hipLaunchKernelGGL((fsel_quant_kernel<HAS_T2, RTKV_F16>), dim3(G), dim3(kST), 0, st, g); break;
+    case RTKV_BF16: hipLaunchKernelGGL((fsel_quant_kernel<HAS_T2, RTKV_BF16>), dim3(G), dim3(kST), 0, st, g); break;
+    default: hipLaunchKernelGGL((fsel_quant_kernel<HAS_T2, RTKV_F32>), dim3(G), dim3(kST), 0, st, g); break;
+  }
+  RTKV_HIP_CHECK(hipGetLastError());
+  return RTKV_OK;
+}
+
 template <int TPT, bool HAS_T2> static int launch_fsel_dt(const FastArgs& g, int G, hipStream_t st) {
   switch (g.f.a_dtype) {
     case RTKV_F16: return launch_fsel<TPT, HAS_T2, RTKV_F16>(g, G, st);
@@ -49,6 +59,10 @@ int launch_select_fast(const FinalizeArgs& f, void* ws, bool zeroed, hipStream_t
   // All G <= 32 workgroups (1024 threads, 64 KB of LDS: one per CU) are resident at once, which the
   // waits of phases 2 and 3 rely on; a busy GPU only delays the last ones.
   const int G = (int)((f.S + kST - 1) / kST);
+  // quantization only (RTKV_NO_SELECTION): scores, classes and row offsets, no selection phases
+  // (RTKV_SELECT_QUANT_FULL keeps the selection kernel's mode 2 for A/B checks)
+  static const bool quant_full = getenv("RTKV_SELECT_QUANT_FULL") != nullptr;
+  if (f.mode_select == 2 && !quant_full) return f.T2 ? launch_fsel_quant<true>(g, G, st) : launch_fsel_quant<false>(g, G, st);
   if (f.S <= 16 * kST) return f.T2 ? launch_fsel_dt<16, true>(g, G, st) : launch_fsel_dt<16, false>(g, G, st);
   return f.T2 ? launch_fsel_dt<32, true>(g, G, st) : launch_fsel_dt<32, false>(g, G, st);
 }

@@ -32,6 +32,8 @@ CASES = [  # dtype, B, S, H, D, ratio, expect: "complete" | "fallback" | "unpubl
     ("float16", 1, 2000, 4, 32, 0.0001, "fallback"),    # U = 1 bit: nothing fits, the top-10% fallback
     ("float16", 2, 1024, 4, 32, 0.6, "unpublished"),    # B > 1: the pipeline K2
     ("float16", 1, 40000, 4, 32, 0.6, "unpublished"),   # S > 32768: the pipeline K2
+    ("float32", 1, 16384, 32, 128, 1.0, "quant"),       # RTKV_NO_SELECTION: the quantization-only K2
+    ("bfloat16", 1, 3001, 4, 64, 1.0, "quant"),
 ]
 
 
@@ -48,7 +50,8 @@ def test_early_stats_equal_the_final_block(dtype, B, S, H, D, ratio, expect):
     cfg = rtkv.CompressionConfig(alpha=0.8, beta=0.1, gamma=0.1, theta_h=0.4, theta_m=0.25, num_hidden_layers=1,
                                  layer_weights=[1.0], high_precision_bits=8, medium_precision_bits=4,
                                  low_precision_bits=2)
-    params = rtkv.params_from_config(cfg, 0, P, ratio, L.EMIT_DEQUANT | L.EMIT_PACKED)
+    params = rtkv.params_from_config(cfg, 0, P, ratio, L.EMIT_DEQUANT | L.EMIT_PACKED |
+                                     (L.NO_SELECTION if expect == "quant" else 0))
     ws = rtkv.Workspace("cuda")
     early = EarlyStatsBuffer()
     outs = []
@@ -59,7 +62,7 @@ def test_early_stats_equal_the_final_block(dtype, B, S, H, D, ratio, expect):
         if use_early:
             published = res._early is not None
             assert published == (expect != "unpublished")
-            if expect == "complete":
+            if expect in ("complete", "quant"):
                 assert np.isnan(st.score_m2) and np.isnan(st.batch[0]["kept_score_sum"])
         fin = res.final_stats()
         outs.append((st, fin, bufs))

@@ -130,22 +130,47 @@ def test_single_matches_pipeline_and_oracle(S, dtype, ratio, over, kind):
         assert np.array_equal(a["pv"].numpy(), o["packed_v"])
 
 
-def test_no_selection_single_matches_pipeline():
+@pytest.mark.parametrize("S,dtype,over", [(8192, "float16", {}), (1, "float32", {}), (17, "bfloat16", {}),
+                                          (1024, "float16", {}), (1025, "float32", {}), (4096, "float32", {}),
+                                          (16385, "bfloat16", {}), (32768, "float16", {}),
+                                          (4096, "float32", dict(low_precision_bits=4, medium_precision_bits=8,
+                                                                 high_precision_bits=16)),
+                                          (5000, "float16", dict(beta=0.0))])
+def test_no_selection_single_matches_pipeline(S, dtype, over):
+    """Quantization only (RTKV_NO_SELECTION, BASELINE config 2): the one-pass K2 (fsel_quant_kernel: scores,
+    classes, row offsets from the predecessors' class counts) against the pipeline and the oracle."""
     import rtkv
     from rtkv import _lib as L
-    S, H, D, dtype = 8192, 4, 64, "float16"
+    H, D = 4, 64
     F = H * D
     P = rtkv.prompt_length(S)
-    K, V = synth.kv(91, 1, S, F, dtype)
-    W = synth.attention_slice(91, 1, H, S, P, dtype)
+    K, V = synth.kv(91 + S, 1, S, F, dtype)
+    W = synth.attention_slice(91 + S, 1, H, S, P, dtype)
     Kd, Vd, Wd = dev(K, dtype), dev(V, dtype), dev(W, dtype)
+    kw = dict(COV, **over)
     base = L.EMIT_DEQUANT | L.EMIT_PACKED | L.NO_SELECTION
-    a, sa = run(Kd, Vd, Wd, dtype, S, F, COV, 0, 0.5, base)
-    b, sb = run(Kd, Vd, Wd, dtype, S, F, COV, 0, 0.5, base | L.SELECT_PIPELINE)
+    a, sa = run(Kd, Vd, Wd, dtype, S, F, kw, 0, 0.5, base)
+    b, sb = run(Kd, Vd, Wd, dtype, S, F, kw, 0, 0.5, base | L.SELECT_PIPELINE)
     assert sa.max_kept == S == sb.max_kept
     for name in a:
         assert torch.equal(a[name].view(torch.uint8) if a[name].dtype != torch.uint8 else a[name],
                            b[name].view(torch.uint8) if b[name].dtype != torch.uint8 else b[name]), name
+    assert (sa.total_packed_bytes, sa.error_flags, sa.score_min, sa.score_max) == \
+        (sb.total_packed_bytes, sb.error_flags, sb.score_min, sb.score_max)
+    ra, rb = sa.batch[0], sb.batch[0]
+    for k in ("class_count", "kept", "kept_class", "cost_units", "packed_bytes", "fallback"):
+        assert ra[k] == rb[k], k
+    for x, y in ((sa.score_sum, sb.score_sum), (sa.score_m2, sb.score_m2), (ra["kept_score_sum"], rb["kept_score_sum"])):
+        assert abs(x - y) <= 1e-12 * max(1.0, abs(y))
+    cfg = rtkv.CompressionConfig(num_hidden_layers=4, **kw)
+    dt = synth.DTYPES[dtype]
+    bits = (cfg.low_precision_bits, cfg.medium_precision_bits, cfg.high_precision_bits)
+    o = orc.compress_layer(K, V, dt, W, dt, P, kw["alpha"], kw["beta"], kw["gamma"], cfg.layer_weights[0],
+                           kw["theta_h"], kw["theta_m"], bits, 1.0, no_selection=True)
+    assert o["max_kept"] == S
+    assert np.array_equal(a["scores"].numpy(), o["scores"]) and np.array_equal(a["labels"].numpy(), o["labels"])
+    assert np.array_equal(a["row_offset"].numpy(), o["row_offset"][0])
+    assert np.array_equal(a["pk"].numpy(), o["packed_k"]) and np.array_equal(a["pv"].numpy(), o["packed_v"])
 
 
 @pytest.mark.parametrize("B,S,ratio,monotone", [(2, 3000, 0.5, False), (1, 12000, 0.3, True),
