@@ -26,6 +26,7 @@ def device_stamps(comp, job, ids, layers, reps):
     """Without a profiler: each layer's device span (first K1 block start to last K4 row) and the idle
     time from one layer's last K4 row to the next layer's first K1 block, from rtkv_layer_times."""
     from rtkv import _lib as L
+    comp = rtkv.RealTimePrefillCompressor(job.cfg, strict=False)  # keeps each layer's result in _unverified
     khz = L.wall_clock_khz(job.device)
     spans, gaps, walls = [], [], []
     for it in range(2 + reps):

@@ -1,12 +1,14 @@
 #!/usr/bin/env python3
 """Summarise tools/mfma_pmc.sh's counter passes into profiles/TAG_mfma.json: per MFMA kernel and grid
-size, the mean duration, the achieved clock, MFMA utilisation and MFMA flops.
+size, the mean duration, the achieved clock, MFMA utilisation over the kernel's own duration, MFMA
+flops and the LDS counters (instructions, bank-conflict cycles).
 
     python tools/mfma_summary.py TAG [gpurun_out/mfma]
 
-MfmaUtil = SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE / 8 XCDs x 1024 SIMDs) (rocprofv3's MfmaUtil
-expression; the per-dispatch GRBM_GUI_ACTIVE value is the sum over the 8 XCDs, MI355X_MICROARCH.md
-DVFS note); flops = (SQ_INSTS_VALU_MFMA_MOPS_F16 + _BF16) x 512.
+Utilisation = SQ_VALU_MFMA_BUSY_CYCLES / (duration x clock x 1024 SIMDs); the clock is GRBM_GUI_ACTIVE / 8
+XCDs / duration (the per-dispatch value is the sum over the 8 XCDs, MI355X_MICROARCH.md DVFS note) unless
+that exceeds 2.4 GHz — then the counter window was wider than the kernel (short kernels), the derived
+clock is rejected and 2.4 GHz gives a lower bound.  flops = (SQ_INSTS_VALU_MFMA_MOPS_F16 + _BF16) x 512.
 """
 import collections
 import csv
@@ -16,6 +18,7 @@ import os
 import sys
 
 SIMDS, XCDS = 1024, 8
+PEAK_GHZ = 2.4  # MI355X peak engine clock (MI355X_MICROARCH.md chip parameters)
 
 
 def load(path):
@@ -43,19 +46,36 @@ def main():
         for (name, grid), d in merged.items():
             m = {k: sum(v) / len(v) for k, v in d.items()}
             rec = {"dispatches": len(d["ns"]), "mean_us": round(m["ns"] / 1e3, 2)}
-            if "GRBM_GUI_ACTIVE" in m:
-                cyc = m["GRBM_GUI_ACTIVE"] / XCDS
-                rec["clock_GHz"] = round(cyc / m["ns"], 3) if m["ns"] else None
+            if "GRBM_GUI_ACTIVE" in m and m["ns"]:
+                # GRBM_GUI_ACTIVE counts the busy cycles of the counter window, which for a short kernel
+                # extends past the kernel's own timestamps: a derived clock above the part's 2.4 GHz peak
+                # means the window is wider than the kernel, and that clock is rejected.  Utilisation is
+                # always taken over the kernel's OWN duration: busy / (duration x clock x 1024 SIMDs), with
+                # the derived clock when it is plausible, else the 2.4 GHz peak (a lower bound).
+                derived = m["GRBM_GUI_ACTIVE"] / XCDS / m["ns"]
+                ok = derived <= PEAK_GHZ
+                rec["clock_GHz_derived"] = round(derived, 3)
+                rec["clock_window_ok"] = ok
+                clk = derived if ok else PEAK_GHZ
+                rec["clock_GHz_used"] = round(clk, 3)
                 if "SQ_VALU_MFMA_BUSY_CYCLES" in m:
-                    rec["mfma_util_pct"] = round(100 * m["SQ_VALU_MFMA_BUSY_CYCLES"] / (cyc * SIMDS), 2)
+                    util = 100 * m["SQ_VALU_MFMA_BUSY_CYCLES"] / (m["ns"] * clk * SIMDS)
+                    rec["mfma_util_pct" if ok else "mfma_util_pct_lower_bound"] = round(util, 2)
+            for k in ("SQ_INSTS_LDS", "SQ_LDS_BANK_CONFLICT", "SQ_LDS_IDX_ACTIVE", "SQ_WAVES", "SQ_INSTS_MFMA"):
+                if k in m:
+                    rec[k] = m[k]
+            if "SQ_LDS_BANK_CONFLICT" in m and m.get("SQ_LDS_IDX_ACTIVE"):
+                rec["lds_bank_conflict_pct"] = round(100 * m["SQ_LDS_BANK_CONFLICT"] / m["SQ_LDS_IDX_ACTIVE"], 2)
             mops = m.get("SQ_INSTS_VALU_MFMA_MOPS_F16", 0.0) + m.get("SQ_INSTS_VALU_MFMA_MOPS_BF16", 0.0)
             if mops:
                 rec["mfma_flops"] = mops * 512
             out[f"{wl}: {name} grid={grid}"] = rec
     doc = {"source": "rocprofv3 --pmc passes of tools/mfma_pmc.sh (tools/lse_bench.py: S = 4096 and 16384; "
                      "bench.py --importance qk --dtype float16, 4 cfg3 layers)",
-           "definition": "mfma_util_pct = SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE/8 * 1024 SIMDs); "
-                         "clock = GRBM_GUI_ACTIVE/8 / duration",
+           "definition": "mfma_util_pct = SQ_VALU_MFMA_BUSY_CYCLES / (kernel duration x clock x 1024 SIMDs), "
+                         "clock = GRBM_GUI_ACTIVE/8 / duration when that is <= 2.4 GHz (the counter window is the "
+                         "kernel's), else 2.4 GHz and the figure is reported as mfma_util_pct_lower_bound; "
+                         "lds_bank_conflict_pct = SQ_LDS_BANK_CONFLICT / SQ_LDS_IDX_ACTIVE",
            "kernels": out}
     here = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "profiles")
     with open(os.path.join(here, f"{tag}_mfma.json"), "w") as f:
