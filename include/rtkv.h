@@ -381,6 +381,38 @@ int rtkv_compress_layer_finish(const rtkv_kv_desc* kv, const rtkv_layer_params* 
  * selection that timed out after the early publication raises in the layer's own call — where the
  * reference caller's try/except falls back for that layer (modified_llama.py:144-149). */
 int rtkv_wait_final(const rtkv_early_stats* early_host, uint64_t seq, int64_t timeout_us);
+/* Armed K4 (the drop-in's default; no reference counterpart).  Instead of rtkv_compress_layer_finish
+ * after the host has read S' and allocated the outputs, rtkv_compress_layer_arm — called right after
+ * rtkv_compress_layer_begin on the same stream — enqueues K4 at once, preceded by a small waiter kernel
+ * that spins (bounded) on a pinned host mailbox and reads the first kept rows into the Infinity Cache
+ * meanwhile (up to prefetch_bytes, as rtkv_prefetch_kept_rows).  The host then allocates K'/V' and the
+ * code planes at their exact sizes and posts their addresses (rtkv_mailbox_post); K4 starts when the
+ * waiter ends, with no host launch on the path between K2's publication and K4.  If the host cannot
+ * post (an error), it must call rtkv_mailbox_cancel: K4 then writes nothing (the early statistics and
+ * the per-token buffers stay valid).  A waiter that never sees either gives up after its poll bound,
+ * flags RTKV_FLAG_SPIN_TIMEOUT and K4 writes nothing.  out: the begin call's per-token buffers and
+ * row_capacity; its k_out/v_out/packed pointers only tell which outputs exist (any non-null value):
+ * the mailbox supplies the real ones, 16-byte aligned, with packed_capacity and out_rows as for
+ * rtkv_compress_layer_finish.  mailbox_host: rtkv_host_alloc memory, one per stream; seq: the begin
+ * call's. */
+typedef struct rtkv_out_mailbox {
+  uint64_t seq;               /* written last (release, system scope) by rtkv_mailbox_post / _cancel */
+  uint64_t k_out_dev, v_out_dev, packed_k_dev, packed_v_dev;
+  int64_t packed_capacity;
+  int64_t out_rows;
+  int32_t cancel;             /* 1: the host cancelled, K4 writes and publishes nothing (2, device copy only:
+                                 the waiter timed out, K4 publishes RTKV_FLAG_SPIN_TIMEOUT and writes nothing) */
+  int32_t reserved;
+} rtkv_out_mailbox;
+int rtkv_compress_layer_arm(const rtkv_kv_desc* kv, const rtkv_layer_params* p, const rtkv_layer_out* out,
+                            void* workspace_dev, size_t workspace_bytes, void* stream, rtkv_early_stats* early_host,
+                            uint64_t seq, rtkv_out_mailbox* mailbox_host, int64_t prefetch_bytes);
+void rtkv_mailbox_post(rtkv_out_mailbox* mailbox_host, uint64_t seq, void* k_out_dev, void* v_out_dev,
+                       void* packed_k_dev, void* packed_v_dev, int64_t packed_capacity, int64_t out_rows);
+void rtkv_mailbox_cancel(rtkv_out_mailbox* mailbox_host, uint64_t seq);
+/* Polls an armed K4's waiter makes before it gives up (default 2^22, about 4-8 s; 0: the default again;
+ * RTKV_ARM_SPIN_LIMIT sets the initial value).  Applies to later rtkv_compress_layer_arm calls. */
+void rtkv_set_arm_spin_limit(uint32_t polls);
 /* start_event (nullable, a hipEvent_t): recorded on the stream right before K1, in the same call —
  * the start of the drop-in's processing_time.  (Recorded from the host separately before this call,
  * the timing event cost ~4.5 us of device idle per layer; recorded here, as rtkv_compress_layer_events

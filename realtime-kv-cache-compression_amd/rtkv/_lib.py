@@ -78,6 +78,13 @@ class EarlyStats(ctypes.Structure):
                 ("batch", BatchStats), ("final_seq", ctypes.c_uint64), ("final_flags", c_i32), ("reserved2", c_i32)]
 
 
+class OutMailbox(ctypes.Structure):
+    """rtkv_out_mailbox: the armed K4's outputs, posted by the host (rtkv_mailbox_post / _cancel)."""
+    _fields_ = [("seq", ctypes.c_uint64), ("k_out_dev", ctypes.c_uint64), ("v_out_dev", ctypes.c_uint64),
+                ("packed_k_dev", ctypes.c_uint64), ("packed_v_dev", ctypes.c_uint64), ("packed_capacity", c_i64),
+                ("out_rows", c_i64), ("cancel", c_i32), ("reserved", c_i32)]
+
+
 _WALL_KHZ = {}
 
 
@@ -140,6 +147,10 @@ _SIGS = {
     "rtkv_compress_layer_qk_begin": ([c_p, c_p, c_p, c_p, c_p, c_sz, c_p, c_p, ctypes.c_uint64, c_p, c_p], c_i32),
     "rtkv_compress_layer_finish": ([c_p, c_p, c_p, c_i64, c_p, c_sz, c_p, c_p, ctypes.c_uint64], c_i32),
     "rtkv_prefetch_kept_rows": ([c_p, c_p, c_i64, c_p], c_i32),
+    "rtkv_compress_layer_arm": ([c_p, c_p, c_p, c_p, c_sz, c_p, c_p, ctypes.c_uint64, c_p, c_i64], c_i32),
+    "rtkv_mailbox_post": ([c_p, ctypes.c_uint64, c_p, c_p, c_p, c_p, c_i64, c_i64], None),
+    "rtkv_mailbox_cancel": ([c_p, ctypes.c_uint64], None),
+    "rtkv_set_arm_spin_limit": ([ctypes.c_uint32], None),
     "rtkv_wall_clock_khz": ([c_i32], c_i64),
     "rtkv_mask_key_padding": ([c_p, c_i32, c_i64, c_i64, c_i64, c_i64, c_i64, c_f, c_p, c_i64, c_p, c_p], c_i32),
     "rtkv_host_alloc": ([c_sz], c_p),

@@ -229,6 +229,22 @@ class EarlyStatsBuffer:
             self.ptr = None
 
 
+class OutMailbox:
+    """Pinned host rtkv_out_mailbox (rtkv_host_alloc) through which the host posts an armed K4's outputs
+    (rtkv_compress_layer_arm); one per device and stream (layer l+1 posts only after layer l's K4 ran)."""
+
+    def __init__(self):
+        self._lib = L.lib()
+        self.ptr = self._lib.rtkv_host_alloc(ctypes.sizeof(L.OutMailbox))
+        if not self.ptr:
+            raise RuntimeError("rtkv: rtkv_host_alloc failed (pinned host memory for the output mailbox)")
+
+    def __del__(self):
+        if getattr(self, "ptr", None):
+            self._lib.rtkv_host_free(self.ptr)
+            self.ptr = None
+
+
 class Workspace:
     """Caller-owned scratch for the C ABI, grown on demand (one per device).
 
@@ -507,6 +523,30 @@ class PendingLayer(LayerResult):
         self.finished = False
         self._raw = None    # the early publication as the device wrote it (converted lazily by stats())
         self._sizes = None
+        self._armed = None  # the OutMailbox of an armed K4 until it is posted or cancelled
+
+    def arm(self, mailbox: "OutMailbox", prefetch_bytes: int = 0) -> "PendingLayer":
+        """Enqueue K4 now (rtkv_compress_layer_arm), behind a waiter kernel that reads the outputs from
+        `mailbox` (and the first kept rows meanwhile): finish() then only allocates and posts, no launch.
+        Only for a layer that publishes its statistics early (the one-launch K2)."""
+        if self._early is None:
+            raise RuntimeError("rtkv: arm() needs a layer with early statistics")
+        L.check(L.lib().rtkv_compress_layer_arm(self._finish_args[0], self._finish_args[1], self._finish_args[2],
+                                                self._finish_tail[0], self._finish_tail[1], self._stream,
+                                                self._finish_tail[3], self._seq, mailbox.ptr, int(prefetch_bytes)),
+                "rtkv_compress_layer_arm")
+        self._armed = mailbox
+        return self
+
+    def cancel_armed(self):
+        """An armed K4 whose outputs will not be posted: it writes nothing (its waiter ends at once)."""
+        if self._armed is not None:
+            L.lib().rtkv_mailbox_cancel(self._armed.ptr, self._seq)
+            self._armed = None
+
+    def __del__(self):
+        if getattr(self, "_armed", None) is not None:  # never leave an armed K4 waiting for the host
+            self.cancel_armed()
 
     def sizes(self):
         """(S'_max, packed bytes per code plane, error flags) for the output allocation: straight from the
@@ -519,6 +559,9 @@ class PendingLayer(LayerResult):
                     self._raw = e
                     self._sizes = (e.stats.max_kept, e.stats.total_packed_bytes, e.stats.error_flags)
                     return self._sizes
+            # incomplete (the top-10% fallback ran): the statistics need a stream sync, which an armed K4
+            # would block (it waits for the host) — cancel it first; finish() then launches K4 itself
+            self.cancel_armed()
             st = self.stats()
             self._sizes = (st.max_kept, st.total_packed_bytes, st.error_flags)
         return self._sizes
@@ -543,7 +586,15 @@ class PendingLayer(LayerResult):
     def finish(self) -> "PendingLayer":
         """Allocate K'/V' [B, S', F] and the packed codes at their exact sizes and enqueue K4 into them.
         Between the early statistics and this launch the device only runs K2's tail, so this path is
-        kept short: one allocation for K'+V', one for both code planes, the begin call's LayerOut patched."""
+        kept short: one allocation for K'+V', one for both code planes, the begin call's LayerOut patched.
+        An armed layer (arm()) posts the outputs to its waiting K4 instead of launching it."""
+        try:
+            return self._finish()
+        except BaseException:
+            self.cancel_armed()  # an armed K4 must not wait for outputs that will never be posted
+            raise
+
+    def _finish(self) -> "PendingLayer":
         Sp, pb, flags = self.sizes()
         check_flags(flags)
         b = self.bufs
@@ -562,8 +613,13 @@ class PendingLayer(LayerResult):
             out.packed_capacity = n
             self._codes = codes
         try:
-            L.check(L.lib().rtkv_compress_layer_finish(*self._finish_args, max(Sp, 1), *self._finish_tail),
-                    "rtkv_compress_layer_finish")
+            if self._armed is not None:  # K4 is queued behind its waiter: post the outputs, no launch
+                L.lib().rtkv_mailbox_post(self._armed.ptr, self._seq, out.k_out_dev, out.v_out_dev, out.packed_k_dev,
+                                          out.packed_v_dev, out.packed_capacity, max(Sp, 1))
+                self._armed = None
+            else:
+                L.check(L.lib().rtkv_compress_layer_finish(*self._finish_args, max(Sp, 1), *self._finish_tail),
+                        "rtkv_compress_layer_finish")
         finally:
             self._wso.pending = None
         self.finished = True
@@ -578,6 +634,7 @@ class PendingLayer(LayerResult):
 
     def final_stats_unchecked(self) -> LayerStats:
         if not self.finished and self._final is None:  # no completion event yet: K1+K2 on the layer's stream
+            self.cancel_armed()  # (a stream sync would wait for an armed K4 that waits for the host)
             torch.cuda.ExternalStream(self._stream, device=self.bufs.device).synchronize()
         return super().final_stats_unchecked()
 

@@ -16,7 +16,7 @@ import torch
 
 from . import _lib as L
 from .dynamic_quantization import F16_OVERFLOW_MSG, DynamicPrecisionQuantizer
-from .engine import (EarlyStatsBuffer, LayerBuffers, Workspace, check_flags, compress_layer_begin,
+from .engine import (EarlyStatsBuffer, LayerBuffers, OutMailbox, Workspace, check_flags, compress_layer_begin,
                      params_from_config, prompt_length)
 from .selective_propagation import SelectiveTokenPropagator
 from .token_importance import LayerWiseImportanceTracker
@@ -105,6 +105,11 @@ class RealTimePrefillCompressor:
         # (past ~40 MB the read outlasts the host's reaction and delays K4).  RTKV_DROPIN_PREFETCH_MB
         # overrides (0: off).
         self.prefetch_bytes = int(float(os.environ.get("RTKV_DROPIN_PREFETCH_MB", "40")) * (1 << 20))
+        # armed K4 (rtkv_compress_layer_arm): K4 is enqueued right after K2 behind a waiter kernel and the host
+        # only posts the output addresses once it has allocated them (no launch between K2's publication
+        # and K4).  RTKV_DROPIN_ARMED=0: the two-call begin / finish path.
+        self.armed = os.environ.get("RTKV_DROPIN_ARMED", "1") != "0"
+        self._mailboxes: Dict[torch.device, OutMailbox] = {}
         self._packable: Dict[tuple, bool] = {}  # (dtype, bits, emit_packed) → whether the codes are emitted
         self.strict = (os.environ.get("RTKV_STRICT", "1") != "0") if strict is None else bool(strict)
 
@@ -180,7 +185,13 @@ class RealTimePrefillCompressor:
         # thresholds; the exactly-sized outputs are allocated then and K4 is enqueued into them
         prev, done = None, False
         try:
-            if self.prefetch_bytes > 0 and res._early is not None:
+            if self.armed and res._early is not None:
+                # K4 queued now behind its waiter (which reads the first kept rows meanwhile); finish() posts
+                mb = self._mailboxes.get(K.device)
+                if mb is None:
+                    mb = self._mailboxes[K.device] = OutMailbox()
+                res.arm(mb, self.prefetch_bytes)
+            elif self.prefetch_bytes > 0 and res._early is not None:
                 # the first kept rows into the Infinity Cache while the host waits and allocates (after K2)
                 L.check(L.lib().rtkv_prefetch_kept_rows(res._finish_args[0], res._finish_args[2], self.prefetch_bytes,
                                                         res._stream), "rtkv_prefetch_kept_rows")
@@ -194,6 +205,8 @@ class RealTimePrefillCompressor:
             res.finish()  # between the publication and this launch the device only runs K2's tail
             done = True
         finally:
+            if not done:
+                res.cancel_armed()  # an armed K4 writes nothing (and ends) when its outputs are not posted
             if ws.pending is res:  # an error before finish(): the workspace is free again
                 ws.pending = None
             if prev is not None and not done:  # still to be checked (next call / overall stats)

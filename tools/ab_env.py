@@ -4,7 +4,8 @@ bench.py process, since the library reads its knobs once per process).
 
     python tools/ab_env.py TAG --rounds 2 --variants 'A=' 'B=RTKV_K4_PK_WAVES=4' -- --dtype float16 --no-dequant
 
-Every run: bench.py --legs none --cpu-baseline-seconds 0 plus the arguments after '--'.  Writes
+Every run: bench.py --legs none (unless --legs is among the arguments) --cpu-baseline-seconds 0 plus the
+arguments after '--'.  Writes
 gpurun_out/ab_TAG.json with, per variant, every run's ms_per_step and per-kernel event times, and the
 means; prints one summary line per variant.
 """
@@ -41,14 +42,18 @@ def main():
     for r in range(a.rounds):
         for name, env in variants:
             e = dict(os.environ, **env)
-            cmd = [sys.executable, os.path.join(REPO, "bench.py"), "--legs", "none", "--cpu-baseline-seconds", "0",
-                   *bench_args]
+            legs = [] if "--legs" in bench_args else ["--legs", "none"]
+            cmd = [sys.executable, os.path.join(REPO, "bench.py"), *legs, "--cpu-baseline-seconds", "0", *bench_args]
             p = subprocess.run(cmd, env=e, capture_output=True, text=True, timeout=a.timeout)
             if p.returncode != 0:
                 print(f"{name}: rc={p.returncode}\n{p.stderr[-2000:]}", flush=True)
                 sys.exit(p.returncode)
             line = json.loads(p.stdout.strip().splitlines()[-1])
             run = {"ms_per_step": line["ms_per_step"], "kernel_us_per_layer": line.get("kernel_us_per_layer")}
+            if "legs" in line:  # extra legs asked for with --legs: their headline numbers
+                run["legs"] = {k: {x: v[x] for x in ("ms_per_step", "ttft_ms", "ttft_device_span_ms",
+                                                      "raw_driver_ms_per_prefill_same_state", "kernel_us_per_layer")
+                                   if x in v} for k, v in line["legs"].items() if isinstance(v, dict)}
             out["variants"][name]["runs"].append(run)
             print(f"round {r} {name}: {run}", flush=True)
             with open(path, "w") as f:

@@ -61,9 +61,17 @@ def main():
                 if "SQ_VALU_MFMA_BUSY_CYCLES" in m:
                     util = 100 * m["SQ_VALU_MFMA_BUSY_CYCLES"] / (m["ns"] * clk * SIMDS)
                     rec["mfma_util_pct" if ok else "mfma_util_pct_lower_bound"] = round(util, 2)
-            for k in ("SQ_INSTS_LDS", "SQ_LDS_BANK_CONFLICT", "SQ_LDS_IDX_ACTIVE", "SQ_WAVES", "SQ_INSTS_MFMA"):
+            for k in ("SQ_INSTS_LDS", "SQ_LDS_BANK_CONFLICT", "SQ_LDS_IDX_ACTIVE", "SQ_WAVES", "SQ_INSTS_MFMA",
+                      "SQ_WAVE_CYCLES", "SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_VALU", "SQ_ACTIVE_INST_LDS",
+                      "SQ_ACTIVE_INST_VMEM", "SQ_WAIT_INST_LDS"):
                 if k in m:
                     rec[k] = m[k]
+            if m.get("SQ_WAVE_CYCLES"):  # shares of wave time (all quad-cycle counters)
+                for k, name in (("SQ_WAIT_ANY", "wait_any_pct"), ("SQ_WAIT_INST_ANY", "wait_inst_any_pct"),
+                                ("SQ_ACTIVE_INST_VALU", "valu_active_pct"), ("SQ_ACTIVE_INST_LDS", "lds_active_pct"),
+                                ("SQ_ACTIVE_INST_VMEM", "vmem_active_pct")):
+                    if k in m:
+                        rec[name] = round(100 * m[k] / m["SQ_WAVE_CYCLES"], 1)
             if "SQ_LDS_BANK_CONFLICT" in m and m.get("SQ_LDS_IDX_ACTIVE"):
                 rec["lds_bank_conflict_pct"] = round(100 * m["SQ_LDS_BANK_CONFLICT"] / m["SQ_LDS_IDX_ACTIVE"], 2)
             mops = m.get("SQ_INSTS_VALU_MFMA_MOPS_F16", 0.0) + m.get("SQ_INSTS_VALU_MFMA_MOPS_BF16", 0.0)
