@@ -59,7 +59,11 @@ enum rtkv_error_flag {
   RTKV_FLAG_SPIN_TIMEOUT = 2,
   /* rtkv_compress_layer_finish: the layer's S'_max or packed byte count exceeds the buffers the caller
    * declared (out_rows, packed_capacity); K4 wrote nothing. */
-  RTKV_FLAG_OUTPUT_OVERFLOW = 4
+  RTKV_FLAG_OUTPUT_OVERFLOW = 4,
+  /* armed K4 (rtkv_compress_layer_arm): the outputs were not posted within the waiter's bound
+   * (rtkv_set_arm_wait_us); K4 wrote nothing and published this flag in final_flags only (not an error of
+   * the layer: the host launches K4 with rtkv_compress_layer_finish instead). */
+  RTKV_FLAG_ARM_TIMEOUT = 8
 };
 
 /* Flags for rtkv_layer_params.flags */
@@ -389,8 +393,11 @@ int rtkv_wait_final(const rtkv_early_stats* early_host, uint64_t seq, int64_t ti
  * code planes at their exact sizes and posts their addresses (rtkv_mailbox_post); K4 starts when the
  * waiter ends, with no host launch on the path between K2's publication and K4.  If the host cannot
  * post (an error), it must call rtkv_mailbox_cancel: K4 then writes nothing (the early statistics and
- * the per-token buffers stay valid).  A waiter that never sees either gives up after its poll bound,
- * flags RTKV_FLAG_SPIN_TIMEOUT and K4 writes nothing.  out: the begin call's per-token buffers and
+ * the per-token buffers stay valid).  A waiter that sees neither within its bound (rtkv_set_arm_wait_us,
+ * default 20 ms: a host stalled by a GC pause or a synchronising runtime call) gives up; K4 then writes
+ * nothing and publishes RTKV_FLAG_ARM_TIMEOUT in final_flags, and the host — which must wait for the
+ * final flags before it trusts the outputs — launches K4 itself (rtkv_compress_layer_finish, with a
+ * different final seq).  out: the begin call's per-token buffers and
  * row_capacity; its k_out/v_out/packed pointers only tell which outputs exist (any non-null value):
  * the mailbox supplies the real ones, 16-byte aligned, with packed_capacity and out_rows as for
  * rtkv_compress_layer_finish.  mailbox_host: rtkv_host_alloc memory, one per stream; seq: the begin
@@ -401,7 +408,7 @@ typedef struct rtkv_out_mailbox {
   int64_t packed_capacity;
   int64_t out_rows;
   int32_t cancel;             /* 1: the host cancelled, K4 writes and publishes nothing (2, device copy only:
-                                 the waiter timed out, K4 publishes RTKV_FLAG_SPIN_TIMEOUT and writes nothing) */
+                                 the waiter timed out, K4 publishes RTKV_FLAG_ARM_TIMEOUT and writes nothing) */
   int32_t reserved;
 } rtkv_out_mailbox;
 int rtkv_compress_layer_arm(const rtkv_kv_desc* kv, const rtkv_layer_params* p, const rtkv_layer_out* out,
@@ -410,9 +417,10 @@ int rtkv_compress_layer_arm(const rtkv_kv_desc* kv, const rtkv_layer_params* p, 
 void rtkv_mailbox_post(rtkv_out_mailbox* mailbox_host, uint64_t seq, void* k_out_dev, void* v_out_dev,
                        void* packed_k_dev, void* packed_v_dev, int64_t packed_capacity, int64_t out_rows);
 void rtkv_mailbox_cancel(rtkv_out_mailbox* mailbox_host, uint64_t seq);
-/* Polls an armed K4's waiter makes before it gives up (default 2^22, about 4-8 s; 0: the default again;
- * RTKV_ARM_SPIN_LIMIT sets the initial value).  Applies to later rtkv_compress_layer_arm calls. */
-void rtkv_set_arm_spin_limit(uint32_t polls);
+/* How long an armed K4's waiter waits for the host's post, in microseconds of the device's real-time
+ * counter (default 20000; 0: the default again; RTKV_ARM_WAIT_US sets the initial value).  Applies to
+ * later rtkv_compress_layer_arm calls. */
+void rtkv_set_arm_wait_us(uint32_t us);
 /* start_event (nullable, a hipEvent_t): recorded on the stream right before K1, in the same call —
  * the start of the drop-in's processing_time.  (Recorded from the host separately before this call,
  * the timing event cost ~4.5 us of device idle per layer; recorded here, as rtkv_compress_layer_events

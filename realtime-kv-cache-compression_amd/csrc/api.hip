@@ -444,7 +444,7 @@ void rtkv_mailbox_post(rtkv_out_mailbox* mb, uint64_t seq, void* k_out_dev, void
   __atomic_store_n(&mb->seq, seq, __ATOMIC_RELEASE);
 }
 
-void rtkv_set_arm_spin_limit(uint32_t polls) { set_arm_spin_limit(polls); }
+void rtkv_set_arm_wait_us(uint32_t us) { set_arm_wait_us(us); }
 
 void rtkv_mailbox_cancel(rtkv_out_mailbox* mb, uint64_t seq) {
   if (!mb) return;

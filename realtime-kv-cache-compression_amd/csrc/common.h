@@ -303,8 +303,8 @@ __device__ __forceinline__ void k4_resolve(QuantArgs& a) {
   a.out_rows = dq ? m->out_rows : ((int64_t)1 << 62);
   if (off) a.out.scale_zp_dev = nullptr;
 }
-uint32_t arm_spin_limit();
-void set_arm_spin_limit(uint32_t polls);
+uint32_t arm_wait_us();
+void set_arm_wait_us(uint32_t us);
 int launch_k4_waiter(const rtkv_out_mailbox* host, uint64_t seq, rtkv_out_mailbox* dev, rtkv_layer_stats* stats,
                      const rtkv_kv_desc* kv, const int32_t* kept_index, int64_t prefetch_bytes, hipStream_t st);
 // rtkv_layer_times.end: every wave of K4 that wrote a row stamps its end into slot (wave index mod

@@ -119,11 +119,12 @@ int launch_prefetch_rows(const rtkv_kv_desc* kv, const int32_t* kept_index, cons
 // Enqueued between K2 and the armed K4 (rtkv_compress_layer_arm): lane 0 of workgroup 0 spins on the
 // pinned host mailbox until the host posts (or cancels) this layer's outputs, copies the mailbox to device
 // memory for K4 (k4_resolve) and ends; the other workgroups read the first kept rows meanwhile (the
-// prefetch above, over the host's allocation window).  Bounded: after `limit` polls the copy is marked
-// cancelled and RTKV_FLAG_SPIN_TIMEOUT is raised, so K4 writes nothing and the host raises.
+// prefetch above, over the host's allocation window).  Bounded: after `ticks` of the 100 MHz real-time
+// counter the copy is marked timed out (cancel = 2): K4 writes nothing, publishes RTKV_FLAG_ARM_TIMEOUT and
+// the host launches K4 itself.
 __global__ __launch_bounds__(256) void k4_waiter_kernel(const rtkv_out_mailbox* __restrict__ host, uint64_t seq,
                                                         rtkv_out_mailbox* __restrict__ dev,
-                                                        rtkv_layer_stats* __restrict__ stats, uint32_t limit,
+                                                        rtkv_layer_stats* __restrict__ stats, uint64_t ticks,
                                                         const uint8_t* __restrict__ k, const uint8_t* __restrict__ v,
                                                         int64_t sss, int64_t row_bytes,
                                                         const int32_t* __restrict__ kept_index, int64_t S,
@@ -131,10 +132,10 @@ __global__ __launch_bounds__(256) void k4_waiter_kernel(const rtkv_out_mailbox* 
   if (blockIdx.x == 0) {
     if (threadIdx.x != 0) return;
     uint64_t* sq = const_cast<uint64_t*>(&host->seq);
-    uint32_t it = 0;
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
     bool ok = true;
     while (__hip_atomic_load(sq, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) != seq) {
-      if (++it >= limit) { ok = false; break; }
+      if (__builtin_amdgcn_s_memrealtime() - t0 > ticks) { ok = false; break; }
       __builtin_amdgcn_s_sleep(8);
     }
     rtkv_out_mailbox m;
@@ -152,8 +153,7 @@ __global__ __launch_bounds__(256) void k4_waiter_kernel(const rtkv_out_mailbox* 
     } else {
       m.k_out_dev = m.v_out_dev = m.packed_k_dev = m.packed_v_dev = 0;
       m.packed_capacity = m.out_rows = 0;
-      m.cancel = 2;  // timed out: K4 publishes RTKV_FLAG_SPIN_TIMEOUT and writes nothing
-      atomicOr(&stats->error_flags, (int)RTKV_FLAG_SPIN_TIMEOUT);
+      m.cancel = 2;  // timed out: K4 publishes RTKV_FLAG_ARM_TIMEOUT and writes nothing
     }
     m.seq = seq;
     m.reserved = 0;
@@ -177,23 +177,24 @@ __global__ __launch_bounds__(256) void k4_waiter_kernel(const rtkv_out_mailbox* 
   asm volatile("" ::"v"(acc));
 }
 
-// polls of ~1-2 us each (a host-memory read + s_sleep): ~4-8 s by default; RTKV_ARM_SPIN_LIMIT or
-// rtkv_set_arm_spin_limit (tests) override
-static uint32_t g_arm_limit = 0;
-uint32_t arm_spin_limit() {
-  if (!g_arm_limit) {
-    const char* e = getenv("RTKV_ARM_SPIN_LIMIT");
-    g_arm_limit = e ? (uint32_t)strtoul(e, nullptr, 10) : (1u << 22);
-    if (!g_arm_limit) g_arm_limit = 1;
+// the waiter's bound in microseconds: 20 ms by default (the host's post normally comes ~10-20 us after K2's
+// publication; past the bound the host relaunches K4, so the bound only trades a stalled GPU for a relaunch);
+// RTKV_ARM_WAIT_US or rtkv_set_arm_wait_us (tests) override
+static uint32_t g_arm_us = 0;
+uint32_t arm_wait_us() {
+  if (!g_arm_us) {
+    const char* e = getenv("RTKV_ARM_WAIT_US");
+    g_arm_us = e ? (uint32_t)strtoul(e, nullptr, 10) : 20000u;
+    if (!g_arm_us) g_arm_us = 1;
   }
-  return g_arm_limit;
+  return g_arm_us;
 }
-void set_arm_spin_limit(uint32_t polls) { g_arm_limit = polls ? polls : (1u << 22); }
+void set_arm_wait_us(uint32_t us) { g_arm_us = us ? us : 20000u; }
 
 int launch_k4_waiter(const rtkv_out_mailbox* host, uint64_t seq, rtkv_out_mailbox* dev, rtkv_layer_stats* stats,
                      const rtkv_kv_desc* kv, const int32_t* kept_index, int64_t prefetch_bytes, hipStream_t st) {
   RTKV_REQUIRE(host && dev && stats && kv && kept_index, "compress_layer_arm: null pointer");
-  const uint32_t limit = arm_spin_limit();
+  const uint64_t ticks = (uint64_t)arm_wait_us() * 100;  // s_memrealtime: 100 MHz
   const int esz = kv->dtype == RTKV_F32 ? 4 : 2;
   const int64_t row_bytes = kv->H * kv->D * esz;
   const bool ok = kv->B == 1 && (kv->H == 1 || kv->stride_h == kv->D) && (row_bytes % 16) == 0 &&
@@ -201,7 +202,7 @@ int launch_k4_waiter(const rtkv_out_mailbox* host, uint64_t seq, rtkv_out_mailbo
   int64_t rows = ok && prefetch_bytes > 0 ? prefetch_bytes / (2 * row_bytes) : 0;
   if (rows > kv->S) rows = kv->S;
   const int64_t blocks = 1 + (2 * rows + 3) / 4;
-  hipLaunchKernelGGL(k4_waiter_kernel, dim3((unsigned)blocks), dim3(256), 0, st, host, seq, dev, stats, limit,
+  hipLaunchKernelGGL(k4_waiter_kernel, dim3((unsigned)blocks), dim3(256), 0, st, host, seq, dev, stats, ticks,
                      static_cast<const uint8_t*>(kv->k_dev), static_cast<const uint8_t*>(kv->v_dev), kv->stride_s * esz,
                      row_bytes, kept_index, kv->S, rows);
   RTKV_HIP_CHECK(hipGetLastError());

@@ -474,9 +474,11 @@ __device__ __forceinline__ bool k4_layer_gate(const QuantArgs& a) {
                                        (a.out.packed_k_dev && nbytes > a.out.packed_capacity));
   if (over) flags |= RTKV_FLAG_OUTPUT_OVERFLOW;
   // armed K4: a host cancel (1) writes nothing and publishes nothing (the host launches K4 itself after a
-  // sync, or has raised); a waiter timeout (2) publishes the flags (RTKV_FLAG_SPIN_TIMEOUT) and writes nothing
+  // sync, or has raised); a waiter timeout (2) writes nothing and publishes RTKV_FLAG_ARM_TIMEOUT (the host
+  // then launches K4 itself)
   const int cancel = a.out_ind ? a.out_ind->cancel : 0;
   if (cancel == 1) return true;
+  if (cancel == 2) flags |= RTKV_FLAG_ARM_TIMEOUT;
   if (blockIdx.x == 0 && threadIdx.x == 0) {
     if (over) atomicOr(&st->error_flags, (int)RTKV_FLAG_OUTPUT_OVERFLOW);
     if (a.final_host) {

@@ -524,6 +524,7 @@ class PendingLayer(LayerResult):
         self._raw = None    # the early publication as the device wrote it (converted lazily by stats())
         self._sizes = None
         self._armed = None  # the OutMailbox of an armed K4 until it is posted or cancelled
+        self._seq_final = seq  # the sequence number K4 publishes its final flags under
 
     def arm(self, mailbox: "OutMailbox", prefetch_bytes: int = 0) -> "PendingLayer":
         """Enqueue K4 now (rtkv_compress_layer_arm), behind a waiter kernel that reads the outputs from
@@ -574,14 +575,25 @@ class PendingLayer(LayerResult):
     def final_flags(self) -> Optional[int]:
         """The layer's complete RTKV_FLAG_* word as K4 published it (no stream sync), or None when it is
         not (yet) available: no early buffer, K4 not started, or overwritten by a later layer's K4."""
-        return self._early.final_flags(self._seq) if self._early is not None and self.finished else None
+        return self._early.final_flags(self._seq_final) if self._early is not None and self.finished else None
 
     def wait_final_flags(self) -> int:
         """Wait (host spin, no stream sync) until this layer's K4 has started and published the layer's
         final flags, and return them; a layer without an early buffer syncs its stream instead."""
         if self._early is None or not self.finished:
             return self.final_stats_unchecked().error_flags
-        return self._early.wait_final(self._seq, self.bufs.device)
+        return self._early.wait_final(self._seq_final, self.bufs.device)
+
+    def relaunch(self) -> "PendingLayer":
+        """K4 through rtkv_compress_layer_finish into the posted outputs, after an armed K4 whose waiter
+        gave up before the post (RTKV_FLAG_ARM_TIMEOUT: it wrote nothing).  Its final flags come under a
+        sequence number of their own."""
+        self._seq_final = self._seq | (1 << 62)
+        ws_ptr, ws_bytes, stream, early_ptr, _ = self._finish_tail
+        L.check(L.lib().rtkv_compress_layer_finish(*self._finish_args, self._out_rows, ws_ptr, ws_bytes, stream,
+                                                    early_ptr, self._seq_final), "rtkv_compress_layer_finish")
+        self._record(self._stream)
+        return self
 
     def finish(self) -> "PendingLayer":
         """Allocate K'/V' [B, S', F] and the packed codes at their exact sizes and enqueue K4 into them.
@@ -612,6 +624,7 @@ class PendingLayer(LayerResult):
             out.packed_k_dev, out.packed_v_dev = cp, cp + n
             out.packed_capacity = n
             self._codes = codes
+        self._out_rows = max(Sp, 1)
         try:
             if self._armed is not None:  # K4 is queued behind its waiter: post the outputs, no launch
                 L.lib().rtkv_mailbox_post(self._armed.ptr, self._seq, out.k_out_dev, out.v_out_dev, out.packed_k_dev,

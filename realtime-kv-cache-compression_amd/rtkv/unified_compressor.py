@@ -107,7 +107,8 @@ class RealTimePrefillCompressor:
         self.prefetch_bytes = int(float(os.environ.get("RTKV_DROPIN_PREFETCH_MB", "40")) * (1 << 20))
         # armed K4 (rtkv_compress_layer_arm): K4 is enqueued right after K2 behind a waiter kernel and the host
         # only posts the output addresses once it has allocated them (no launch between K2's publication
-        # and K4).  RTKV_DROPIN_ARMED=0: the two-call begin / finish path.
+        # and K4).  Strict mode only (the call must see K4's final flags before it returns: a waiter that
+        # gave up means K4 is launched again).  RTKV_DROPIN_ARMED=0: the two-call begin / finish path.
         self.armed = os.environ.get("RTKV_DROPIN_ARMED", "1") != "0"
         self._mailboxes: Dict[torch.device, OutMailbox] = {}
         self._packable: Dict[tuple, bool] = {}  # (dtype, bits, emit_packed) → whether the codes are emitted
@@ -185,7 +186,7 @@ class RealTimePrefillCompressor:
         # thresholds; the exactly-sized outputs are allocated then and K4 is enqueued into them
         prev, done = None, False
         try:
-            if self.armed and res._early is not None:
+            if self.armed and self.strict and res._early is not None:
                 # K4 queued now behind its waiter (which reads the first kept rows meanwhile); finish() posts
                 mb = self._mailboxes.get(K.device)
                 if mb is None:
@@ -216,7 +217,10 @@ class RealTimePrefillCompressor:
         st = res.stats()
         if res._early is not None:
             if self.strict:  # K2's end (K4's first wave publishes the final flags): raise in this call
-                check_flags(res.wait_final_flags(), f"compress_layer_kv_cache (layer {layer_idx})")
+                fl = res.wait_final_flags()
+                if fl & L.FLAG_ARM_TIMEOUT:  # the armed K4's waiter gave up before the post: K4 again, launched
+                    fl = res.relaunch().wait_final_flags()
+                check_flags(fl, f"compress_layer_kv_cache (layer {layer_idx})")
             else:
                 self._unverified[K.device] = (res, layer_idx)
         selected_keys, selected_values = res.kv()

@@ -415,8 +415,8 @@ def test_armed_k4_equals_the_two_call_path(dtype, S, H, D, ratio, extra, bits):
 
 def test_armed_k4_cancel_and_waiter_timeout():
     """An armed K4 whose outputs are never posted: cancelled by the host it writes and publishes
-    nothing; left alone, its waiter gives up after the poll bound (rtkv_set_arm_spin_limit), the layer
-    flags RTKV_FLAG_SPIN_TIMEOUT and K4 writes nothing.  Neither hangs the stream."""
+    nothing; left alone, its waiter gives up after its bound (rtkv_set_arm_wait_us), K4 writes nothing
+    and publishes RTKV_FLAG_ARM_TIMEOUT (not a layer error).  Neither hangs the stream."""
     import rtkv
     from rtkv import _lib as L
     from rtkv.engine import EarlyStatsBuffer, OutMailbox, compress_layer_begin
@@ -427,11 +427,11 @@ def test_armed_k4_cancel_and_waiter_timeout():
         bufs = rtkv.LayerBuffers(1, S, F, Kd.dtype, "cuda", (2, 4, 8), outputs=False)
         bufs.scale_zp.fill_(7.0)
         if mode == "timeout":
-            L.lib().rtkv_set_arm_spin_limit(2000)
+            L.lib().rtkv_set_arm_wait_us(2000)
         try:
             res = compress_layer_begin(Kd, Vd, Wd, p, bufs, ws, early).arm(mb, 0)
         finally:
-            L.lib().rtkv_set_arm_spin_limit(0)
+            L.lib().rtkv_set_arm_wait_us(0)
         st = res.stats()
         assert st.error_flags == 0 and st.max_kept > 0
         if mode == "cancel":
@@ -443,5 +443,28 @@ def test_armed_k4_cancel_and_waiter_timeout():
             assert res.final_flags() is None  # nothing published (finish never ran)
             assert res._early.final_flags(res._seq) is None
         else:
-            assert early.final_flags(res._seq) & L.FLAG_SPIN_TIMEOUT
+            assert early.final_flags(res._seq) == L.FLAG_ARM_TIMEOUT
             res.cancel_armed()  # (no effect on a finished waiter)
+
+
+def test_drop_in_relaunches_k4_when_the_waiter_gives_up():
+    """A host slower than the waiter's bound (here a 1 us bound): every layer's armed K4 writes nothing,
+    the call sees RTKV_FLAG_ARM_TIMEOUT in the final flags and launches K4 itself — the outputs equal the
+    two-call path's, byte for byte."""
+    import rtkv
+    from rtkv import _lib as L
+    S, F, P, cfg, Kd, Vd, Wd = _lookback_inputs()
+    ids = torch.zeros(1, S, dtype=torch.long, device="cuda")
+    ref = rtkv.RealTimePrefillCompressor(cfg)
+    ref.armed = False
+    want = [ref.compress_layer_kv_cache(Kd, Vd, Wd, ids, l)[:2] for l in range(3)]
+    comp = rtkv.RealTimePrefillCompressor(cfg)
+    L.lib().rtkv_set_arm_wait_us(1)
+    try:
+        got = [comp.compress_layer_kv_cache(Kd, Vd, Wd, ids, l)[:2] for l in range(3)]
+    finally:
+        L.lib().rtkv_set_arm_wait_us(0)
+    torch.cuda.synchronize()
+    for (k, v), (rk, rv) in zip(got, want):
+        assert torch.equal(k.view(torch.int16), rk.view(torch.int16)) and torch.equal(v.view(torch.int16), rv.view(torch.int16))
+    assert sorted(comp.layer_states) == [0, 1, 2]
