@@ -325,19 +325,31 @@ int rtkv_compress_layer_events(const rtkv_kv_desc* kv, const rtkv_attn_desc* w,
  * kept_score_sum must be read from stats_dev after the stream syncs.  *published = 1 when this call
  * will publish (the two-launch K2: B = 1, S <= 32768); 0: read stats_dev after a stream sync.
  * complete = 0 on publication means the top-10% fallback ran: read stats_dev after a sync too. */
+/* The published statistics are ONE 128-byte line (this struct's first 128 bytes, 128-byte aligned: the
+ * start of an rtkv_host_alloc block) written by ONE wave store instruction (16 lanes x 8 bytes), with the
+ * call's seq in its first AND last word: a line that reaches host memory in two 64-byte halves is never
+ * taken as complete, and no ordering wait (nor a system-scope release, whose L2 write-back cost the
+ * selection kernel ~4 us) is needed before the seq.  B = 1: kept = max_kept, packed_bytes =
+ * total_packed_bytes; score_m2 and kept_score_sum are not part of it (read after the layer). */
 typedef struct rtkv_early_stats {
-  uint64_t seq;              /* written last (release, system scope) */
-  int32_t complete;
-  int32_t reserved;
-  rtkv_layer_stats stats;    /* score_m2 not set */
-  rtkv_batch_stats batch;    /* B = 1; kept_score_sum not set */
-  /* Written by rtkv_compress_layer_finish's K4 when it starts (all selection waits are over then):
-   * final_flags = the layer's complete RTKV_FLAG_* word, then final_seq = the begin call's seq
-   * (release, system scope).  A flag raised after the early publication (a look-back timeout) or by
-   * K4 itself (RTKV_FLAG_OUTPUT_OVERFLOW) is seen here without a stream sync. */
-  uint64_t final_seq;
-  int32_t final_flags;
-  int32_t reserved2;
+  uint64_t seq;                 /* word 0 */
+  int64_t max_kept;             /* S' (= the batch row's kept count) */
+  int64_t total_packed_bytes;   /* (= the batch row's packed bytes) */
+  double score_sum;
+  float score_min, score_max;
+  int32_t error_flags;
+  int32_t complete;             /* 1: complete (0: the top-10% fallback ran, read stats_dev after a sync) */
+  int64_t class_count[3];
+  int64_t kept_class[3];
+  int64_t cost_units;
+  int64_t reserved[2];
+  uint64_t seq_tail;            /* word 15: seq again */
+  /* Written by K4 (rtkv_compress_layer_finish / _arm) when it starts, all selection waits being over: ONE
+   * 8-byte store of (seq mod 2^48) << 16 | the layer's complete RTKV_FLAG_* word.  A flag raised after the
+   * early publication (a look-back timeout) or by K4 itself (RTKV_FLAG_OUTPUT_OVERFLOW) is seen here
+   * without a stream sync. */
+  uint64_t final_word;
+  uint64_t reserved2[15];
 } rtkv_early_stats;
 
 int rtkv_compress_layer_early(const rtkv_kv_desc* kv, const rtkv_attn_desc* w, const rtkv_layer_params* p,
@@ -346,7 +358,7 @@ int rtkv_compress_layer_early(const rtkv_kv_desc* kv, const rtkv_attn_desc* w, c
 int rtkv_compress_layer_qk_early(const rtkv_kv_desc* kv, const rtkv_qk_desc* q, const rtkv_layer_params* p,
                                  const rtkv_layer_out* out, void* workspace_dev, size_t workspace_bytes,
                                  void* stream, rtkv_early_stats* early_host, uint64_t seq, int32_t* published);
-/* Spin until early_host->seq == seq (RTKV_OK) or timeout_us passes (RTKV_ERR_TIMEOUT). */
+/* Spin until early_host->seq == seq_tail == seq (RTKV_OK) or timeout_us passes (RTKV_ERR_TIMEOUT). */
 int rtkv_wait_early(const rtkv_early_stats* early_host, uint64_t seq, int64_t timeout_us);
 
 /* The layer in two calls, for exactly-sized outputs (the drop-in: the reference returns K'/V' of S'
@@ -379,7 +391,7 @@ int rtkv_compress_layer_qk_begin(const rtkv_kv_desc* kv, const rtkv_qk_desc* q, 
 int rtkv_compress_layer_finish(const rtkv_kv_desc* kv, const rtkv_layer_params* p, const rtkv_layer_out* out,
                                int64_t out_rows, void* workspace_dev, size_t workspace_bytes, void* stream,
                                rtkv_early_stats* early_host, uint64_t seq);
-/* Spin until early_host->final_seq == seq, i.e. until the finish call's K4 has started and published
+/* Spin until early_host->final_word carries seq, i.e. until the finish call's K4 has started and published
  * the layer's final flags (RTKV_OK; read final_flags then), or timeout_us passes (RTKV_ERR_TIMEOUT).
  * The drop-in's strict mode (RealTimePrefillCompressor(strict=True)) waits here before it returns, so a
  * selection that timed out after the early publication raises in the layer's own call — where the

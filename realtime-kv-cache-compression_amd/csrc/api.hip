@@ -1,6 +1,7 @@
 // api.hip — the C ABI of include/rtkv.h: argument validation, workspace carving, host-side scalar
 // preparation (the Python-float → fp32 casts the reference performs) and stream-ordered launches.
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 
@@ -305,7 +306,8 @@ static int compress_layer_impl(const rtkv_kv_desc* kv, const rtkv_attn_desc* w, 
   a.mode_select = (p->flags & RTKV_NO_SELECTION) ? 2 : 1;
   const bool row_labels = select_fast_eligible(a);  // the fast path also writes each kept row's class
   a.row_label = row_labels ? ws.labels : nullptr;
-  if (early && row_labels) {  // the fast path's F1 publishes the final counts to the host
+  static const bool no_early = getenv("RTKV_NO_EARLY") != nullptr;  // diagnostic: publish nothing (host syncs)
+  if (early && row_labels && !no_early) {  // the fast path's F1 publishes the final counts to the host
     a.early = early;
     a.early_seq = early_seq;
     if (published) *published = 1;
@@ -424,7 +426,8 @@ int rtkv_compress_layer_arm(const rtkv_kv_desc* kv, const rtkv_layer_params* p, 
   q.out_ind = ws.mbox;
   q.final_host = early_host;
   q.final_seq = seq;
-  q.t_end = reinterpret_cast<unsigned long long*>(layer_times(out->stats_dev, kv->B)->end);
+  static const bool no_stamp = getenv("RTKV_NO_KSTAMP") != nullptr;  // diagnostic: K4 without end stamps
+  q.t_end = no_stamp ? nullptr : reinterpret_cast<unsigned long long*>(layer_times(out->stats_dev, kv->B)->end);
   hipStream_t st = (hipStream_t)stream;
   rc = launch_k4_waiter(mailbox_host, seq, ws.mbox, out->stats_dev, kv, out->kept_index_dev, prefetch_bytes, st);
   if (rc) return rc;
@@ -461,7 +464,9 @@ int rtkv_wait_early(const rtkv_early_stats* early_host, uint64_t seq, int64_t ti
   RTKV_REQUIRE(early_host != nullptr, "null early-stats buffer");
   const auto t0 = std::chrono::steady_clock::now();
   for (uint32_t it = 0;; ++it) {
-    if (__atomic_load_n(&early_host->seq, __ATOMIC_ACQUIRE) == seq) return RTKV_OK;
+    if (__atomic_load_n(&early_host->seq, __ATOMIC_ACQUIRE) == seq &&
+        __atomic_load_n(&early_host->seq_tail, __ATOMIC_ACQUIRE) == seq)
+      return RTKV_OK;
     if ((it & 255u) == 255u &&
         std::chrono::duration_cast<std::chrono::microseconds>(std::chrono::steady_clock::now() - t0).count() >
             timeout_us) {
@@ -476,7 +481,8 @@ int rtkv_wait_final(const rtkv_early_stats* early_host, uint64_t seq, int64_t ti
   RTKV_REQUIRE(early_host != nullptr, "null early-stats buffer");
   const auto t0 = std::chrono::steady_clock::now();
   for (uint32_t it = 0;; ++it) {
-    if (__atomic_load_n(&early_host->final_seq, __ATOMIC_ACQUIRE) == seq) return RTKV_OK;
+    if ((__atomic_load_n(&early_host->final_word, __ATOMIC_ACQUIRE) >> 16) == (seq & ((1ull << 48) - 1)))
+      return RTKV_OK;
     if ((it & 255u) == 255u &&
         std::chrono::duration_cast<std::chrono::microseconds>(std::chrono::steady_clock::now() - t0).count() >
             timeout_us) {

@@ -84,6 +84,15 @@ template <typename T> __device__ __forceinline__ void st_sc1(T* p, T v) {
 template <typename T> __device__ __forceinline__ T ld_sc1(const T* p) {
   return __hip_atomic_load(const_cast<T*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
+// The early statistics' 128-byte host line (rtkv_early_stats, include/rtkv.h) from one wave: lane l < 16
+// stores word l of `w` (the caller's 16 words, wave-uniform in LDS) with ONE system-scope store
+// instruction — no ordering wait: the seq sits in words 0 and 15.  (Field-by-field stores, a wait for
+// their acknowledgements and the seq last made the publishing selection kernel ~4 us longer: the wait,
+// then the seq's own round trip to host memory, ran past the kernel's natural end.)
+__device__ __forceinline__ void host_line_store(uint64_t* line, const uint64_t* w) {
+  const int lane = threadIdx.x & 63;
+  if (lane < 16) __hip_atomic_store(line + lane, w[lane], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
 
 // ------------------------------------------------------------------------------------ keys
 // Order-preserving uint32 key of an fp32 score (larger key = larger score; -0 folded onto +0 so
@@ -307,10 +316,10 @@ uint32_t arm_wait_us();
 void set_arm_wait_us(uint32_t us);
 int launch_k4_waiter(const rtkv_out_mailbox* host, uint64_t seq, rtkv_out_mailbox* dev, rtkv_layer_stats* stats,
                      const rtkv_kv_desc* kv, const int32_t* kept_index, int64_t prefetch_bytes, hipStream_t st);
-// rtkv_layer_times.end: every wave of K4 that wrote a row stamps its end into slot (wave index mod
-// RTKV_TIME_SLOTS), the largest stays.  Per wave, no barrier (a workgroup-end barrier held finished
-// waves' slots: K4 +7 %); spread over 128-byte lines (one address: the atomics serialised, K4 x2).
-// Waves without a row end within their dispatch, before the last row is written.
+// rtkv_layer_times.end: the waves of K4 that wrote one of the layer's last rows (kStampWindow tasks,
+// quant_impl.h) stamp their end into slot (wave index mod RTKV_TIME_SLOTS), the largest stays.  Per wave, no
+// barrier (a workgroup-end barrier held finished waves' slots: K4 +7 %); spread over 128-byte lines (one
+// address: the atomics serialised, K4 x2).  Earlier waves end before the last rows are written.
 __device__ __forceinline__ void stamp_end(unsigned long long* t, bool wrote) {
   if (!t || !wrote || (threadIdx.x & 63) != 0) return;
   const unsigned slot = ((unsigned)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) % RTKV_TIME_SLOTS;

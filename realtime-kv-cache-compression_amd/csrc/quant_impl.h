@@ -481,10 +481,10 @@ __device__ __forceinline__ bool k4_layer_gate(const QuantArgs& a) {
   if (cancel == 2) flags |= RTKV_FLAG_ARM_TIMEOUT;
   if (blockIdx.x == 0 && threadIdx.x == 0) {
     if (over) atomicOr(&st->error_flags, (int)RTKV_FLAG_OUTPUT_OVERFLOW);
-    if (a.final_host) {
-      __hip_atomic_store(&a.final_host->final_flags, flags, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-      __hip_atomic_store(&a.final_host->final_seq, a.final_seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-    }
+    if (a.final_host)  // one 8-byte store: seq and flags together (no ordering wait)
+      __hip_atomic_store(&a.final_host->final_word,
+                         ((a.final_seq & ((1ull << 48) - 1)) << 16) | (uint64_t)(uint32_t)(flags & 0xffff),
+                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
   if (over) return true;
   if (cancel) return true;
@@ -510,6 +510,11 @@ __device__ __forceinline__ bool k4_layer_gate(const QuantArgs& a) {
   }
   return true;
 }
+
+// rtkv_layer_times.end: only waves that ran one of the layer's last kStampWindow row tasks stamp it (the
+// last-dispatched tasks end last; every wave stamping — ~100k atomics per cfg3 layer — cost K4 ~2.9 us,
+// rocprofv3 trace of the drop-in)
+constexpr int kStampWindow = 2048;
 
 // Contiguous fp32 rows of exactly 4096 elements fit 128 VGPRs (4 waves/SIMD); the gate bookkeeping would push the
 // compiler to 129 (3 waves) without the bound.  Wider fp32 rows keep the 256-register budget.
@@ -638,7 +643,7 @@ __global__ __launch_bounds__(256, PKW ? PKW : ((DT == RTKV_F32 && NCH == 8 && FU
     uint8_t* pk = emit_pk ? (which ? a.out.packed_v_dev : a.out.packed_k_dev) + roff : nullptr;
     emit_row<DT, NCH, CONTIG, FULL, PK_ONLY>(raw, rp, row_nan, w, orow, out_off, pk, nch, lane, emit_deq, emit_pk,
                                              stage);
-    wrote = true;
+    wrote |= t >= (one_row ? 2 * kept_b : tasks) - kStampWindow;  // one of the last tasks
   }
   stamp_end(a.t_end, wrote);
 }
@@ -730,7 +735,7 @@ __global__ __launch_bounds__(64 * NSPLIT) void quant_rows_split_kernel(QuantArgs
     uint8_t* pk = emit_pk ? (which ? a.out.packed_v_dev : a.out.packed_k_dev) + roff + (int64_t)q * NCHW * 64 * w
                           : nullptr;
     emit_row<DT, NCHW, true, true>(raw, rp, nan_any, w, orow, off, pk, NCHW * 64, lane, emit_deq, emit_pk, stage);
-    wrote = true;
+    wrote |= t >= 2 * kept_b - kStampWindow;  // one of the last tasks
   }
   stamp_end(a.t_end, wrote);
 }

@@ -483,8 +483,10 @@ __device__ __forceinline__ void rescan_thresholds(const FastArgs& g, uint32_t* h
 // runs, score sum and range, the f16 16-bit flag) into the device block and, with an early buffer, the
 // host mirror — published by the selecting workgroup as soon as the quotas and the partials are in,
 // before its threshold search: the drop-in host allocates the exact outputs while the selection runs.
+// Called by ONE lane; with an early buffer it fills `line` (16 words in LDS) for host_line_store, which the
+// whole wave then issues.
 __device__ __forceinline__ void publish_stats(const FastArgs& g, bool fallback, double ssum, uint32_t kr0, uint32_t kr1,
-                                           const int64_t (&ccount)[3], const int64_t (&quota)[3]) {
+                                           const int64_t (&ccount)[3], const int64_t (&quota)[3], uint64_t* line) {
   const FinalizeArgs& a = g.f;
   rtkv_layer_stats* hs = a.stats;
   rtkv_batch_stats* bs = reinterpret_cast<rtkv_batch_stats*>(hs + 1);
@@ -513,34 +515,23 @@ __device__ __forceinline__ void publish_stats(const FastArgs& g, bool fallback, 
     hs->max_kept = n;
     hs->total_packed_bytes = bytes;
   }
-  if (g.early) {  // host-mapped mirror for the caller's early return (rtkv_compress_layer_early)
-    rtkv_early_stats* e = g.early;
-    auto put64 = [](void* dst, uint64_t v) {
-      __hip_atomic_store(reinterpret_cast<uint64_t*>(dst), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    };
-    auto put32 = [](void* dst, uint32_t v) {
-      __hip_atomic_store(reinterpret_cast<uint32_t*>(dst), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    };
+  if (g.early && line) {  // host-mapped mirror for the caller's early return (rtkv_compress_layer_early)
     const bool complete = !fallback && g.withhold != 1;  // withheld: the host takes the synchronised statistics
-    put32(&e->complete, complete ? 1u : 0u);
+    for (int k = 0; k < 16; ++k) line[k] = 0ull;
+    line[0] = line[15] = g.early_seq;
     if (complete) {
-      put64(&e->stats.max_kept, (uint64_t)bs->kept);
-      put64(&e->stats.total_packed_bytes, (uint64_t)bs->packed_bytes);
-      put64(&e->stats.score_sum, __builtin_bit_cast(uint64_t, ssum));
-      put32(&e->stats.score_min, __builtin_bit_cast(uint32_t, hs->score_min));
-      put32(&e->stats.score_max, __builtin_bit_cast(uint32_t, hs->score_max));
-      put32(&e->stats.error_flags, (uint32_t)(flags | ld_sc1(&hs->error_flags)));
-      put32(&e->stats.B, 1u);
+      line[1] = (uint64_t)bs->kept;
+      line[2] = (uint64_t)bs->packed_bytes;
+      line[3] = __builtin_bit_cast(uint64_t, ssum);
+      line[4] = (uint64_t)__builtin_bit_cast(uint32_t, hs->score_min) |
+                ((uint64_t)__builtin_bit_cast(uint32_t, hs->score_max) << 32);
+      line[5] = (uint64_t)(uint32_t)(flags | ld_sc1(&hs->error_flags)) | (1ull << 32);
       for (int q = 0; q < 3; ++q) {
-        put64(&e->batch.class_count[q], (uint64_t)ccount[q]);
-        put64(&e->batch.kept_class[q], (uint64_t)quota[q]);
+        line[6 + q] = (uint64_t)ccount[q];
+        line[9 + q] = (uint64_t)quota[q];
       }
-      put64(&e->batch.kept, (uint64_t)bs->kept);
-      put64(&e->batch.cost_units, (uint64_t)bs->cost_units);
-      put64(&e->batch.packed_bytes, (uint64_t)bs->packed_bytes);
-      put32(&e->batch.fallback, 0u);
+      line[12] = (uint64_t)bs->cost_units;
     }
-    __hip_atomic_store(&e->seq, g.early_seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
   }
 }
 
@@ -648,10 +639,19 @@ __device__ __forceinline__ void select_thresholds(const FastArgs& g, uint32_t* h
   }
 #endif
   __syncthreads();
-  if (publish && t == 0) {  // statistics known here; phase 3 adds the kept-token sums (stats zeroed before)
-    const int64_t ccount[3] = {s_cc[0], s_cc[1], s_cc[2]};
-    const int64_t quota[3] = {s_quota[0], s_quota[1], s_quota[2]};
-    publish_stats(g, s_q[3] != M_NONE, s_ssum, s_kr[0], s_kr[1], ccount, quota);
+  // statistics known here; phase 3 adds the kept-token sums (stats zeroed before).  Published by the LAST wave
+  // (its later vmcnt waits include the host store; wave 0 runs the thresholds and the look-back): lane 0
+  // writes the device block and the line's words, the wave stores the host line in one instruction
+  if (publish && wid == kSW - 1) {
+    __shared__ uint64_t s_line[16];
+    if (lane == 0) {
+      const int64_t ccount[3] = {s_cc[0], s_cc[1], s_cc[2]};
+      const int64_t quota[3] = {s_quota[0], s_quota[1], s_quota[2]};
+      publish_stats(g, s_q[3] != M_NONE, s_ssum, s_kr[0], s_kr[1], ccount, quota, s_line);
+    }
+    __builtin_amdgcn_wave_barrier();
+    asm volatile("" ::: "memory");  // (the same wave: its LDS writes are read in order)
+    if (g.early) host_line_store(reinterpret_cast<uint64_t*>(g.early), s_line);
   }
   int mode[kGrp], need[kGrp];
 #pragma unroll
@@ -1190,13 +1190,18 @@ __global__ __launch_bounds__(kST) void fsel_quant_kernel(FastArgs g) {
   const double mean = ssum / (double)S;
   const double dj = nj ? ps / (double)nj - mean : 0.0;
   const double M2 = wave_sum(lane < G ? pm2 + (double)nj * dj * dj : 0.0);
-  if (lane != 0) return;
-  rtkv_layer_stats* hs = a.stats;
-  rtkv_batch_stats* bs = reinterpret_cast<rtkv_batch_stats*>(hs + 1);
-  const int64_t ccount[3] = {(int64_t)fld(cnt, 0), (int64_t)fld(cnt, 1), (int64_t)fld(cnt, 2)};
-  publish_stats(g, false, ssum, pmn, pmx, ccount, ccount);
-  hs->score_m2 = M2;
-  bs->kept_score_sum = ssum;
+  __shared__ uint64_t s_line[16];
+  if (lane == 0) {
+    rtkv_layer_stats* hs = a.stats;
+    rtkv_batch_stats* bs = reinterpret_cast<rtkv_batch_stats*>(hs + 1);
+    const int64_t ccount[3] = {(int64_t)fld(cnt, 0), (int64_t)fld(cnt, 1), (int64_t)fld(cnt, 2)};
+    publish_stats(g, false, ssum, pmn, pmx, ccount, ccount, s_line);
+    hs->score_m2 = M2;
+    bs->kept_score_sum = ssum;
+  }
+  __builtin_amdgcn_wave_barrier();
+  asm volatile("" ::: "memory");
+  if (g.early) host_line_store(reinterpret_cast<uint64_t*>(g.early), s_line);
 }
 
 template <int TPT, bool HAS_T2, int DT>

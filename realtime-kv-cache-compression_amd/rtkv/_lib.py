@@ -73,9 +73,15 @@ class LayerOut(ctypes.Structure):
 
 
 class EarlyStats(ctypes.Structure):
-    """rtkv_early_stats: the layer statistics the device publishes to host memory (B = 1)."""
-    _fields_ = [("seq", ctypes.c_uint64), ("complete", c_i32), ("reserved", c_i32), ("stats", LayerStatsHeader),
-                ("batch", BatchStats), ("final_seq", ctypes.c_uint64), ("final_flags", c_i32), ("reserved2", c_i32)]
+    """rtkv_early_stats: the layer statistics the device publishes to host memory (B = 1) as one 128-byte
+    line with the seq in its first and last word, then K4's final word ((seq mod 2^48) << 16 | flags)."""
+    _fields_ = [("seq", ctypes.c_uint64), ("max_kept", c_i64), ("total_packed_bytes", c_i64), ("score_sum", c_d),
+                ("score_min", c_f), ("score_max", c_f), ("error_flags", c_i32), ("complete", c_i32),
+                ("class_count", c_i64 * 3), ("kept_class", c_i64 * 3), ("cost_units", c_i64), ("reserved", c_i64 * 2),
+                ("seq_tail", ctypes.c_uint64), ("final_word", ctypes.c_uint64), ("reserved2", ctypes.c_uint64 * 15)]
+
+
+FINAL_SEQ_MASK = (1 << 48) - 1  # rtkv_early_stats.final_word = (seq & mask) << 16 | flags
 
 
 class OutMailbox(ctypes.Structure):

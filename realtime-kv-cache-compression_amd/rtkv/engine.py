@@ -161,12 +161,12 @@ def decode_stats(raw: bytes, B: int) -> LayerStats:
 
 
 def _early_to_stats(e: L.EarlyStats) -> LayerStats:
-    """Statistics published early by the device (score_m2 / kept_score_sum are not final there)."""
-    h, b = e.stats, e.batch
-    row = dict(class_count=list(b.class_count), kept=b.kept, kept_class=list(b.kept_class), cost_units=b.cost_units,
-               packed_bytes=b.packed_bytes, fallback=bool(b.fallback), kept_score_sum=float("nan"))
-    return LayerStats(h.max_kept, h.total_packed_bytes, h.score_sum, float("nan"), h.score_min, h.score_max,
-                      h.error_flags, [row])
+    """Statistics published early by the device (score_m2 / kept_score_sum are not final there; B = 1, complete,
+    so kept = max_kept and packed_bytes = total_packed_bytes)."""
+    row = dict(class_count=list(e.class_count), kept=e.max_kept, kept_class=list(e.kept_class), cost_units=e.cost_units,
+               packed_bytes=e.total_packed_bytes, fallback=False, kept_score_sum=float("nan"))
+    return LayerStats(e.max_kept, e.total_packed_bytes, e.score_sum, float("nan"), e.score_min, e.score_max,
+                      e.error_flags, [row])
 
 
 class EarlyStatsBuffer:
@@ -193,10 +193,10 @@ class EarlyStatsBuffer:
     def final_flags(self, seq: int) -> Optional[int]:
         """The final RTKV_FLAG_* word K4 published for call `seq` (rtkv_compress_layer_finish), or None
         while that K4 has not started (or a later layer's K4 has overwritten it)."""
-        e = self._view
-        if ctypes.c_uint64.from_address(ctypes.addressof(e) + L.EarlyStats.final_seq.offset).value != seq:
+        w = ctypes.c_uint64.from_address(ctypes.addressof(self._view) + L.EarlyStats.final_word.offset).value
+        if (w >> 16) != (seq & L.FINAL_SEQ_MASK):
             return None
-        return int(e.final_flags)
+        return int(w & 0xffff)
 
     def wait_final(self, seq: int, device=None) -> int:
         """The final RTKV_FLAG_* word of call `seq` once its K4 has started and published it
@@ -208,7 +208,7 @@ class EarlyStatsBuffer:
             if flags is not None:
                 return flags
         L.check(rc, "rtkv_wait_final")
-        return int(self._view.final_flags)
+        return int(self._view.final_word & 0xffff)
 
     def wait(self, seq: int, device=None) -> L.EarlyStats:
         """The statistics of call `seq` once the device has published them.  A queue slower than the
@@ -218,7 +218,8 @@ class EarlyStatsBuffer:
         rc = self._lib.rtkv_wait_early(self.ptr, seq, self.TIMEOUT_US)
         if rc == L.ERR_TIMEOUT:
             torch.cuda.synchronize(device)  # also surfaces a device fault, if that is what happened
-            if self._read().seq == seq:
+            e = self._read()
+            if e.seq == seq and e.seq_tail == seq:
                 rc = 0
         L.check(rc, "rtkv_wait_early")
         return self._read()
@@ -558,7 +559,7 @@ class PendingLayer(LayerResult):
                 e = self._early.wait(self._seq, self.bufs.device)
                 if e.complete:
                     self._raw = e
-                    self._sizes = (e.stats.max_kept, e.stats.total_packed_bytes, e.stats.error_flags)
+                    self._sizes = (e.max_kept, e.total_packed_bytes, e.error_flags)
                     return self._sizes
             # incomplete (the top-10% fallback ran): the statistics need a stream sync, which an armed K4
             # would block (it waits for the host) — cancel it first; finish() then launches K4 itself
@@ -583,6 +584,13 @@ class PendingLayer(LayerResult):
         if self._early is None or not self.finished:
             return self.final_stats_unchecked().error_flags
         return self._early.wait_final(self._seq_final, self.bufs.device)
+
+    def _patch_out(self, kp, vp, pkp, pvp, n):
+        out = self._out
+        if self.bufs.emit_dequant:
+            out.k_out_dev, out.v_out_dev = kp, vp
+        if self.bufs.emit_packed:
+            out.packed_k_dev, out.packed_v_dev, out.packed_capacity = pkp, pvp, n
 
     def relaunch(self) -> "PendingLayer":
         """K4 through rtkv_compress_layer_finish into the posted outputs, after an armed K4 whose waiter
@@ -611,27 +619,28 @@ class PendingLayer(LayerResult):
         check_flags(flags)
         b = self.bufs
         dev = b.device
-        out = self._out
+        kp = vp = pkp = pvp = 0
+        n = 0
         if b.emit_dequant:
             kv = torch.empty((2, self.B, Sp, b.F), dtype=b.dtype, device=dev)
             kp = kv.data_ptr()
-            out.k_out_dev, out.v_out_dev = kp, kp + self.B * Sp * b.F * kv.element_size()
+            vp = kp + self.B * Sp * b.F * kv.element_size()
             self._kv = kv
         if b.emit_packed:
             n = (max(pb, 1) + 255) // 256 * 256
             codes = torch.empty((2, n), dtype=torch.uint8, device=dev)
-            cp = codes.data_ptr()
-            out.packed_k_dev, out.packed_v_dev = cp, cp + n
-            out.packed_capacity = n
+            pkp = codes.data_ptr()
+            pvp = pkp + n
             self._codes = codes
-        self._out_rows = max(Sp, 1)
+        self._out_rows = rows = max(Sp, 1)
         try:
             if self._armed is not None:  # K4 is queued behind its waiter: post the outputs, no launch
-                L.lib().rtkv_mailbox_post(self._armed.ptr, self._seq, out.k_out_dev, out.v_out_dev, out.packed_k_dev,
-                                          out.packed_v_dev, out.packed_capacity, max(Sp, 1))
+                L.lib().rtkv_mailbox_post(self._armed.ptr, self._seq, kp, vp, pkp, pvp, n, rows)
                 self._armed = None
+                self._patch_out(kp, vp, pkp, pvp, n)  # (after the post: only a relaunch reads it)
             else:
-                L.check(L.lib().rtkv_compress_layer_finish(*self._finish_args, max(Sp, 1), *self._finish_tail),
+                self._patch_out(kp, vp, pkp, pvp, n)
+                L.check(L.lib().rtkv_compress_layer_finish(*self._finish_args, rows, *self._finish_tail),
                         "rtkv_compress_layer_finish")
         finally:
             self._wso.pending = None

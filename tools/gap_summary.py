@@ -29,6 +29,8 @@ def phase(name):
         return "K1"
     if "quant_rows" in name:
         return "K4"
+    if "prefetch" in name or "waiter" in name:
+        return "PF"  # the drop-in's kept-row prefetch / the armed K4's waiter, between K2 and K4
     return "K2"
 
 
@@ -41,8 +43,8 @@ def region(label, first_layer, nlayers):
         nlayers = len(k1) - first_layer - 1
     if nlayers <= 0:
         return
-    dur = {"K1": [], "K2": [], "K4": []}
-    gap = {"K1": [], "K2": [], "K4": []}
+    dur = {"K1": [], "K2": [], "PF": [], "K4": []}
+    gap = {"K1": [], "K2": [], "PF": [], "K4": []}
     boundary = []
     for li in range(first_layer, first_layer + nlayers):
         for i in range(k1[li], k1[li + 1]):
@@ -58,7 +60,9 @@ def region(label, first_layer, nlayers):
                     gap[p].append(g)
     span = (int(rows[k1[first_layer + nlayers]]["Start_Timestamp"]) - int(rows[k1[first_layer]]["Start_Timestamp"])) / 1e3
     print(f"{label}: {nlayers} layers, {span / nlayers:.1f} us per layer start to start (run boundaries included)")
-    for p in ("K1", "K2", "K4"):
+    for p in ("K1", "K2", "PF", "K4"):
+        if not dur[p]:
+            continue
         g = sorted(gap[p]) or [0.0]
         print(f"  {p}: dur {statistics.mean(dur[p]):7.2f} us   gap before: mean {statistics.mean(g):6.2f}  "
               f"p50 {g[len(g) // 2]:6.2f}  p90 {g[len(g) * 9 // 10]:6.2f}  max {g[-1]:7.2f} us")
