@@ -59,11 +59,7 @@ enum rtkv_error_flag {
   RTKV_FLAG_SPIN_TIMEOUT = 2,
   /* rtkv_compress_layer_finish: the layer's S'_max or packed byte count exceeds the buffers the caller
    * declared (out_rows, packed_capacity); K4 wrote nothing. */
-  RTKV_FLAG_OUTPUT_OVERFLOW = 4,
-  /* armed K4 (rtkv_compress_layer_arm): the outputs were not posted within the waiter's bound
-   * (rtkv_set_arm_wait_us); K4 wrote nothing and published this flag in final_flags only (not an error of
-   * the layer: the host launches K4 with rtkv_compress_layer_finish instead). */
-  RTKV_FLAG_ARM_TIMEOUT = 8
+  RTKV_FLAG_OUTPUT_OVERFLOW = 4
 };
 
 /* Flags for rtkv_layer_params.flags */
@@ -344,7 +340,7 @@ typedef struct rtkv_early_stats {
   int64_t cost_units;
   int64_t reserved[2];
   uint64_t seq_tail;            /* word 15: seq again */
-  /* Written by K4 (rtkv_compress_layer_finish / _arm) when it starts, all selection waits being over: ONE
+  /* Written by K4 (rtkv_compress_layer_finish) when it starts, all selection waits being over: ONE
    * 8-byte store of (seq mod 2^48) << 16 | the layer's complete RTKV_FLAG_* word.  A flag raised after the
    * early publication (a look-back timeout) or by K4 itself (RTKV_FLAG_OUTPUT_OVERFLOW) is seen here
    * without a stream sync. */
@@ -397,42 +393,6 @@ int rtkv_compress_layer_finish(const rtkv_kv_desc* kv, const rtkv_layer_params* 
  * selection that timed out after the early publication raises in the layer's own call — where the
  * reference caller's try/except falls back for that layer (modified_llama.py:144-149). */
 int rtkv_wait_final(const rtkv_early_stats* early_host, uint64_t seq, int64_t timeout_us);
-/* Armed K4 (the drop-in's default; no reference counterpart).  Instead of rtkv_compress_layer_finish
- * after the host has read S' and allocated the outputs, rtkv_compress_layer_arm — called right after
- * rtkv_compress_layer_begin on the same stream — enqueues K4 at once, preceded by a small waiter kernel
- * that spins (bounded) on a pinned host mailbox and reads the first kept rows into the Infinity Cache
- * meanwhile (up to prefetch_bytes, as rtkv_prefetch_kept_rows).  The host then allocates K'/V' and the
- * code planes at their exact sizes and posts their addresses (rtkv_mailbox_post); K4 starts when the
- * waiter ends, with no host launch on the path between K2's publication and K4.  If the host cannot
- * post (an error), it must call rtkv_mailbox_cancel: K4 then writes nothing (the early statistics and
- * the per-token buffers stay valid).  A waiter that sees neither within its bound (rtkv_set_arm_wait_us,
- * default 20 ms: a host stalled by a GC pause or a synchronising runtime call) gives up; K4 then writes
- * nothing and publishes RTKV_FLAG_ARM_TIMEOUT in final_flags, and the host — which must wait for the
- * final flags before it trusts the outputs — launches K4 itself (rtkv_compress_layer_finish, with a
- * different final seq).  out: the begin call's per-token buffers and
- * row_capacity; its k_out/v_out/packed pointers only tell which outputs exist (any non-null value):
- * the mailbox supplies the real ones, 16-byte aligned, with packed_capacity and out_rows as for
- * rtkv_compress_layer_finish.  mailbox_host: rtkv_host_alloc memory, one per stream; seq: the begin
- * call's. */
-typedef struct rtkv_out_mailbox {
-  uint64_t seq;               /* written last (release, system scope) by rtkv_mailbox_post / _cancel */
-  uint64_t k_out_dev, v_out_dev, packed_k_dev, packed_v_dev;
-  int64_t packed_capacity;
-  int64_t out_rows;
-  int32_t cancel;             /* 1: the host cancelled, K4 writes and publishes nothing (2, device copy only:
-                                 the waiter timed out, K4 publishes RTKV_FLAG_ARM_TIMEOUT and writes nothing) */
-  int32_t reserved;
-} rtkv_out_mailbox;
-int rtkv_compress_layer_arm(const rtkv_kv_desc* kv, const rtkv_layer_params* p, const rtkv_layer_out* out,
-                            void* workspace_dev, size_t workspace_bytes, void* stream, rtkv_early_stats* early_host,
-                            uint64_t seq, rtkv_out_mailbox* mailbox_host, int64_t prefetch_bytes);
-void rtkv_mailbox_post(rtkv_out_mailbox* mailbox_host, uint64_t seq, void* k_out_dev, void* v_out_dev,
-                       void* packed_k_dev, void* packed_v_dev, int64_t packed_capacity, int64_t out_rows);
-void rtkv_mailbox_cancel(rtkv_out_mailbox* mailbox_host, uint64_t seq);
-/* How long an armed K4's waiter waits for the host's post, in microseconds of the device's real-time
- * counter (default 20000; 0: the default again; RTKV_ARM_WAIT_US sets the initial value).  Applies to
- * later rtkv_compress_layer_arm calls. */
-void rtkv_set_arm_wait_us(uint32_t us);
 /* start_event (nullable, a hipEvent_t): recorded on the stream right before K1, in the same call —
  * the start of the drop-in's processing_time.  (Recorded from the host separately before this call,
  * the timing event cost ~4.5 us of device idle per layer; recorded here, as rtkv_compress_layer_events

@@ -26,12 +26,10 @@ struct Workspace {
   uint8_t* labels;
   rtkv_layer_stats* stats;
   void* sel;
-  rtkv_out_mailbox* mbox;  // armed K4: the waiter's device copy of the host mailbox
 };
 static size_t ws_bytes(int64_t B, int64_t S) {
   return align_up((size_t)(B * S) * 4, 256) + align_up((size_t)S * 4, 256) + align_up((size_t)(B * S) * 8, 256) +
-         align_up((size_t)(B * S), 256) + align_up(rtkv_stats_bytes(B), 256) + align_up(select_workspace_bytes(B, S), 256) +
-         256;  // the armed K4's device copy of the output mailbox
+         align_up((size_t)(B * S), 256) + align_up(rtkv_stats_bytes(B), 256) + align_up(select_workspace_bytes(B, S), 256);
 }
 static int carve(void* ws, size_t bytes, int64_t B, int64_t S, Workspace& w) {
   if (!ws || bytes < ws_bytes(B, S)) {
@@ -50,8 +48,6 @@ static int carve(void* ws, size_t bytes, int64_t B, int64_t S, Workspace& w) {
   w.stats = reinterpret_cast<rtkv_layer_stats*>(p);
   p += align_up(rtkv_stats_bytes(B), 256);
   w.sel = p;
-  p += align_up(select_workspace_bytes(B, S), 256);
-  w.mbox = reinterpret_cast<rtkv_out_mailbox*>(p);
   return RTKV_OK;
 }
 
@@ -306,8 +302,7 @@ static int compress_layer_impl(const rtkv_kv_desc* kv, const rtkv_attn_desc* w, 
   a.mode_select = (p->flags & RTKV_NO_SELECTION) ? 2 : 1;
   const bool row_labels = select_fast_eligible(a);  // the fast path also writes each kept row's class
   a.row_label = row_labels ? ws.labels : nullptr;
-  static const bool no_early = getenv("RTKV_NO_EARLY") != nullptr;  // diagnostic: publish nothing (host syncs)
-  if (early && row_labels && !no_early) {  // the fast path's F1 publishes the final counts to the host
+  if (early && row_labels) {  // the fast path's F1 publishes the final counts to the host
     a.early = early;
     a.early_seq = early_seq;
     if (published) *published = 1;
@@ -402,57 +397,6 @@ int rtkv_compress_layer_finish(const rtkv_kv_desc* kv, const rtkv_layer_params* 
   q.final_seq = seq;
   q.t_end = reinterpret_cast<unsigned long long*>(layer_times(out->stats_dev, kv->B)->end);
   return launch_quant(q, (hipStream_t)stream);
-}
-
-int rtkv_compress_layer_arm(const rtkv_kv_desc* kv, const rtkv_layer_params* p, const rtkv_layer_out* out,
-                            void* workspace_dev, size_t workspace_bytes, void* stream, rtkv_early_stats* early_host,
-                            uint64_t seq, rtkv_out_mailbox* mailbox_host, int64_t prefetch_bytes) {
-  int rc = check_params(p);
-  if (rc) return rc;
-  RTKV_REQUIRE(kv && out && mailbox_host && out->labels_dev && out->kept_index_dev && out->stats_dev,
-               "compress_layer_arm needs the begin call's per-token buffers and a mailbox");
-  RTKV_REQUIRE(out->row_capacity >= kv->S, "row_capacity must be the capacity rtkv_compress_layer_begin used (>= S)");
-  if (p->flags & RTKV_EMIT_PACKED)
-    RTKV_REQUIRE(out->row_offset_dev && out->scale_zp_dev, "EMIT_PACKED needs row_offset and scale_zp");
-  if (p->flags & RTKV_EMIT_DEQUANT) RTKV_REQUIRE(out->o_stride_b < 0, "EMIT_DEQUANT needs o_stride_b = -1");
-  Workspace ws;
-  rc = carve(workspace_dev, workspace_bytes, kv->B, kv->S, ws);
-  if (rc) return rc;
-  const bool row_labels = select_fast_shape(kv->B, kv->S) && !(p->flags & RTKV_SELECT_PIPELINE);
-  rtkv_layer_out o = *out;  // placeholders: the mailbox supplies the outputs (16-byte aligned)
-  o.k_out_dev = o.v_out_dev = (p->flags & RTKV_EMIT_DEQUANT) ? reinterpret_cast<void*>((uintptr_t)256) : nullptr;
-  o.packed_k_dev = o.packed_v_dev = (p->flags & RTKV_EMIT_PACKED) ? reinterpret_cast<uint8_t*>((uintptr_t)256) : nullptr;
-  QuantArgs q = make_quant_args(kv, out->labels_dev, out->kept_index_dev, p, &o, row_labels ? ws.labels : nullptr);
-  q.out_ind = ws.mbox;
-  q.final_host = early_host;
-  q.final_seq = seq;
-  static const bool no_stamp = getenv("RTKV_NO_KSTAMP") != nullptr;  // diagnostic: K4 without end stamps
-  q.t_end = no_stamp ? nullptr : reinterpret_cast<unsigned long long*>(layer_times(out->stats_dev, kv->B)->end);
-  hipStream_t st = (hipStream_t)stream;
-  rc = launch_k4_waiter(mailbox_host, seq, ws.mbox, out->stats_dev, kv, out->kept_index_dev, prefetch_bytes, st);
-  if (rc) return rc;
-  return launch_quant(q, st);
-}
-
-void rtkv_mailbox_post(rtkv_out_mailbox* mb, uint64_t seq, void* k_out_dev, void* v_out_dev, void* packed_k_dev,
-                       void* packed_v_dev, int64_t packed_capacity, int64_t out_rows) {
-  if (!mb) return;
-  mb->k_out_dev = (uint64_t)(uintptr_t)k_out_dev;
-  mb->v_out_dev = (uint64_t)(uintptr_t)v_out_dev;
-  mb->packed_k_dev = (uint64_t)(uintptr_t)packed_k_dev;
-  mb->packed_v_dev = (uint64_t)(uintptr_t)packed_v_dev;
-  mb->packed_capacity = packed_capacity;
-  mb->out_rows = out_rows;
-  mb->cancel = 0;
-  __atomic_store_n(&mb->seq, seq, __ATOMIC_RELEASE);
-}
-
-void rtkv_set_arm_wait_us(uint32_t us) { set_arm_wait_us(us); }
-
-void rtkv_mailbox_cancel(rtkv_out_mailbox* mb, uint64_t seq) {
-  if (!mb) return;
-  mb->cancel = 1;
-  __atomic_store_n(&mb->seq, seq, __ATOMIC_RELEASE);
 }
 
 int rtkv_prefetch_kept_rows(const rtkv_kv_desc* kv, const rtkv_layer_out* out, int64_t max_bytes, void* stream) {

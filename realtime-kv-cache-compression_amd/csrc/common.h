@@ -293,29 +293,7 @@ struct QuantArgs {
   uint64_t final_seq;
   // rtkv_layer_times.end of the fused driver's layer (atomic max over K4's workgroups), or null
   unsigned long long* t_end;
-  // armed K4 (rtkv_compress_layer_arm): the outputs come from this device copy of the host mailbox,
-  // written by the waiter kernel that precedes K4 (k4_resolve), or null
-  const rtkv_out_mailbox* out_ind;
 };
-// Armed K4: replace the placeholder output pointers by the posted ones (a cancelled or timed-out post
-// leaves no output: the gate then writes nothing).  Scalar loads of memory the previous kernel wrote.
-__device__ __forceinline__ void k4_resolve(QuantArgs& a) {
-  const rtkv_out_mailbox* m = a.out_ind;
-  if (!m) return;
-  const bool off = m->cancel != 0;
-  const bool dq = a.out.k_out_dev != nullptr, pk = a.out.packed_k_dev != nullptr;
-  a.out.k_out_dev = (dq && !off) ? reinterpret_cast<void*>(m->k_out_dev) : nullptr;
-  a.out.v_out_dev = (dq && !off) ? reinterpret_cast<void*>(m->v_out_dev) : nullptr;
-  a.out.packed_k_dev = (pk && !off) ? reinterpret_cast<uint8_t*>(m->packed_k_dev) : nullptr;
-  a.out.packed_v_dev = (pk && !off) ? reinterpret_cast<uint8_t*>(m->packed_v_dev) : nullptr;
-  a.out.packed_capacity = pk ? m->packed_capacity : ((int64_t)1 << 62);
-  a.out_rows = dq ? m->out_rows : ((int64_t)1 << 62);
-  if (off) a.out.scale_zp_dev = nullptr;
-}
-uint32_t arm_wait_us();
-void set_arm_wait_us(uint32_t us);
-int launch_k4_waiter(const rtkv_out_mailbox* host, uint64_t seq, rtkv_out_mailbox* dev, rtkv_layer_stats* stats,
-                     const rtkv_kv_desc* kv, const int32_t* kept_index, int64_t prefetch_bytes, hipStream_t st);
 // rtkv_layer_times.end: the waves of K4 that wrote one of the layer's last rows (kStampWindow tasks,
 // quant_impl.h) stamp their end into slot (wave index mod RTKV_TIME_SLOTS), the largest stays.  Per wave, no
 // barrier (a workgroup-end barrier held finished waves' slots: K4 +7 %); spread over 128-byte lines (one

@@ -234,11 +234,10 @@ __global__ __launch_bounds__(256) void qk_importance_kernel(QKArgs g) {
 #ifndef QK_HEAD_WPE
 #define QK_HEAD_WPE 4
 #endif
-// COAL: the query tiles are loaded row-contiguous (each wave-instruction 4 rows × 256 B = 1 KiB, where the
-// fragment-shaped load touches 16 rows × 64 B) and put into the MFMA A-fragment layout through a
-// wave-private 4 KiB LDS buffer (swizzled like the keys), at the cost of 16 KiB more LDS per workgroup.
-template <int DT, int NT, int KS, bool COAL = false>
-__global__ __launch_bounds__(256, COAL ? 3 : QK_HEAD_WPE) void qk_head_kernel(QKArgs g, float* __restrict__ part, int rpw) {
+// (Row-contiguous query loads through a wave-private LDS transpose measured slower: 60 against 49 us per cfg3
+// f16 layer at 3 waves per SIMD, profiles/r05_qk_coal_ab.json.)
+template <int DT, int NT, int KS>
+__global__ __launch_bounds__(256, QK_HEAD_WPE) void qk_head_kernel(QKArgs g, float* __restrict__ part, int rpw) {
   using FT = typename Frag<DT>::T;
   using S_ = typename Dt<DT>::S;
   constexpr int D = 32 * KS;
@@ -280,24 +279,13 @@ __global__ __launch_bounds__(256, COAL ? 3 : QK_HEAD_WPE) void qk_head_kernel(QK
   const int ntile = rpw / 16;
   auto load_tile = [&](int k, FT (&a)[KS], f32x4& l) {  // tile k of this wave (clamped rows)
     const int r0 = wrow + 16 * (k < ntile ? k : ntile - 1);
-    if constexpr (COAL) {  // instruction j: rows r0 + 4j + (lane >> 4), chunk lane & 15 (KS == 4: 16 chunks)
+    const int qr = r0 + c16 < S ? r0 + c16 : S - 1;
+    const S_* qp = Qh + (int64_t)qr * q.q_stride_s;
 #pragma unroll
-      for (int j = 0; j < KS; ++j) {
-        const int rr = r0 + 4 * j + (lane >> 4);
-        const int qr = rr < S ? rr : S - 1;
-        a[j] = *reinterpret_cast<const FT*>(Qh + (int64_t)qr * q.q_stride_s + (lane & 15) * 8);
-      }
-    } else {
-      const int qr = r0 + c16 < S ? r0 + c16 : S - 1;
-      const S_* qp = Qh + (int64_t)qr * q.q_stride_s;
-#pragma unroll
-      for (int s_ = 0; s_ < KS; ++s_) a[s_] = *reinterpret_cast<const FT*>(qp + (4 * s_ + kg) * 8);
-    }
+    for (int s_ = 0; s_ < KS; ++s_) a[s_] = *reinterpret_cast<const FT*>(qp + (4 * s_ + kg) * 8);
     const int lr = r0 + 4 * kg < S ? r0 + 4 * kg : S - 4;
     l = *reinterpret_cast<const f32x4*>(Lh + lr);
   };
-  static_assert(!COAL || KS == 4, "COAL: 256-byte query rows");
-  uint8_t* qbuf = lds + KEY_BYTES + wave * 16 * RB;  // COAL: this wave's 16-row transpose buffer
   FT qa[KS], qn[KS];
   f32x4 ql, qln;
   load_tile(0, qa, ql);
@@ -312,17 +300,6 @@ __global__ __launch_bounds__(256, COAL ? 3 : QK_HEAD_WPE) void qk_head_kernel(QK
     uint32_t kofs = 0;  // opaque zero offset: the LDS reads stay in the loop (and ds_read, not flat)
     asm volatile("" : "+v"(kofs));
     const uint8_t* kt = lds + kofs;
-    if constexpr (COAL) {  // row-contiguous pieces → LDS (chunk c of row r at c ^ r) → A fragments
-#pragma unroll
-      for (int j = 0; j < KS; ++j) {
-        const int rr = 4 * j + (lane >> 4), cc = lane & 15;
-        *reinterpret_cast<FT*>(qbuf + kofs + rr * RB + ((cc ^ (rr & (CH - 1))) * 16)) = qa[j];
-      }
-      asm volatile("" ::: "memory");  // wave-private: the reads below come after the writes (in-order LDS)
-#pragma unroll
-      for (int s_ = 0; s_ < KS; ++s_)
-        qa[s_] = *reinterpret_cast<const FT*>(qbuf + kofs + c16 * RB + (((4 * s_ + kg) ^ (c16 & (CH - 1))) * 16));
-    }
     f32x4 acc[NT];
 #pragma unroll
     for (int t = 0; t < NT; ++t) {
@@ -438,8 +415,7 @@ static int launch_qk_head_reduce(const QKArgs& a, float* part, hipStream_t st, i
 
 template <int DT, int NT, int KS>
 static int launch_qk_head(const QKArgs& a, float* part, hipStream_t st, int* nparts) {
-  static const bool coal = getenv("RTKV_QK_COAL") != nullptr;  // A/B knob: row-contiguous query loads
-  const size_t lds = (size_t)(16 * NT) * (64 * KS) + (coal ? (size_t)4 * 16 * (64 * KS) : 0);
+  const size_t lds = (size_t)(16 * NT) * (64 * KS);
   const int64_t S = a.q.S;
   // rows per wave: 16-row tiles, enough workgroups to fill the chip (>= 1024 with the heads)
   // RTKV_QK_WGS: workgroups to aim for.  1024 (128 rows per wave: the head's 32 KB of keys staged once per
@@ -452,8 +428,7 @@ static int launch_qk_head(const QKArgs& a, float* part, hipStream_t st, int* npa
   int rpw = 256;
   while (rpw > 16 && (S + 4 * rpw - 1) / (4 * rpw) * a.q.H * a.q.B < target) rpw /= 2;
   const dim3 grid((unsigned)((S + 4 * rpw - 1) / (4 * rpw)), (unsigned)a.q.H, (unsigned)a.q.B);
-  if (coal) hipLaunchKernelGGL((qk_head_kernel<DT, NT, KS, true>), grid, dim3(256), lds, st, a, part, rpw);
-  else hipLaunchKernelGGL((qk_head_kernel<DT, NT, KS>), grid, dim3(256), lds, st, a, part, rpw);
+  hipLaunchKernelGGL((qk_head_kernel<DT, NT, KS>), grid, dim3(256), lds, st, a, part, rpw);
   RTKV_HIP_CHECK(hipGetLastError());
   QKArgs r = a;
   r.ex.t_begin = nullptr;  // the layer started with the head kernel

@@ -115,100 +115,6 @@ int launch_prefetch_rows(const rtkv_kv_desc* kv, const int32_t* kept_index, cons
   return RTKV_OK;
 }
 
-// ------------------------------------------------------------------------------------ armed K4 waiter
-// Enqueued between K2 and the armed K4 (rtkv_compress_layer_arm): lane 0 of workgroup 0 spins on the
-// pinned host mailbox until the host posts (or cancels) this layer's outputs, copies the mailbox to device
-// memory for K4 (k4_resolve) and ends; the other workgroups read the first kept rows meanwhile (the
-// prefetch above, over the host's allocation window).  Bounded: after `ticks` of the 100 MHz real-time
-// counter the copy is marked timed out (cancel = 2): K4 writes nothing, publishes RTKV_FLAG_ARM_TIMEOUT and
-// the host launches K4 itself.
-__global__ __launch_bounds__(256) void k4_waiter_kernel(const rtkv_out_mailbox* __restrict__ host, uint64_t seq,
-                                                        rtkv_out_mailbox* __restrict__ dev,
-                                                        rtkv_layer_stats* __restrict__ stats, uint64_t ticks,
-                                                        const uint8_t* __restrict__ k, const uint8_t* __restrict__ v,
-                                                        int64_t sss, int64_t row_bytes,
-                                                        const int32_t* __restrict__ kept_index, int64_t S,
-                                                        int64_t max_rows) {
-  if (blockIdx.x == 0) {
-    if (threadIdx.x != 0) return;
-    uint64_t* sq = const_cast<uint64_t*>(&host->seq);
-    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-    bool ok = true;
-    while (__hip_atomic_load(sq, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) != seq) {
-      if (__builtin_amdgcn_s_memrealtime() - t0 > ticks) { ok = false; break; }
-      __builtin_amdgcn_s_sleep(8);
-    }
-    rtkv_out_mailbox m;
-    if (ok) {
-      auto ld64 = [](const uint64_t* p) {
-        return __hip_atomic_load(const_cast<uint64_t*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-      };
-      m.k_out_dev = ld64(&host->k_out_dev);
-      m.v_out_dev = ld64(&host->v_out_dev);
-      m.packed_k_dev = ld64(&host->packed_k_dev);
-      m.packed_v_dev = ld64(&host->packed_v_dev);
-      m.packed_capacity = (int64_t)ld64(reinterpret_cast<const uint64_t*>(&host->packed_capacity));
-      m.out_rows = (int64_t)ld64(reinterpret_cast<const uint64_t*>(&host->out_rows));
-      m.cancel = __hip_atomic_load(const_cast<int32_t*>(&host->cancel), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    } else {
-      m.k_out_dev = m.v_out_dev = m.packed_k_dev = m.packed_v_dev = 0;
-      m.packed_capacity = m.out_rows = 0;
-      m.cancel = 2;  // timed out: K4 publishes RTKV_FLAG_ARM_TIMEOUT and writes nothing
-    }
-    m.seq = seq;
-    m.reserved = 0;
-    *dev = m;  // visible to K4: the kernel boundary
-    return;
-  }
-  // prefetch of K4's first tasks (as prefetch_rows_kernel), workgroups 1..
-  const int64_t kept = stats->max_kept < max_rows ? stats->max_kept : max_rows;
-  const int lane = threadIdx.x & 63;
-  const int64_t t = (int64_t)(blockIdx.x - 1) * (blockDim.x >> 6) + (threadIdx.x >> 6);
-  const int64_t r = t >> 1;
-  if (r >= kept) return;
-  const int64_t i = kept_index[r];
-  if (i < 0 || i >= S) return;
-  const uint8_t* src = ((t & 1) ? v : k) + i * sss;
-  uint32_t acc = 0;
-  for (int64_t o = (int64_t)lane * 16; o < row_bytes; o += 64 * 16) {
-    const uint4 x = *reinterpret_cast<const uint4*>(src + o);
-    acc ^= x.x ^ x.w;
-  }
-  asm volatile("" ::"v"(acc));
-}
-
-// the waiter's bound in microseconds: 20 ms by default (the host's post normally comes ~10-20 us after K2's
-// publication; past the bound the host relaunches K4, so the bound only trades a stalled GPU for a relaunch);
-// RTKV_ARM_WAIT_US or rtkv_set_arm_wait_us (tests) override
-static uint32_t g_arm_us = 0;
-uint32_t arm_wait_us() {
-  if (!g_arm_us) {
-    const char* e = getenv("RTKV_ARM_WAIT_US");
-    g_arm_us = e ? (uint32_t)strtoul(e, nullptr, 10) : 20000u;
-    if (!g_arm_us) g_arm_us = 1;
-  }
-  return g_arm_us;
-}
-void set_arm_wait_us(uint32_t us) { g_arm_us = us ? us : 20000u; }
-
-int launch_k4_waiter(const rtkv_out_mailbox* host, uint64_t seq, rtkv_out_mailbox* dev, rtkv_layer_stats* stats,
-                     const rtkv_kv_desc* kv, const int32_t* kept_index, int64_t prefetch_bytes, hipStream_t st) {
-  RTKV_REQUIRE(host && dev && stats && kv && kept_index, "compress_layer_arm: null pointer");
-  const uint64_t ticks = (uint64_t)arm_wait_us() * 100;  // s_memrealtime: 100 MHz
-  const int esz = kv->dtype == RTKV_F32 ? 4 : 2;
-  const int64_t row_bytes = kv->H * kv->D * esz;
-  const bool ok = kv->B == 1 && (kv->H == 1 || kv->stride_h == kv->D) && (row_bytes % 16) == 0 &&
-                  ((kv->stride_s * esz) % 16) == 0 && (((uintptr_t)kv->k_dev | (uintptr_t)kv->v_dev) & 15) == 0;
-  int64_t rows = ok && prefetch_bytes > 0 ? prefetch_bytes / (2 * row_bytes) : 0;
-  if (rows > kv->S) rows = kv->S;
-  const int64_t blocks = 1 + (2 * rows + 3) / 4;
-  hipLaunchKernelGGL(k4_waiter_kernel, dim3((unsigned)blocks), dim3(256), 0, st, host, seq, dev, stats, ticks,
-                     static_cast<const uint8_t*>(kv->k_dev), static_cast<const uint8_t*>(kv->v_dev), kv->stride_s * esz,
-                     row_bytes, kept_index, kv->S, rows);
-  RTKV_HIP_CHECK(hipGetLastError());
-  return RTKV_OK;
-}
-
 // ------------------------------------------------------------------------------------ shard ranges
 // ranges[b][j] = {first output row, first packed byte} of rank j's tokens [j*S_local, (j+1)*S_local)
 // (j = nranks: one past the last kept row of batch row b).  kept_index is ascending per batch row.

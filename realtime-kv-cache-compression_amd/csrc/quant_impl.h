@@ -473,12 +473,6 @@ __device__ __forceinline__ bool k4_layer_gate(const QuantArgs& a) {
   const bool over = a.out_rows > 0 && ((a.out.k_out_dev && max_kept > a.out_rows) ||
                                        (a.out.packed_k_dev && nbytes > a.out.packed_capacity));
   if (over) flags |= RTKV_FLAG_OUTPUT_OVERFLOW;
-  // armed K4: a host cancel (1) writes nothing and publishes nothing (the host launches K4 itself after a
-  // sync, or has raised); a waiter timeout (2) writes nothing and publishes RTKV_FLAG_ARM_TIMEOUT (the host
-  // then launches K4 itself)
-  const int cancel = a.out_ind ? a.out_ind->cancel : 0;
-  if (cancel == 1) return true;
-  if (cancel == 2) flags |= RTKV_FLAG_ARM_TIMEOUT;
   if (blockIdx.x == 0 && threadIdx.x == 0) {
     if (over) atomicOr(&st->error_flags, (int)RTKV_FLAG_OUTPUT_OVERFLOW);
     if (a.final_host)  // one 8-byte store: seq and flags together (no ordering wait)
@@ -487,7 +481,6 @@ __device__ __forceinline__ bool k4_layer_gate(const QuantArgs& a) {
                          __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
   if (over) return true;
-  if (cancel) return true;
   if (!(flags & RTKV_FLAG_SPIN_TIMEOUT)) return false;
   if (a.S_glob != 0 || !a.kept_index) return true;  // shard launches: the host raises; nothing to poison locally
   using S_ = typename Dt<DT>::S;
@@ -524,9 +517,7 @@ constexpr int kStampWindow = 2048;
 // PKW > 0 (compile time): packed codes + scale/zero-point only (no dequantized K'/V': the decode and packed
 // consumers' mode), the dequantization path compiled out, at a launch bound of PKW waves per SIMD.
 template <int DT, int NCH, bool CONTIG, bool FULL, int PKW = 0>
-__global__ __launch_bounds__(256, PKW ? PKW : ((DT == RTKV_F32 && NCH == 8 && FULL && CONTIG) ? 4 : 2)) void quant_rows_kernel(QuantArgs a_in) {
-  QuantArgs a = a_in;
-  k4_resolve(a);  // armed K4: the posted outputs
+__global__ __launch_bounds__(256, PKW ? PKW : ((DT == RTKV_F32 && NCH == 8 && FULL && CONTIG) ? 4 : 2)) void quant_rows_kernel(QuantArgs a) {
   constexpr bool PK_ONLY = PKW > 0;
   using S_ = typename Dt<DT>::S;
   const int lane = threadIdx.x & 63;
@@ -656,9 +647,7 @@ __global__ __launch_bounds__(256, PKW ? PKW : ((DT == RTKV_F32 && NCH == 8 && FU
 // row's min / max / min |x| / NaN flag are combined through LDS; fminf/fmaxf are order-independent
 // (a zero's sign reaches neither scale nor zero-point), so every output equals quant_rows_kernel's.
 template <int DT, int NCHW, int NSPLIT>
-__global__ __launch_bounds__(64 * NSPLIT) void quant_rows_split_kernel(QuantArgs a_in) {
-  QuantArgs a = a_in;
-  k4_resolve(a);  // armed K4: the posted outputs
+__global__ __launch_bounds__(64 * NSPLIT) void quant_rows_split_kernel(QuantArgs a) {
   using S_ = typename Dt<DT>::S;
   const int lane = threadIdx.x & 63;
   const int q = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -742,9 +731,7 @@ __global__ __launch_bounds__(64 * NSPLIT) void quant_rows_split_kernel(QuantArgs
 
 // Generic path: any D, any alignment, any F (scalar element access, partial last chunk).
 template <int DT>
-__global__ __launch_bounds__(256) void quant_rows_generic_kernel(QuantArgs a_in) {
-  QuantArgs a = a_in;
-  k4_resolve(a);  // armed K4: the posted outputs
+__global__ __launch_bounds__(256) void quant_rows_generic_kernel(QuantArgs a) {
   using S_ = typename Dt<DT>::S;
   const int lane = threadIdx.x & 63;
   const int64_t gw = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);

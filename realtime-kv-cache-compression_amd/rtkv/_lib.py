@@ -19,7 +19,7 @@ LIB_PATH = os.environ.get("RTKV_LIB", os.path.join(ROOT, "librtkv.so"))
 F32, F16, BF16 = 0, 1, 2
 EMIT_DEQUANT, EMIT_PACKED, NO_SELECTION, NO_FALLBACK, SELECT_PIPELINE = 1, 2, 4, 8, 16
 TEST_WITHHOLD_SELECTION, TEST_WITHHOLD_LOOKBACK = 1 << 16, 1 << 17
-FLAG_F16_QMAX_OVERFLOW, FLAG_SPIN_TIMEOUT, FLAG_OUTPUT_OVERFLOW, FLAG_ARM_TIMEOUT = 1, 2, 4, 8
+FLAG_F16_QMAX_OVERFLOW, FLAG_SPIN_TIMEOUT, FLAG_OUTPUT_OVERFLOW = 1, 2, 4
 ERR_NAMES = {-1: "RTKV_ERR_INVALID", -2: "RTKV_ERR_UNSUPPORTED", -3: "RTKV_ERR_HIP", -4: "RTKV_ERR_WORKSPACE",
              -5: "RTKV_ERR_TIMEOUT"}
 ERR_TIMEOUT = -5
@@ -84,13 +84,6 @@ class EarlyStats(ctypes.Structure):
 FINAL_SEQ_MASK = (1 << 48) - 1  # rtkv_early_stats.final_word = (seq & mask) << 16 | flags
 
 
-class OutMailbox(ctypes.Structure):
-    """rtkv_out_mailbox: the armed K4's outputs, posted by the host (rtkv_mailbox_post / _cancel)."""
-    _fields_ = [("seq", ctypes.c_uint64), ("k_out_dev", ctypes.c_uint64), ("v_out_dev", ctypes.c_uint64),
-                ("packed_k_dev", ctypes.c_uint64), ("packed_v_dev", ctypes.c_uint64), ("packed_capacity", c_i64),
-                ("out_rows", c_i64), ("cancel", c_i32), ("reserved", c_i32)]
-
-
 _WALL_KHZ = {}
 
 
@@ -153,10 +146,6 @@ _SIGS = {
     "rtkv_compress_layer_qk_begin": ([c_p, c_p, c_p, c_p, c_p, c_sz, c_p, c_p, ctypes.c_uint64, c_p, c_p], c_i32),
     "rtkv_compress_layer_finish": ([c_p, c_p, c_p, c_i64, c_p, c_sz, c_p, c_p, ctypes.c_uint64], c_i32),
     "rtkv_prefetch_kept_rows": ([c_p, c_p, c_i64, c_p], c_i32),
-    "rtkv_compress_layer_arm": ([c_p, c_p, c_p, c_p, c_sz, c_p, c_p, ctypes.c_uint64, c_p, c_i64], c_i32),
-    "rtkv_mailbox_post": ([c_p, ctypes.c_uint64, c_p, c_p, c_p, c_p, c_i64, c_i64], None),
-    "rtkv_mailbox_cancel": ([c_p, ctypes.c_uint64], None),
-    "rtkv_set_arm_wait_us": ([ctypes.c_uint32], None),
     "rtkv_wall_clock_khz": ([c_i32], c_i64),
     "rtkv_mask_key_padding": ([c_p, c_i32, c_i64, c_i64, c_i64, c_i64, c_i64, c_f, c_p, c_i64, c_p, c_p], c_i32),
     "rtkv_host_alloc": ([c_sz], c_p),

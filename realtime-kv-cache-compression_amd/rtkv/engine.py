@@ -230,22 +230,6 @@ class EarlyStatsBuffer:
             self.ptr = None
 
 
-class OutMailbox:
-    """Pinned host rtkv_out_mailbox (rtkv_host_alloc) through which the host posts an armed K4's outputs
-    (rtkv_compress_layer_arm); one per device and stream (layer l+1 posts only after layer l's K4 ran)."""
-
-    def __init__(self):
-        self._lib = L.lib()
-        self.ptr = self._lib.rtkv_host_alloc(ctypes.sizeof(L.OutMailbox))
-        if not self.ptr:
-            raise RuntimeError("rtkv: rtkv_host_alloc failed (pinned host memory for the output mailbox)")
-
-    def __del__(self):
-        if getattr(self, "ptr", None):
-            self._lib.rtkv_host_free(self.ptr)
-            self.ptr = None
-
-
 class Workspace:
     """Caller-owned scratch for the C ABI, grown on demand (one per device).
 
@@ -524,31 +508,6 @@ class PendingLayer(LayerResult):
         self.finished = False
         self._raw = None    # the early publication as the device wrote it (converted lazily by stats())
         self._sizes = None
-        self._armed = None  # the OutMailbox of an armed K4 until it is posted or cancelled
-        self._seq_final = seq  # the sequence number K4 publishes its final flags under
-
-    def arm(self, mailbox: "OutMailbox", prefetch_bytes: int = 0) -> "PendingLayer":
-        """Enqueue K4 now (rtkv_compress_layer_arm), behind a waiter kernel that reads the outputs from
-        `mailbox` (and the first kept rows meanwhile): finish() then only allocates and posts, no launch.
-        Only for a layer that publishes its statistics early (the one-launch K2)."""
-        if self._early is None:
-            raise RuntimeError("rtkv: arm() needs a layer with early statistics")
-        L.check(L.lib().rtkv_compress_layer_arm(self._finish_args[0], self._finish_args[1], self._finish_args[2],
-                                                self._finish_tail[0], self._finish_tail[1], self._stream,
-                                                self._finish_tail[3], self._seq, mailbox.ptr, int(prefetch_bytes)),
-                "rtkv_compress_layer_arm")
-        self._armed = mailbox
-        return self
-
-    def cancel_armed(self):
-        """An armed K4 whose outputs will not be posted: it writes nothing (its waiter ends at once)."""
-        if self._armed is not None:
-            L.lib().rtkv_mailbox_cancel(self._armed.ptr, self._seq)
-            self._armed = None
-
-    def __del__(self):
-        if getattr(self, "_armed", None) is not None:  # never leave an armed K4 waiting for the host
-            self.cancel_armed()
 
     def sizes(self):
         """(S'_max, packed bytes per code plane, error flags) for the output allocation: straight from the
@@ -561,9 +520,6 @@ class PendingLayer(LayerResult):
                     self._raw = e
                     self._sizes = (e.max_kept, e.total_packed_bytes, e.error_flags)
                     return self._sizes
-            # incomplete (the top-10% fallback ran): the statistics need a stream sync, which an armed K4
-            # would block (it waits for the host) — cancel it first; finish() then launches K4 itself
-            self.cancel_armed()
             st = self.stats()
             self._sizes = (st.max_kept, st.total_packed_bytes, st.error_flags)
         return self._sizes
@@ -576,14 +532,14 @@ class PendingLayer(LayerResult):
     def final_flags(self) -> Optional[int]:
         """The layer's complete RTKV_FLAG_* word as K4 published it (no stream sync), or None when it is
         not (yet) available: no early buffer, K4 not started, or overwritten by a later layer's K4."""
-        return self._early.final_flags(self._seq_final) if self._early is not None and self.finished else None
+        return self._early.final_flags(self._seq) if self._early is not None and self.finished else None
 
     def wait_final_flags(self) -> int:
         """Wait (host spin, no stream sync) until this layer's K4 has started and published the layer's
         final flags, and return them; a layer without an early buffer syncs its stream instead."""
         if self._early is None or not self.finished:
             return self.final_stats_unchecked().error_flags
-        return self._early.wait_final(self._seq_final, self.bufs.device)
+        return self._early.wait_final(self._seq, self.bufs.device)
 
     def _patch_out(self, kp, vp, pkp, pvp, n):
         out = self._out
@@ -592,29 +548,10 @@ class PendingLayer(LayerResult):
         if self.bufs.emit_packed:
             out.packed_k_dev, out.packed_v_dev, out.packed_capacity = pkp, pvp, n
 
-    def relaunch(self) -> "PendingLayer":
-        """K4 through rtkv_compress_layer_finish into the posted outputs, after an armed K4 whose waiter
-        gave up before the post (RTKV_FLAG_ARM_TIMEOUT: it wrote nothing).  Its final flags come under a
-        sequence number of their own."""
-        self._seq_final = self._seq | (1 << 62)
-        ws_ptr, ws_bytes, stream, early_ptr, _ = self._finish_tail
-        L.check(L.lib().rtkv_compress_layer_finish(*self._finish_args, self._out_rows, ws_ptr, ws_bytes, stream,
-                                                    early_ptr, self._seq_final), "rtkv_compress_layer_finish")
-        self._record(self._stream)
-        return self
-
     def finish(self) -> "PendingLayer":
         """Allocate K'/V' [B, S', F] and the packed codes at their exact sizes and enqueue K4 into them.
         Between the early statistics and this launch the device only runs K2's tail, so this path is
-        kept short: one allocation for K'+V', one for both code planes, the begin call's LayerOut patched.
-        An armed layer (arm()) posts the outputs to its waiting K4 instead of launching it."""
-        try:
-            return self._finish()
-        except BaseException:
-            self.cancel_armed()  # an armed K4 must not wait for outputs that will never be posted
-            raise
-
-    def _finish(self) -> "PendingLayer":
+        kept short: one allocation for K'+V', one for both code planes, the begin call's LayerOut patched."""
         Sp, pb, flags = self.sizes()
         check_flags(flags)
         b = self.bufs
@@ -633,15 +570,10 @@ class PendingLayer(LayerResult):
             pvp = pkp + n
             self._codes = codes
         self._out_rows = rows = max(Sp, 1)
+        self._patch_out(kp, vp, pkp, pvp, n)
         try:
-            if self._armed is not None:  # K4 is queued behind its waiter: post the outputs, no launch
-                L.lib().rtkv_mailbox_post(self._armed.ptr, self._seq, kp, vp, pkp, pvp, n, rows)
-                self._armed = None
-                self._patch_out(kp, vp, pkp, pvp, n)  # (after the post: only a relaunch reads it)
-            else:
-                self._patch_out(kp, vp, pkp, pvp, n)
-                L.check(L.lib().rtkv_compress_layer_finish(*self._finish_args, rows, *self._finish_tail),
-                        "rtkv_compress_layer_finish")
+            L.check(L.lib().rtkv_compress_layer_finish(*self._finish_args, rows, *self._finish_tail),
+                    "rtkv_compress_layer_finish")
         finally:
             self._wso.pending = None
         self.finished = True
@@ -656,7 +588,6 @@ class PendingLayer(LayerResult):
 
     def final_stats_unchecked(self) -> LayerStats:
         if not self.finished and self._final is None:  # no completion event yet: K1+K2 on the layer's stream
-            self.cancel_armed()  # (a stream sync would wait for an armed K4 that waits for the host)
             torch.cuda.ExternalStream(self._stream, device=self.bufs.device).synchronize()
         return super().final_stats_unchecked()
 

@@ -16,7 +16,7 @@ import torch
 
 from . import _lib as L
 from .dynamic_quantization import F16_OVERFLOW_MSG, DynamicPrecisionQuantizer
-from .engine import (EarlyStatsBuffer, LayerBuffers, OutMailbox, Workspace, check_flags, compress_layer_begin,
+from .engine import (EarlyStatsBuffer, LayerBuffers, Workspace, check_flags, compress_layer_begin,
                      params_from_config, prompt_length)
 from .selective_propagation import SelectiveTokenPropagator
 from .token_importance import LayerWiseImportanceTracker
@@ -99,18 +99,12 @@ class RealTimePrefillCompressor:
         # next call on that device or by get_overall_compression_stats, without a stream sync
         self._unverified: Dict[torch.device, tuple] = {}
         self._test_flags = 0  # RTKV_TEST_* bits OR-ed into every layer's flags (tests only)
-        # bytes of kept K/V rows read into the Infinity Cache between K2 and K4 (rtkv_prefetch_kept_rows),
-        # in the window where the host allocates the outputs.  Drop-in step at cfg3 fp32 by size (one box,
-        # profiles/r04k_dropin_prefetch_sweep.json): 0 MB 7.59 ms, 24 MB 7.56, 40 MB 7.49, 64 MB 7.59
-        # (past ~40 MB the read outlasts the host's reaction and delays K4).  RTKV_DROPIN_PREFETCH_MB
-        # overrides (0: off).
-        self.prefetch_bytes = int(float(os.environ.get("RTKV_DROPIN_PREFETCH_MB", "40")) * (1 << 20))
-        # armed K4 (rtkv_compress_layer_arm): K4 is enqueued right after K2 behind a waiter kernel and the host
-        # only posts the output addresses once it has allocated them (no launch between K2's publication
-        # and K4).  Strict mode only (the call must see K4's final flags before it returns: a waiter that
-        # gave up means K4 is launched again).  RTKV_DROPIN_ARMED=0: the two-call begin / finish path.
-        self.armed = os.environ.get("RTKV_DROPIN_ARMED", "1") != "0"
-        self._mailboxes: Dict[torch.device, OutMailbox] = {}
+        # bytes of kept K/V rows read into the Infinity Cache between K2 and K4 (rtkv_prefetch_kept_rows), in the
+        # window where the host allocates the outputs.  Re-swept on the split-row K4 (round 5, cfg3 fp32, two
+        # interleaved rounds on one box, profiles/r05_dropin_ab.json; raw driver per prefill 6.99-7.02 ms):
+        # 0 MB 7.22 / 7.22 ms, 24 MB 7.18 / 7.19, 40 MB 7.22 / 7.22, 64 MB 7.32 / 7.34 (past ~40 MB the read
+        # outlasts the host's reaction and delays K4).  RTKV_DROPIN_PREFETCH_MB overrides (0: off).
+        self.prefetch_bytes = int(float(os.environ.get("RTKV_DROPIN_PREFETCH_MB", "24")) * (1 << 20))
         self._packable: Dict[tuple, bool] = {}  # (dtype, bits, emit_packed) → whether the codes are emitted
         self.strict = (os.environ.get("RTKV_STRICT", "1") != "0") if strict is None else bool(strict)
 
@@ -186,13 +180,7 @@ class RealTimePrefillCompressor:
         # thresholds; the exactly-sized outputs are allocated then and K4 is enqueued into them
         prev, done = None, False
         try:
-            if self.armed and self.strict and res._early is not None:
-                # K4 queued now behind its waiter (which reads the first kept rows meanwhile); finish() posts
-                mb = self._mailboxes.get(K.device)
-                if mb is None:
-                    mb = self._mailboxes[K.device] = OutMailbox()
-                res.arm(mb, self.prefetch_bytes)
-            elif self.prefetch_bytes > 0 and res._early is not None:
+            if self.prefetch_bytes > 0 and res._early is not None:
                 # the first kept rows into the Infinity Cache while the host waits and allocates (after K2)
                 L.check(L.lib().rtkv_prefetch_kept_rows(res._finish_args[0], res._finish_args[2], self.prefetch_bytes,
                                                         res._stream), "rtkv_prefetch_kept_rows")
@@ -206,8 +194,6 @@ class RealTimePrefillCompressor:
             res.finish()  # between the publication and this launch the device only runs K2's tail
             done = True
         finally:
-            if not done:
-                res.cancel_armed()  # an armed K4 writes nothing (and ends) when its outputs are not posted
             if ws.pending is res:  # an error before finish(): the workspace is free again
                 ws.pending = None
             if prev is not None and not done:  # still to be checked (next call / overall stats)
@@ -217,10 +203,7 @@ class RealTimePrefillCompressor:
         st = res.stats()
         if res._early is not None:
             if self.strict:  # K2's end (K4's first wave publishes the final flags): raise in this call
-                fl = res.wait_final_flags()
-                if fl & L.FLAG_ARM_TIMEOUT:  # the armed K4's waiter gave up before the post: K4 again, launched
-                    fl = res.relaunch().wait_final_flags()
-                check_flags(fl, f"compress_layer_kv_cache (layer {layer_idx})")
+                check_flags(res.wait_final_flags(), f"compress_layer_kv_cache (layer {layer_idx})")
             else:
                 self._unverified[K.device] = (res, layer_idx)
         selected_keys, selected_values = res.kv()

@@ -365,106 +365,3 @@ def test_prefetch_and_start_event_leave_the_outputs_unchanged():
     end.record()
     end.synchronize()
     assert ev.elapsed_time(end) > 0 and 0 < res.device_seconds() < ev.elapsed_time(end) / 1e3 + 1e-5
-
-
-ARMED_CASES = [  # dtype, S, H, D, ratio, flags extra (None: default), bits
-    ("float32", 16384, 32, 128, 0.6, None, (2, 4, 8)),
-    ("float16", 8192, 16, 128, 0.4, None, (2, 4, 8)),
-    ("bfloat16", 3001, 4, 64, 0.8, None, (4, 8, 16)),
-    ("float16", 2000, 4, 32, 0.0001, None, (2, 4, 8)),    # the top-10% fallback: incomplete publication
-    ("float32", 4096, 32, 128, 1.0, "quant", (2, 4, 8)),  # quantization only
-]
-
-
-@pytest.mark.parametrize("dtype,S,H,D,ratio,extra,bits", ARMED_CASES)
-def test_armed_k4_equals_the_two_call_path(dtype, S, H, D, ratio, extra, bits):
-    """The drop-in's armed K4 (rtkv_compress_layer_arm: K4 queued behind a waiter kernel, outputs posted
-    through the pinned mailbox) against the begin / finish path: K'/V', packed codes, scale/zero-points
-    and statistics byte for byte, over consecutive layers (the mailbox is reused), including the fallback
-    layer whose publication is incomplete (the armed K4 is cancelled and K4 launched after a sync)."""
-    import rtkv
-    from rtkv import _lib as L
-    F, P = H * D, rtkv.prompt_length(S)
-    cfg = rtkv.CompressionConfig(alpha=0.8, beta=0.1, gamma=0.1, theta_h=0.4, theta_m=0.25, num_hidden_layers=3,
-                                 low_precision_bits=bits[0], medium_precision_bits=bits[1], high_precision_bits=bits[2],
-                                 early_layer_ratio=ratio, middle_layer_ratio=ratio, later_layer_ratio=ratio)
-    ins = []
-    for l in range(3):
-        K, V = synth.kv(40 + S + l, 1, S, F, dtype)
-        W = synth.attention_slice(40 + S + l, 1, H, S, P, dtype)
-        ins.append((_dev(K, dtype), _dev(V, dtype), _dev(W, dtype)))
-    ids = torch.zeros(1, S, dtype=torch.long, device="cuda")
-    outs = []
-    for armed in (True, False):
-        comp = rtkv.RealTimePrefillCompressor(cfg)
-        comp.armed = armed
-        if extra == "quant":
-            comp._test_flags = L.NO_SELECTION
-        got = [comp.compress_layer_kv_cache(K, V, W, ids, l) for l, (K, V, W) in enumerate(ins)]
-        torch.cuda.synchronize()
-        outs.append(got)
-    iv = torch.int32 if dtype == "float32" else torch.int16
-    for (ka, va, ia), (kb, vb, ib) in zip(*outs):
-        assert ka.shape == kb.shape and torch.equal(ka.view(iv), kb.view(iv)) and torch.equal(va.view(iv), vb.view(iv))
-        for key in ("codes_k", "codes_v", "scale_zp", "row_offset", "kept_index"):
-            assert torch.equal(ia["packed"][key], ib["packed"][key]), key
-        assert ia["precision_stats"] == ib["precision_stats"]
-        assert ia["compression_ratio"] == ib["compression_ratio"]
-        assert ia["processing_time"] > 0
-
-
-def test_armed_k4_cancel_and_waiter_timeout():
-    """An armed K4 whose outputs are never posted: cancelled by the host it writes and publishes
-    nothing; left alone, its waiter gives up after its bound (rtkv_set_arm_wait_us), K4 writes nothing
-    and publishes RTKV_FLAG_ARM_TIMEOUT (not a layer error).  Neither hangs the stream."""
-    import rtkv
-    from rtkv import _lib as L
-    from rtkv.engine import EarlyStatsBuffer, OutMailbox, compress_layer_begin
-    S, F, P, cfg, Kd, Vd, Wd = _lookback_inputs()
-    p = rtkv.params_from_config(cfg, 0, P, 0.6, L.EMIT_DEQUANT | L.EMIT_PACKED)
-    ws, early, mb = rtkv.Workspace("cuda"), EarlyStatsBuffer(), OutMailbox()
-    for mode in ("cancel", "timeout"):
-        bufs = rtkv.LayerBuffers(1, S, F, Kd.dtype, "cuda", (2, 4, 8), outputs=False)
-        bufs.scale_zp.fill_(7.0)
-        if mode == "timeout":
-            L.lib().rtkv_set_arm_wait_us(2000)
-        try:
-            res = compress_layer_begin(Kd, Vd, Wd, p, bufs, ws, early).arm(mb, 0)
-        finally:
-            L.lib().rtkv_set_arm_wait_us(0)
-        st = res.stats()
-        assert st.error_flags == 0 and st.max_kept > 0
-        if mode == "cancel":
-            res.cancel_armed()
-        torch.cuda.synchronize()  # the waiter ends (cancel, or its bound) and K4 with it
-        ws.pending = None
-        assert torch.all(bufs.scale_zp == 7.0)  # K4 wrote nothing
-        if mode == "cancel":
-            assert res.final_flags() is None  # nothing published (finish never ran)
-            assert res._early.final_flags(res._seq) is None
-        else:
-            assert early.final_flags(res._seq) == L.FLAG_ARM_TIMEOUT
-            res.cancel_armed()  # (no effect on a finished waiter)
-
-
-def test_drop_in_relaunches_k4_when_the_waiter_gives_up():
-    """A host slower than the waiter's bound (here a 1 us bound): every layer's armed K4 writes nothing,
-    the call sees RTKV_FLAG_ARM_TIMEOUT in the final flags and launches K4 itself — the outputs equal the
-    two-call path's, byte for byte."""
-    import rtkv
-    from rtkv import _lib as L
-    S, F, P, cfg, Kd, Vd, Wd = _lookback_inputs()
-    ids = torch.zeros(1, S, dtype=torch.long, device="cuda")
-    ref = rtkv.RealTimePrefillCompressor(cfg)
-    ref.armed = False
-    want = [ref.compress_layer_kv_cache(Kd, Vd, Wd, ids, l)[:2] for l in range(3)]
-    comp = rtkv.RealTimePrefillCompressor(cfg)
-    L.lib().rtkv_set_arm_wait_us(1)
-    try:
-        got = [comp.compress_layer_kv_cache(Kd, Vd, Wd, ids, l)[:2] for l in range(3)]
-    finally:
-        L.lib().rtkv_set_arm_wait_us(0)
-    torch.cuda.synchronize()
-    for (k, v), (rk, rv) in zip(got, want):
-        assert torch.equal(k.view(torch.int16), rk.view(torch.int16)) and torch.equal(v.view(torch.int16), rv.view(torch.int16))
-    assert sorted(comp.layer_states) == [0, 1, 2]
