@@ -354,6 +354,156 @@ __global__ __launch_bounds__(256, QK_HEAD_WPE) void qk_head_kernel(QKArgs g, flo
   }
 }
 
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+template <int DT> struct Frag32;
+template <> struct Frag32<RTKV_F16> {
+  using T = f16x8;
+  __device__ __forceinline__ static f32x16 mfma(T a, T b, f32x16 c) {
+    return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
+  }
+};
+template <> struct Frag32<RTKV_BF16> {
+  using T = bf16x8;
+  __device__ __forceinline__ static f32x16 mfma(T a, T b, f32x16 c) {
+    return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+  }
+};
+
+// Transposed head-major K1' on v_mfma_f32_32x32x16 (D = 128, P <= 128).  The head's prompt keys are
+// the A operand (32 prompt columns per MFMA row block, from LDS) and a wave's 32-row query tile the B
+// operand (straight from HBM into registers), so the accumulator holds ONE query row per lane (column
+// lane & 31) and 16 prompt columns in its registers: the row's LSE is one value per lane, the P-sum is
+// in-lane plus one add across the two lane halves (the 16x16x32 kernel above: 4 rows x 4 shuffle
+// steps per 16 rows), and every key fragment read from LDS serves 32 query rows instead of 16.
+// k order: k-step s takes the 16-byte chunk 2s + h of the row in lane half h, for A and B alike (the
+// dot product is the same sum), so a query load instruction reads 32 contiguous bytes of each of 32 rows.
+// Two waves per SIMD (256 VGPRs): the wave keeps QK32_AHEAD query tiles in flight beyond the one it
+// computes, in registers (the loop is unrolled over the tile buffers, no register copies).
+// KB: a key bias (padding), kept in LDS as kb[p]·scale·log2(e), added to the row's −lse·log2(e).
+#ifndef QK32_WPE
+#define QK32_WPE 2
+#endif
+template <int DT, bool KB, int NTILE, int NB>
+__global__ __launch_bounds__(256, QK32_WPE) void qk_head32_kernel(QKArgs g, float* __restrict__ part) {
+  using FT = typename Frag32<DT>::T;
+  using S_ = typename Dt<DT>::S;
+  constexpr int RB = 256, CH = 16, PT = 128, NT = 4, KS = 8;  // NB query tile buffers (NB - 1 ahead)
+  constexpr int KEY_BYTES = PT * RB;
+  constexpr int RPI = 1024 / RB;
+  constexpr int KI = KEY_BYTES / 1024 / 4;
+  extern __shared__ __attribute__((aligned(1024))) uint8_t lds[];  // keys, then (KB) PT key-bias terms
+  float* kbl = reinterpret_cast<float*>(lds + KEY_BYTES);
+  const rtkv_qk_desc& q = g.q;
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int r32 = lane & 31, hh = lane >> 5;
+  const int h = blockIdx.y, b = blockIdx.z;
+  const int S = (int)q.S, grp = (int)(q.H / q.Hkv), P = g.P;
+  stamp_begin(g.ex.t_begin);
+  const int wrow = (blockIdx.x * 4 + wave) * (32 * NTILE);  // this wave's first row
+  const float l2e = 1.4426950408889634f;
+  const float sc = q.scale * l2e;
+  const S_* Qh = static_cast<const S_*>(q.q_dev) + b * q.q_stride_b + (int64_t)h * q.q_stride_h;
+  const float* Lh = q.lse_dev + b * q.lse_stride_b + (int64_t)h * q.lse_stride_h;
+  float* Ph = part + ((int64_t)b * q.H + h) * S;
+  // the head's prompt keys: loaded into registers here, written to LDS below (chunk c of row r at
+  // c ^ (r & 15), as qk_head_kernel's LDS-DMA).  Not by LDS-DMA: the compiler then makes the first LDS
+  // read wait for every vector load in flight (vmcnt(0)), i.e. for all the query tiles issued ahead.
+  FT kreg[KI];
+  {
+    const S_* kh = static_cast<const S_*>(q.k_dev) + b * q.k_stride_b + (int64_t)(h / grp) * q.k_stride_h;
+    const int lrow = lane / CH, lpc = lane % CH;
+#pragma unroll
+    for (int k = 0; k < KI; ++k) {
+      const int r = (wave * KI + k) * RPI + lrow;
+      const int c = lpc ^ (r & (CH - 1));
+      const int pr = r < P ? r : P - 1;
+      kreg[k] = *reinterpret_cast<const FT*>(kh + (int64_t)pr * q.k_stride_s + c * 8);
+    }
+  }
+  if constexpr (KB) {
+    if (threadIdx.x < PT)
+      kbl[threadIdx.x] = (int)threadIdx.x < P ? key_bias_raw(q, b, threadIdx.x, 1.f / q.scale) * sc : 0.f;
+  }
+  FT qb[NB][KS];
+  float ql[NB];
+  auto load_tile = [&](int k, FT (&a)[KS], float& l) {  // tile k of this wave (rows clamped to S - 1)
+    const int qr = wrow + 32 * k + r32 < S ? wrow + 32 * k + r32 : S - 1;
+    const S_* qp = Qh + (int64_t)qr * q.q_stride_s + 8 * hh;
+#pragma unroll
+    for (int s_ = 0; s_ < KS; ++s_) a[s_] = *reinterpret_cast<const FT*>(qp + 16 * s_);
+    l = Lh[qr];
+  };
+#pragma unroll
+  for (int k = 0; k < NB && k < NTILE; ++k) load_tile(k, qb[k], ql[k]);
+#pragma unroll
+  for (int k = 0; k < KI; ++k) *reinterpret_cast<FT*>(lds + (wave * KI + k) * 1024 + lane * 16) = kreg[k];
+  // every wave's key pieces (and key-bias terms) in LDS: a raw barrier after the LDS writes, since
+  // __syncthreads would also wait for the query tiles in flight
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+  // fully unrolled over the wave's NTILE tiles: the buffer of tile k is k % NB at compile time, and the
+  // compiler's wait counts stay exact (a runtime loop over the buffers merged into vmcnt(0))
+#pragma unroll
+  for (int k = 0; k < NTILE; ++k) {
+    const FT (&cur)[KS] = qb[k % NB];
+    const int r0 = wrow + 32 * k;
+    const int i = r0 + r32;
+    const float nl2 = -ql[k % NB] * l2e;
+    // columns this lane's row may see: p < P, p <= row0 + i when causal, none past S
+    const int lim = i >= S ? 0 : (q.causal && q.row0 + i + 1 < P ? (int)(q.row0 + i + 1) : P);
+    const bool masked = (q.causal && q.row0 + r0 < PT - 1) || r0 + 32 > S || P < PT;
+    uint32_t kofs = 0;  // opaque zero offset: the LDS reads stay here (and ds_read, not flat)
+    asm volatile("" : "+v"(kofs));
+    const uint8_t* kt = lds + kofs;
+    float hs = 0.f;
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      // a compiler fence per column block: its 8 key fragments (32 VGPRs) are read from LDS just
+      // before its MFMAs, not all 32 hoisted together
+      asm volatile("" ::: "memory");
+      f32x16 acc;
+#pragma unroll
+      for (int j = 0; j < 16; ++j) acc[j] = 0.f;
+      const int kr = 32 * t + r32;
+      const uint8_t* krow = kt + kr * RB;
+#pragma unroll
+      for (int s_ = 0; s_ < KS; ++s_) {
+        const FT af = *reinterpret_cast<const FT*>(krow + (((2 * s_ + hh) ^ (kr & (CH - 1))) * 16));
+        acc = Frag32<DT>::mfma(af, cur[s_], acc);
+      }
+      // acc[j]: prompt column p = 32t + (j & 3) + 8 (j >> 2) + 4 hh of query row i
+      float off[16];
+#pragma unroll
+      for (int j = 0; j < 16; ++j) off[j] = nl2;
+      if constexpr (KB) {
+#pragma unroll
+        for (int gq = 0; gq < 4; ++gq) {
+          const f32x4 kb4 = *reinterpret_cast<const f32x4*>(kt + 4 * (32 * t + 8 * gq + 4 * hh) + KEY_BYTES);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) off[4 * gq + e] = nl2 + kb4[e];
+        }
+      }
+      if (!masked) {
+#pragma unroll
+        for (int j = 0; j < 16; ++j) hs += __builtin_amdgcn_exp2f(__builtin_fmaf(acc[j], sc, off[j]));
+      } else {
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+          const int p = 32 * t + (j & 3) + 8 * (j >> 2) + 4 * hh;
+          const float w = __builtin_amdgcn_exp2f(__builtin_fmaf(acc[j], sc, off[j]));
+          hs += p < lim ? w : 0.f;
+        }
+      }
+    }
+    if (k + NB < NTILE) load_tile(k + NB, qb[k % NB], ql[k % NB]);  // (compile-time condition)
+    hs += __shfl_xor(hs, 32, 64);
+    // a row that sees no key (lse = -inf, padding): the reference's all-masked row is uniform over S
+    if (nl2 == INFINITY) hs = (float)P / (float)S;
+    if (hh == 0 && i < S) Ph[i] = hs;
+  }
+}
+
 // A[b,i] = (Σ_h part[b,h,i]) / H in head order, plus K1's epilogue (β·pos, block min/max, zeroing).
 __global__ __launch_bounds__(256) void qk_head_reduce_kernel(const float* __restrict__ part, int64_t H, int64_t S,
                                                              float* __restrict__ A, AggExtras ex) {
@@ -435,6 +585,37 @@ static int launch_qk_head(const QKArgs& a, float* part, hipStream_t st, int* npa
   return launch_qk_head_reduce(r, part, st, nparts);
 }
 
+template <int DT, int NTILE>
+static void launch_qk_head32_n(const QKArgs& a, float* part, hipStream_t st, dim3 grid, size_t lds) {
+  // 3 tile buffers (2 tiles ahead): 4 buffers measured 43.6 against 42.6 us per cfg3 f16 layer
+  // (profiles/r05_qk32_ab.json)
+  if (a.q.kbias_dev) hipLaunchKernelGGL((qk_head32_kernel<DT, true, NTILE, 3>), grid, dim3(256), lds, st, a, part);
+  else hipLaunchKernelGGL((qk_head32_kernel<DT, false, NTILE, 3>), grid, dim3(256), lds, st, a, part);
+}
+
+template <int DT>
+static int launch_qk_head32(const QKArgs& a, float* part, hipStream_t st, int* nparts) {
+  const size_t lds = (size_t)128 * 256 + (a.q.kbias_dev ? 128 * sizeof(float) : 0);
+  const int64_t S = a.q.S;
+  // 32-row tiles per wave (8, 4, 2 or 1): the most that still gives about RTKV_QK32_WGS workgroups
+  // (default 512: two per CU, the occupancy the 2-wave register budget allows)
+  static const int target = [] {
+    const char* e = getenv("RTKV_QK32_WGS");
+    return e ? atoi(e) : 512;
+  }();
+  int nt = 8;
+  while (nt > 1 && (S + 128 * nt - 1) / (128 * nt) * a.q.H * a.q.B < target) nt /= 2;
+  const dim3 grid((unsigned)((S + 128 * nt - 1) / (128 * nt)), (unsigned)a.q.H, (unsigned)a.q.B);
+  if (nt == 8) launch_qk_head32_n<DT, 8>(a, part, st, grid, lds);
+  else if (nt == 4) launch_qk_head32_n<DT, 4>(a, part, st, grid, lds);
+  else if (nt == 2) launch_qk_head32_n<DT, 2>(a, part, st, grid, lds);
+  else launch_qk_head32_n<DT, 1>(a, part, st, grid, lds);
+  RTKV_HIP_CHECK(hipGetLastError());
+  QKArgs r = a;
+  r.ex.t_begin = nullptr;  // the layer started with the head kernel
+  return launch_qk_head_reduce(r, part, st, nparts);
+}
+
 template <int DT, int NT, int KS>
 static int launch_qk_tpl(const QKArgs& a, dim3 grid, hipStream_t st) {
   constexpr size_t lds = (size_t)kQKStages * ((size_t)(16 * NT) * (64 * KS) + (size_t)kQKRows * (64 * KS) + kQKRows * 4);
@@ -505,6 +686,13 @@ int launch_qk_importance(const rtkv_qk_desc& q, int P, float* A, hipStream_t st,
     RTKV_REQUIRE(head_ok && q.S % 4 == 0, "importance_qk_lse: a key bias needs head_dim 128, S % 4 == 0 and the "
                                           "head-major scratch");
   if (head_ok && q.S % 4 == 0 && ((!ring && P > 64) || q.kbias_dev)) {
+    // the 32x32x16 transposed kernel: 42.6 against 47.6 us per cfg3 f16 layer for the 16x16x32 one
+    // (head + reduce, profiles/r05_qk32_ab.json); RTKV_QK16 keeps the latter as a cross-check
+    static const bool k16 = getenv("RTKV_QK16") != nullptr;
+    if (!k16) {
+      if (q.dtype == RTKV_F16) return launch_qk_head32<RTKV_F16>(a, scratch, st, nparts);
+      return launch_qk_head32<RTKV_BF16>(a, scratch, st, nparts);
+    }
     if (q.dtype == RTKV_F16) return launch_qk_head<RTKV_F16, 8, 4>(a, scratch, st, nparts);
     return launch_qk_head<RTKV_BF16, 8, 4>(a, scratch, st, nparts);
   }

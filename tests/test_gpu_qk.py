@@ -58,6 +58,9 @@ def _reference_softmax(Q, K, Hkv, causal, scale):
     (torch.bfloat16, 1, 16, 4, 1000, 128, True),     # grouped-query heads
     (torch.float16, 1, 4, 4, 300, 64, False),        # P = 60 (partial MFMA tile), no mask
     (torch.bfloat16, 1, 40, 40, 2048, 128, True),    # Llama-2-13B heads
+    (torch.float16, 1, 8, 8, 400, 128, True),        # head-major kernel with P = 80 (< 128 columns)
+    (torch.float16, 1, 8, 8, 4000, 128, False),      # one 32-row tile per wave, rows past S in the last tile
+    (torch.bfloat16, 1, 32, 8, 16384, 128, True),    # cfg3 shape: 8 tiles per wave, 2 ahead in flight
 ])
 def test_fused_importance_matches_fp32_softmax(dtype, B, H, Hkv, S, D, causal):
     import rtkv
