@@ -888,6 +888,16 @@ int launch_quant_dt(const QuantArgs& a, hipStream_t st) {
   }();
   const int64_t split_maxs = split_env >= 0 ? split_env
                                : (DT == RTKV_F32 ? (a.out.k_out_dev ? INT64_MAX : (int64_t)8192) : (int64_t)4096);
+  // 2-byte dtypes with the dequantized outputs: a row over 2 waves (4 KB each) at every S — fp16 cfg3
+  // K4 87.2 -> 82.5 us, S = 4096 29.0 -> 26.8 (against 4 waves), S = 65536 332 -> 317; bf16 cfg3 150.7
+  // -> 142.0 (profiles/r05_k4_split2_ab.json).  fp32 (153.3 vs 154.6 us at cfg3, 43.9 vs 45.4 at
+  // S = 4096) and fp16 packed-only (59.2 vs 59.9) keep theirs.  (F = 4096 rows: the measured shape.)
+  if (DT != RTKV_F32 && a.out.k_out_dev && split_env < 0 && contig && kv.B == 1 && a.S_glob == 0 && a.kept_index &&
+      nch == 512) {
+    hipLaunchKernelGGL((quant_rows_split_kernel<DT, 4, 2>), dim3((unsigned)tasks), dim3(128), 0, st, a);
+    RTKV_HIP_CHECK(hipGetLastError());
+    return RTKV_OK;
+  }
   if (contig && kv.B == 1 && a.S_glob == 0 && a.kept_index && Sg <= split_maxs && (nch % 64) == 0) {
     const unsigned g = (unsigned)tasks;
 #define RTKV_QS(NCHT, NCHW, NSPLIT)                                                                       \

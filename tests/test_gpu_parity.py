@@ -584,8 +584,8 @@ def test_full_size_properties(S, dtype, ratio, H):
 @pytest.mark.parametrize("dtype,H", [("float32", 32), ("float16", 32), ("bfloat16", 32), ("float32", 40),
                                      ("float16", 40)])
 def test_split_row_k4_matches_oracle(dtype, H):
-    """Short single-row layers (S <= 8192, F = 4096 / 5120) take quant_rows_split_kernel: each row is
-    quantized by 4 (5) waves that combine its min/max in LDS.  Dequantized rows, codes, scale/zp and
+    """Single-row layers take quant_rows_split_kernel: each row is quantized by 4 (5) waves — 2 for the
+    2-byte dtypes with F = 4096 and dequantized outputs (every S) — that combine its min/max in LDS.  Dequantized rows, codes, scale/zp and
     row offsets equal the oracle's, including the division-gate edge rows (NaN / ±inf rows: the
     dual-vs-packed test above; their codes are platform-defined conversions)."""
     import rtkv
