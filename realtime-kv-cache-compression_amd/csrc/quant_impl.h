@@ -898,6 +898,8 @@ int launch_quant_dt(const QuantArgs& a, hipStream_t st) {
     RTKV_HIP_CHECK(hipGetLastError());
     return RTKV_OK;
   }
+  // (packed-only 2-byte rows over 2 waves, compile-time packed-only at 4 or 5 waves per SIMD: 60.3 / 60.5
+  // against 59.7 us for the whole-row kernel at cfg3 fp16, profiles/r05_k4_split2_ab.json: not used)
   if (contig && kv.B == 1 && a.S_glob == 0 && a.kept_index && Sg <= split_maxs && (nch % 64) == 0) {
     const unsigned g = (unsigned)tasks;
 #define RTKV_QS(NCHT, NCHW, NSPLIT)                                                                       \

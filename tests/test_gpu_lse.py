@@ -1,8 +1,9 @@
 """GPU: the attention row log-sum-exp (rtkv_attention_lse, csrc/attn_lse.hip) against a torch fp32
 logsumexp of the masked scores, and the fused importance mode fed by it.
 
-The kernel multiplies fp16/bf16 Q·K on MFMA with fp32 accumulation and sums exp2 in fp32, so the
-tolerance is |Δlse| ≤ 2e-4 + 1e-5·|lse| (summation order and the hardware exp2/log2).  Cases: causal
+The kernel multiplies fp16/bf16 Q·K on MFMA with fp32 accumulation (fp32 Q·K: three bf16 parts per
+operand, six part products — fp32-accurate) and sums exp2 in fp32, so the tolerance is
+|Δlse| ≤ 2e-4 + 1e-5·|lse| (summation order and the hardware exp2/log2).  Cases: causal
 and full attention, head_dim 64 and 128, GQA (H / Hkv = 4), S not a multiple of the 64-row tiles,
 tiny S, batch 2, both layouts of K."""
 import pytest
@@ -38,6 +39,12 @@ CASES = [
     (1, 2, 2, 64, 128, torch.float16, True),
     (1, 2, 1, 5, 64, torch.float16, True),
     (1, 32, 32, 4096, 128, torch.float16, True),
+    # fp32 states: the split-bf16 kernel (three bf16 parts per operand, six products; attn_f32.hip)
+    (1, 4, 4, 1000, 128, torch.float32, True),
+    (2, 8, 2, 333, 128, torch.float32, True),
+    (1, 4, 4, 777, 128, torch.float32, False),
+    (1, 2, 2, 64, 128, torch.float32, True),
+    (1, 32, 32, 4096, 128, torch.float32, True),
 ]
 
 
