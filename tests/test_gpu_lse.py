@@ -79,10 +79,11 @@ def test_fused_importance_from_own_lse():
     torch.testing.assert_close(A, A_ref, rtol=1e-3, atol=1e-6)
 
 
-@pytest.mark.parametrize("dtype", [torch.float16, torch.bfloat16])
+@pytest.mark.parametrize("dtype", [torch.float16, torch.bfloat16, torch.float32])
 def test_overflow_rows_take_the_fixup_pass(dtype):
     """The 32x32 kernel sums against each row's first logit unchecked; a later logit ~180 log2 units
-    above it overflows the sum, and the fix-up pass must recompute those rows (attn_lse32.hip)."""
+    above it overflows the sum, and the fix-up pass must recompute those rows (attn_lse32.hip).  fp32
+    (the split-bf16 kernel) raises its reference max lazily instead: the same rows must stay finite."""
     import rtkv
     B, H, S, D = 1, 4, 1024, 128
     g = torch.Generator(device="cuda").manual_seed(9)
@@ -102,3 +103,33 @@ def test_rejects_unsupported():
     Q = torch.zeros(1, 2, 64, 96, device="cuda", dtype=torch.float16)
     with pytest.raises(RuntimeError, match="head_dim"):
         rtkv.attention_lse(Q, Q)
+
+
+_EXACT_CHILD = r"""
+import sys, torch
+sys.path.insert(0, sys.argv[2])
+import rtkv
+g = torch.Generator(device="cuda").manual_seed(17)
+B, H, Hkv, S, D = 1, 8, 2, 1500, 128
+Q = torch.randn(B, H, S, D, device="cuda", generator=g) * 1.5
+K = torch.randn(B, Hkv, S, D, device="cuda", generator=g) * 1.5
+torch.save({"lse": rtkv.attention_lse(Q, K, causal=True).cpu(), "Q": Q.cpu(), "K": K.cpu()}, sys.argv[1])
+"""
+
+
+def test_fp32_split_lse_matches_the_exact_f32_kernel(tmp_path):
+    """The split-bf16 fp32 LSE (six bf16 part products) against the exact f32-MFMA kernel
+    (RTKV_LSE_F32_EXACT, run in a child process: the knob is read once per process) on the same
+    inputs: fp32-accurate, i.e. far inside the 2e-4 tolerance against torch."""
+    import os
+    import subprocess
+    import sys
+    import rtkv
+    out = tmp_path / "exact.pt"
+    pkg = os.path.dirname(os.path.dirname(os.path.abspath(rtkv.__file__)))
+    env = dict(os.environ, RTKV_LSE_F32_EXACT="1")
+    subprocess.run([sys.executable, "-c", _EXACT_CHILD, str(out), pkg], env=env, check=True, timeout=120)
+    d = torch.load(out, weights_only=True)
+    lse = rtkv.attention_lse(d["Q"].cuda(), d["K"].cuda(), causal=True).cpu()
+    assert torch.isfinite(lse).all()
+    torch.testing.assert_close(lse, d["lse"], rtol=1e-6, atol=2e-5)
