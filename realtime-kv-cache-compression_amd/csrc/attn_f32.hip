@@ -256,20 +256,21 @@ __global__ __launch_bounds__(256) void qk_head_f32_kernel(rtkv_qk_desc q, int P,
 // parts, x = x_h + x_l + x_ll (round-to-nearest splits: every part holds the next 8 significant bits, the
 // residual is below 2^-27 |x|), and q·k is the sum of the six part products down to order 2^-18:
 // h·h, h·l, l·h, h·ll, ll·h, l·l — the dropped l·ll, ll·l, ll·ll are below 2^-27 |q||k| each, under
-// fp32's own 2^-24 rounding of a product.  Six v_mfma_f32_32x32x16_bf16 (fp32 accumulation) per
-// 32 × 32 × 16 block take 6 × 32 cycles where the exact f32 MFMA takes 8 × 4 × 32 (v_mfma_f32_16x16x4_f32
-// at 1/16 of the bf16 rate): 2.7× fewer matrix cycles for the same logits to fp32 accuracy (not bit for
+// fp32's own 2^-24 rounding of a product.  Six v_mfma_f32_16x16x32_bf16 (fp32 accumulation) per
+// 16 × 16 × 32 block take 6 × 16 cycles where the exact f32 MFMA takes 8 × 32 (v_mfma_f32_16x16x4_f32 at
+// 1/16 of the bf16 rate): 2.7× fewer matrix cycles for the same logits to fp32 accuracy (not bit for
 // bit: the f32 kernel above stays as RTKV_LSE_F32_EXACT).
 //
-// Work decomposition: a workgroup of 4 waves owns 128 query rows of one (b, h) (32 per wave, Q split
-// once into registers: 3 planes × 8 k-steps; ~300 VGPRs, so one wave per SIMD, the 32x32x16 chain
-// issuing back to back with the exp2 work in its gaps); key tiles of 64 rows are loaded by all 256 threads into
-// registers one tile ahead, split, and written to LDS as three swizzled bf16 planes (double-buffered,
-// 2 × 48 KiB, one barrier per tile).  Fragments and the k order as attn_lse32.hip (lane l: row l & 31,
-// k-step s = chunk 2s + (l >> 5)).  Softmax bookkeeping as attn_lse_f32_kernel: a checked lazy max
-// (raised by 8 log2 units at most once per tile and row), so no fix-up pass.
+// Work decomposition (attn_lse_f32x3s_kernel below): a workgroup of 16 waves owns 256 query rows of one
+// (b, h), 16 per wave (Q split once into registers: 3 planes × 4 k-steps, 48 registers, so four waves
+// per SIMD overlap one another's bookkeeping and MFMAs); key tiles of 64 rows are loaded by all 1024
+// threads into registers a full iteration ahead, split, and written to LDS as three swizzled bf16 planes
+// (double-buffered, 2 × 48 KiB, one barrier per tile), the split of tile kt + 1 issuing inside tile kt's
+// MFMA block.  Softmax bookkeeping as attn_lse_f32_kernel: a checked lazy max (raised by 8 log2 units at
+// most once per tile and row), so no fix-up pass.  Measured (S = 16384, 32 heads): 5.2 ms against 10.5
+// for the exact kernel; a 32-row tiling on 32x32x16 (96 registers of Q planes: one wave per SIMD) 6.8 ms,
+// this tiling at 8 waves per workgroup (two per SIMD) 6.3 ms.
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
-typedef float f32x16 __attribute__((ext_vector_type(16)));
 
 constexpr int kX3Keys = 64;              // key rows per tile
 constexpr int kX3Plane = kX3Keys * 256;  // one bf16 plane of a tile (16 KiB)
@@ -294,18 +295,23 @@ __device__ __forceinline__ void split8(const f32x4& x0, const f32x4& x1, bf16x8&
   }
 }
 
-__device__ __forceinline__ f32x16 mfma_bf16(bf16x8 a, bf16x8 b, f32x16 c) {
-  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
-}
-
-template <int RB>  // 32-row blocks per wave
-__global__ __launch_bounds__(256) void attn_lse_f32x3_kernel(LseF32Args g) {
+// The split-bf16 LSE on 16-row wave tiles (v_mfma_f32_16x16x32_bf16): Q's three planes take 48
+// registers, so NW = 16 waves (four per SIMD, 128 registers) share a workgroup of 256 query rows and the
+// waves' bookkeeping overlaps one another's MFMAs.  Fragments (cdna_hip_programming.md §3): lane l supplies
+// A[row l & 15][k = 8 (l >> 4) + j] and B[k = 8 (l >> 4) + j][col l & 15]; k-step s covers the 16-byte
+// chunk 4s + (l >> 4) of a row (A and B alike); the accumulator holds key column l & 15 of rows
+// 4 (l >> 4) + r.  Bookkeeping as attn_lse_f32_kernel (4 rows per lane, 16 lanes per row group).
+template <int NW>
+__global__ __launch_bounds__(64 * NW) void attn_lse_f32x3s_kernel(LseF32Args g) {
   extern __shared__ __attribute__((aligned(1024))) uint8_t lds[];  // 2 buffers × 3 planes × kX3Plane
-  constexpr int ROWS = 4 * 32 * RB;  // query rows per workgroup
+  constexpr int ROWS = 16 * NW;
+  constexpr int EPT = kX3Keys * 128 / (64 * NW);  // key elements per thread and tile
+  static_assert(EPT % 8 == 0, "whole 16-byte chunks per thread");
+  constexpr int CPT = EPT / 8;                      // chunks per thread and plane
   const rtkv_qk_desc& q = g.q;
   const int t = threadIdx.x;
   const int lane = t & 63, wave = __builtin_amdgcn_readfirstlane(t >> 6);
-  const int r32 = lane & 31, hh = lane >> 5;
+  const int c16 = lane & 15, kg = lane >> 4;
   int qb, hd, b;  // XCD-aware order, as attn_lse32.hip
   {
     const int nwg = (int)(gridDim.x * gridDim.y * gridDim.z);
@@ -317,52 +323,47 @@ __global__ __launch_bounds__(256) void attn_lse_f32x3_kernel(LseF32Args g) {
     b = unit / (int)gridDim.y;
   }
   const int S = (int)q.S, grp = (int)(q.H / q.Hkv);
-  const int i0 = qb * ROWS, wrow0 = i0 + 32 * RB * wave;  // row block rb: rows wrow0 + 32 rb ..
+  const int i0 = qb * ROWS, wrow0 = i0 + 16 * wave, crow0 = wrow0 + 4 * kg;
   const float sc = q.scale * kL2E, inv_scale = 1.f / q.scale;
   const float* Kh = static_cast<const float*>(q.k_dev) + b * q.k_stride_b + (int64_t)(hd / grp) * q.k_stride_h;
   int64_t kend = q.causal ? q.row0 + i0 + ROWS : S;
   if (kend > S) kend = S;
   const int ntiles = (int)((kend + kX3Keys - 1) / kX3Keys);
-  // this thread's share of a key tile: key row kr = t >> 2, dims 32 (t & 3) .. +31
-  const int kr = t >> 2, kd = (t & 3) * 32;
-  f32x4 kreg[8], knext[8];  // tile kt + 1 (split during tile kt's MFMAs) and tile kt + 2 (in flight)
-  auto load_tile = [&](int kt, f32x4 (&dst)[8]) {  // (rows clamped: a tile past the end is a harmless re-read)
+  // this thread's share of a key tile: key row kr, EPT consecutive dims from kd
+  constexpr int TPR = 128 / EPT;  // threads per key row
+  const int kr = t / TPR, kd = (t % TPR) * EPT;
+  f32x4 kreg[EPT / 4], knext[EPT / 4];
+  auto load_tile = [&](int kt, f32x4 (&dst)[EPT / 4]) {  // (rows clamped: a tile past the end is a harmless re-read)
     int r = kt * kX3Keys + kr;
     r = r < S ? r : S - 1;
     const float* src = Kh + (int64_t)r * q.k_stride_s + kd;
 #pragma unroll
-    for (int e = 0; e < 8; ++e) dst[e] = *reinterpret_cast<const f32x4*>(src + 4 * e);
+    for (int e = 0; e < EPT / 4; ++e) dst[e] = *reinterpret_cast<const f32x4*>(src + 4 * e);
   };
   load_tile(0, kreg);
-  // Q: this lane's row of each row block, k-step s = dims 8 (2s + hh) .. +7, split into three planes
-  bf16x8 ah[RB][8], al[RB][8], all[RB][8];
-#pragma unroll
-  for (int rb = 0; rb < RB; ++rb) {
-    const int qr = wrow0 + 32 * rb + r32 < S ? wrow0 + 32 * rb + r32 : S - 1;
+  bf16x8 ah[4], al[4], all[4];  // Q row c16 of the wave's 16, k-step s = chunk 4s + kg
+  {
+    const int qr = wrow0 + c16 < S ? wrow0 + c16 : S - 1;
     const float* qrow = static_cast<const float*>(q.q_dev) + b * q.q_stride_b + (int64_t)hd * q.q_stride_h +
                         (int64_t)qr * q.q_stride_s;
 #pragma unroll
-    for (int s_ = 0; s_ < 8; ++s_) {
-      const f32x4 x0 = *reinterpret_cast<const f32x4*>(qrow + (2 * s_ + hh) * 8);
-      const f32x4 x1 = *reinterpret_cast<const f32x4*>(qrow + (2 * s_ + hh) * 8 + 4);
-      split8(x0, x1, ah[rb][s_], al[rb][s_], all[rb][s_]);
+    for (int s_ = 0; s_ < 4; ++s_) {
+      const f32x4 x0 = *reinterpret_cast<const f32x4*>(qrow + (4 * s_ + kg) * 8);
+      const f32x4 x1 = *reinterpret_cast<const f32x4*>(qrow + (4 * s_ + kg) * 8 + 4);
+      split8(x0, x1, ah[s_], al[s_], all[s_]);
     }
   }
-  float m[RB][16], l[RB][16];
+  float m[4], l[4];
 #pragma unroll
-  for (int rb = 0; rb < RB; ++rb)
-#pragma unroll
-    for (int r = 0; r < 16; ++r) { m[rb][r] = -1e30f; l[rb][r] = 0.f; }
-  // split this thread's 32 values of a tile (kreg) into the three planes of buffer (kt & 1), chunks
-  // 4 (t & 3) + c of row kr
+  for (int r = 0; r < 4; ++r) { m[r] = -1e30f; l[r] = 0.f; }
   auto split_store = [&](int kt) {
     uint8_t* buf = lds + (kt & 1) * 3 * kX3Plane;
     const int sw = kr & 15;
 #pragma unroll
-    for (int c = 0; c < 4; ++c) {
+    for (int c = 0; c < CPT; ++c) {
       bf16x8 h, lo, ll;
       split8(kreg[2 * c], kreg[2 * c + 1], h, lo, ll);
-      const int off = kr * 256 + (((4 * (t & 3) + c) ^ sw) * 16);
+      const int off = kr * 256 + ((((kd >> 3) + c) ^ sw) * 16);
       *reinterpret_cast<bf16x8*>(buf + off) = h;
       *reinterpret_cast<bf16x8*>(buf + kX3Plane + off) = lo;
       *reinterpret_cast<bf16x8*>(buf + 2 * kX3Plane + off) = ll;
@@ -376,105 +377,83 @@ __global__ __launch_bounds__(256) void attn_lse_f32x3_kernel(LseF32Args g) {
   for (int kt = 0; kt < ntiles; ++kt) {
     load_tile(kt + 2, knext);  // a whole iteration ahead of its split
     const uint8_t* buf = lds + (kt & 1) * 3 * kX3Plane;
-    // the key bias of this tile's two column blocks (0 without one), before the MFMA block
-    float kb[2] = {0.f, 0.f};
-    if (q.kbias_dev) {
+    f32x4 acc[4];
 #pragma unroll
-      for (int cb = 0; cb < 2; ++cb) {
-        const int64_t j = (int64_t)kt * kX3Keys + 32 * cb + r32;
-        kb[cb] = j < S ? key_bias_raw(q, b, j, inv_scale) : 0.f;
-      }
-    }
-    // Software pipeline, one basic block: this tile's MFMAs (RB row blocks × 2 column blocks × 48) and
-    // the split of tile kt + 1 into the other buffer (read last in iteration kt - 1, before the previous
-    // barrier by every wave), so the conversion issues in the MFMA chains' gaps.  Every key fragment
-    // read from LDS serves the RB row blocks.  The MFMAs run for every tile, also past a block's last
-    // causal row (masked below).
-    f32x16 acc[RB][2];
-#pragma unroll
-    for (int cb = 0; cb < 2; ++cb) {
-      const int kro = 32 * cb + r32;
+    for (int tc = 0; tc < 4; ++tc) {  // 16-key column tiles
+      const int kro = 16 * tc + c16;
       const uint8_t* krow = buf + kro * 256;
       const int sw = kro & 15;
+      acc[tc] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int rb = 0; rb < RB; ++rb)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) acc[rb][cb][r] = 0.f;
-#pragma unroll
-      for (int s_ = 0; s_ < 8; ++s_) {
-        const int c = ((2 * s_ + hh) ^ sw) * 16;
+      for (int s_ = 0; s_ < 4; ++s_) {
+        const int c = ((4 * s_ + kg) ^ sw) * 16;
         const bf16x8 bh = *reinterpret_cast<const bf16x8*>(krow + c);
         const bf16x8 bl = *reinterpret_cast<const bf16x8*>(krow + kX3Plane + c);
         const bf16x8 bll = *reinterpret_cast<const bf16x8*>(krow + 2 * kX3Plane + c);
+        acc[tc] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al[s_], bl, acc[tc], 0, 0, 0);
+        acc[tc] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[s_], bll, acc[tc], 0, 0, 0);
+        acc[tc] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(all[s_], bh, acc[tc], 0, 0, 0);
+        acc[tc] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[s_], bl, acc[tc], 0, 0, 0);
+        acc[tc] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al[s_], bh, acc[tc], 0, 0, 0);
+        acc[tc] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[s_], bh, acc[tc], 0, 0, 0);
+      }
+    }
+    if constexpr (NW > 8) {  // a k-step's 3 fragment reads just ahead of its 6 MFMAs (registers)
 #pragma unroll
-        for (int rb = 0; rb < RB; ++rb) {  // the small products first, then h·h
-          acc[rb][cb] = mfma_bf16(al[rb][s_], bl, acc[rb][cb]);
-          acc[rb][cb] = mfma_bf16(ah[rb][s_], bll, acc[rb][cb]);
-          acc[rb][cb] = mfma_bf16(all[rb][s_], bh, acc[rb][cb]);
-          acc[rb][cb] = mfma_bf16(ah[rb][s_], bl, acc[rb][cb]);
-          acc[rb][cb] = mfma_bf16(al[rb][s_], bh, acc[rb][cb]);
-          acc[rb][cb] = mfma_bf16(ah[rb][s_], bh, acc[rb][cb]);
-        }
+      for (int i = 0; i < 16; ++i) {
+        __builtin_amdgcn_sched_group_barrier(0x100, 3, 0);
+        __builtin_amdgcn_sched_group_barrier(0x008, 6, 0);
       }
     }
     split_store(kt + 1);
+    const bool edge = (int64_t)(kt + 1) * kX3Keys > (q.causal ? q.row0 + wrow0 : (int64_t)S) || (kt + 1) * kX3Keys > S;
 #pragma unroll
-    for (int rb = 0; rb < RB; ++rb) {
-      f32x16& a0 = acc[rb][0];
-      f32x16& a1 = acc[rb][1];
+    for (int tc = 0; tc < 4; ++tc) {
+      const int64_t j = (int64_t)kt * kX3Keys + 16 * tc + c16;
+      const float kb = (q.kbias_dev && j < S) ? kb_raw(q, b, j, inv_scale) : 0.f;
 #pragma unroll
-      for (int r = 0; r < 16; ++r) { a0[r] += kb[0]; a1[r] += kb[1]; }
-      const int64_t brow0 = q.row0 + wrow0 + 32 * rb;  // first row of the block
-      const bool edge = (int64_t)(kt + 1) * kX3Keys > (q.causal ? brow0 : (int64_t)S) || (kt + 1) * kX3Keys > S;
-      if (edge) {
-        const int64_t j0 = (int64_t)kt * kX3Keys + r32, j1 = j0 + 32;
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int64_t row = brow0 + (r & 3) + 8 * (r >> 2) + 4 * hh;
-          a0[r] = (j0 < S && (!q.causal || j0 <= row)) ? a0[r] : -INFINITY;
-          a1[r] = (j1 < S && (!q.causal || j1 <= row)) ? a1[r] : -INFINITY;
-        }
-      }
-      bool up = false;
-#pragma unroll
-      for (int r = 0; r < 16; ++r) up |= fmaxf(a0[r], a1[r]) * sc > m[rb][r] + 8.f;
-      if (__ballot(up)) {
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const float mt = fmaxf(a0[r], a1[r]) * sc;
-          const float mn = mt > m[rb][r] + 8.f ? mt : m[rb][r];
-          l[rb][r] *= __builtin_amdgcn_exp2f(m[rb][r] - mn);
-          m[rb][r] = mn;
-        }
-      }
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const float nm = -m[rb][r];
-        l[rb][r] += __builtin_amdgcn_exp2f(__builtin_fmaf(a0[r], sc, nm)) + __builtin_amdgcn_exp2f(__builtin_fmaf(a1[r], sc, nm));
+      for (int r = 0; r < 4; ++r) {
+        const bool ok = !edge || (j < S && (!q.causal || j <= q.row0 + crow0 + r));
+        acc[tc][r] = ok ? acc[tc][r] + kb : -INFINITY;
       }
     }
-    // the planes of tile kt + 1 written by every thread
+    bool up = false;
+    float mt[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      mt[r] = fmaxf(fmaxf(acc[0][r], acc[1][r]), fmaxf(acc[2][r], acc[3][r])) * sc;
+      up |= mt[r] > m[r] + 8.f;
+    }
+    if (__ballot(up)) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float mn = mt[r] > m[r] + 8.f ? mt[r] : m[r];
+        l[r] *= __builtin_amdgcn_exp2f(m[r] - mn);
+        m[r] = mn;
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+      for (int tc = 0; tc < 4; ++tc) l[r] += __builtin_amdgcn_exp2f(__builtin_fmaf(acc[tc][r], sc, -m[r]));
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
 #pragma unroll
-    for (int e = 0; e < 8; ++e) kreg[e] = knext[e];
+    for (int e = 0; e < EPT / 4; ++e) kreg[e] = knext[e];
   }
-  // the 32 lanes of each row: M = max m, L = Σ l·2^(m − M); lse = (M + log2 L)·ln 2, -inf for no key
 #pragma unroll
-  for (int rb = 0; rb < RB; ++rb)
+  for (int r = 0; r < 4; ++r) {
+    float M = m[r];
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      float M = m[rb][r];
+    for (int o = 1; o < 16; o <<= 1) M = fmaxf(M, __shfl_xor(M, o, 64));
+    float L = l[r] * __builtin_amdgcn_exp2f(m[r] - M);
 #pragma unroll
-      for (int o = 1; o < 32; o <<= 1) M = fmaxf(M, __shfl_xor(M, o, 64));
-      float L = l[rb][r] * __builtin_amdgcn_exp2f(m[rb][r] - M);
-#pragma unroll
-      for (int o = 1; o < 32; o <<= 1) L += __shfl_xor(L, o, 64);
-      const int i = wrow0 + 32 * rb + (r & 3) + 8 * (r >> 2) + 4 * hh;
-      if (r32 == 0 && i < S)
-        g.lse[b * q.lse_stride_b + (int64_t)hd * q.lse_stride_h + i] = L > 0.f ? (M + __log2f(L)) * 0.6931471805599453f : -INFINITY;
-    }
+    for (int o = 1; o < 16; o <<= 1) L += __shfl_xor(L, o, 64);
+    const int i = crow0 + r;
+    if (c16 == 0 && i < S)
+      g.lse[b * q.lse_stride_b + (int64_t)hd * q.lse_stride_h + i] = L > 0.f ? (M + __log2f(L)) * 0.6931471805599453f : -INFINITY;
+  }
 }
 
 }  // namespace
@@ -490,19 +469,18 @@ int launch_attention_lse_f32(const rtkv_qk_desc& q, float* lse, hipStream_t st) 
   static const bool exact = getenv("RTKV_LSE_F32_EXACT") != nullptr;
   if (!exact) {
     constexpr size_t lds3 = 6 * (size_t)kX3Plane;
-    // one 32-row block per wave (two, sharing each key fragment, need ~640 registers: spilled)
     static bool attr3 = false;
     if (!attr3) {
-      RTKV_HIP_CHECK(hipFuncSetAttribute((const void*)attn_lse_f32x3_kernel<1>,
+      RTKV_HIP_CHECK(hipFuncSetAttribute((const void*)attn_lse_f32x3s_kernel<16>,
                                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds3));
       attr3 = true;
     }
     LseF32Args a;
     a.q = q;
     a.lse = lse;
-    a.nblk = (int)((q.S + 127) / 128);
-    hipLaunchKernelGGL(attn_lse_f32x3_kernel<1>, dim3((unsigned)a.nblk, (unsigned)q.H, (unsigned)q.B), dim3(256), lds3,
-                       st, a);
+    a.nblk = (int)((q.S + 255) / 256);
+    hipLaunchKernelGGL(attn_lse_f32x3s_kernel<16>, dim3((unsigned)a.nblk, (unsigned)q.H, (unsigned)q.B), dim3(1024),
+                       lds3, st, a);
     RTKV_HIP_CHECK(hipGetLastError());
     return RTKV_OK;
   }
