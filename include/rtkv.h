@@ -131,7 +131,7 @@ typedef struct rtkv_qk_desc {
   const void* q_dev;
   const void* k_dev;
   const float* lse_dev;
-  int32_t dtype;                       /* RTKV_F16, RTKV_BF16 (16x16x32 MFMA) or RTKV_F32 (16x16x4 f32 MFMA) */
+  int32_t dtype;                       /* RTKV_F16, RTKV_BF16 (bf16/f16 MFMA) or RTKV_F32 (three-way bf16 split; exact f32 MFMA with RTKV_LSE_F32_EXACT) */
   int32_t causal;
   int64_t B, H, Hkv, S, D;
   int64_t q_stride_b, q_stride_h, q_stride_s;
