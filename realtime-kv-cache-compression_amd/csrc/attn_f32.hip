@@ -456,6 +456,120 @@ __global__ __launch_bounds__(64 * NW) void attn_lse_f32x3s_kernel(LseF32Args g) 
   }
 }
 
+// Head-major K1' for fp32 states on the bf16 matrix cores, with the LSE kernel's three-way split: the
+// head's P ≤ 128 prompt keys are split once per workgroup into three bf16 planes in LDS (96 KiB); 16 waves
+// (1024 threads, four per SIMD at 128 registers) each walk their rows in 16-row tiles, the tile's queries
+// split into registers (48), 8 column tiles × 4 k-steps × 6 part products on v_mfma_f32_16x16x32_bf16,
+// then exp2(x·scale·log2e − lse·log2e) (+ key bias) summed over the prompt columns and written to
+// part[b][h][i] as qk_head_f32_kernel does (qk_head_reduce_kernel sums the heads).
+template <int NW>
+__global__ __launch_bounds__(64 * NW) void qk_head_f32x3_kernel(rtkv_qk_desc q, int P, float* __restrict__ part, int rpw,
+                                                               unsigned long long* t_begin) {
+  stamp_begin(t_begin);
+  extern __shared__ __attribute__((aligned(1024))) uint8_t lds[];  // 3 planes × 128 rows × 256 B
+  constexpr int PL = 128 * 256;                                     // one plane
+  const int t = threadIdx.x;
+  const int lane = t & 63, wave = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int c16 = lane & 15, kg = lane >> 4;
+  const int h = blockIdx.y, b = blockIdx.z;
+  const int S = (int)q.S, grp = (int)(q.H / q.Hkv);
+  const int wrow = (blockIdx.x * NW + wave) * rpw;
+  const float sc = q.scale * kL2E, inv_scale = 1.f / q.scale;
+  const float* Qh = static_cast<const float*>(q.q_dev) + b * q.q_stride_b + (int64_t)h * q.q_stride_h;
+  const float* Lh = q.lse_dev + b * q.lse_stride_b + (int64_t)h * q.lse_stride_h;
+  float* Ph = part + ((int64_t)b * q.H + h) * S;
+  {  // the head's prompt keys: thread t splits EPT dims of key row kr (rows past P: row P - 1)
+    constexpr int EPT = 128 * 128 / (64 * NW), TPR = 128 / EPT;
+    const float* kh = static_cast<const float*>(q.k_dev) + b * q.k_stride_b + (int64_t)(h / grp) * q.k_stride_h;
+    const int kr = t / TPR, kd = (t % TPR) * EPT;
+    const float* src = kh + (int64_t)(kr < P ? kr : P - 1) * q.k_stride_s + kd;
+    f32x4 x[EPT / 4];
+#pragma unroll
+    for (int e = 0; e < EPT / 4; ++e) x[e] = *reinterpret_cast<const f32x4*>(src + 4 * e);
+    const int sw = kr & 15;
+#pragma unroll
+    for (int c = 0; c < EPT / 8; ++c) {
+      bf16x8 hi, lo, ll;
+      split8(x[2 * c], x[2 * c + 1], hi, lo, ll);
+      const int off = kr * 256 + ((((kd >> 3) + c) ^ sw) * 16);
+      *reinterpret_cast<bf16x8*>(lds + off) = hi;
+      *reinterpret_cast<bf16x8*>(lds + PL + off) = lo;
+      *reinterpret_cast<bf16x8*>(lds + 2 * PL + off) = ll;
+    }
+  }
+  // the prompt columns' key bias (raw units), the same for every row: a 128-entry LDS table
+  float* kbl = reinterpret_cast<float*>(lds + 3 * PL);
+  if (t < 128) kbl[t] = t < P ? kb_raw(q, b, t, inv_scale) : 0.f;
+  __syncthreads();
+  const int ntile = rpw / 16;
+  for (int k = 0; k < ntile; ++k) {
+    const int r0 = wrow + 16 * k;
+    if (r0 >= S) break;
+    const int crow0 = r0 + 4 * kg;
+    bf16x8 ah[4], al[4], all[4];  // row c16 of the tile, k-step s = chunk 4s + kg
+    {
+      const int qr = r0 + c16 < S ? r0 + c16 : S - 1;
+      const float* qp = Qh + (int64_t)qr * q.q_stride_s;
+#pragma unroll
+      for (int s_ = 0; s_ < 4; ++s_) {
+        const f32x4 x0 = *reinterpret_cast<const f32x4*>(qp + (4 * s_ + kg) * 8);
+        const f32x4 x1 = *reinterpret_cast<const f32x4*>(qp + (4 * s_ + kg) * 8 + 4);
+        split8(x0, x1, ah[s_], al[s_], all[s_]);
+      }
+    }
+    float lv[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) lv[r] = crow0 + r < S ? Lh[crow0 + r] : 0.f;
+    float v[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int tc = 0; tc < 8; ++tc) {
+      if (16 * tc >= P) break;
+      const int kro = 16 * tc + c16;
+      const uint8_t* krow = lds + kro * 256;
+      const int sw = kro & 15;
+      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int s_ = 0; s_ < 4; ++s_) {
+        const int c = ((4 * s_ + kg) ^ sw) * 16;
+        const bf16x8 bh = *reinterpret_cast<const bf16x8*>(krow + c);
+        const bf16x8 bl = *reinterpret_cast<const bf16x8*>(krow + PL + c);
+        const bf16x8 bll = *reinterpret_cast<const bf16x8*>(krow + 2 * PL + c);
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al[s_], bl, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[s_], bll, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(all[s_], bh, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[s_], bl, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al[s_], bh, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[s_], bh, acc, 0, 0, 0);
+      }
+      // a k-step's 3 fragment reads just ahead of its 6 MFMAs (registers)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        __builtin_amdgcn_sched_group_barrier(0x100, 3, 0);
+        __builtin_amdgcn_sched_group_barrier(0x008, 6, 0);
+      }
+      const int p = kro;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int i = crow0 + r;
+        const bool ok = p < P && i < S && (!q.causal || (int64_t)p <= q.row0 + i);
+        const float w = __builtin_amdgcn_exp2f(__builtin_fmaf(acc[r] + kbl[kro], sc, -lv[r] * kL2E));
+        v[r] += ok ? w : 0.f;
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+#pragma unroll
+      for (int o = 1; o < 16; o <<= 1) v[r] += __shfl_xor(v[r], o, 64);
+      if (lv[r] == -INFINITY) v[r] = (float)P / (float)S;  // a row that sees no key: the uniform row
+    }
+    if (c16 == 0 && crow0 < S) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        if (crow0 + r < S) Ph[crow0 + r] = v[r];
+    }
+  }
+}
+
 }  // namespace
 
 int launch_attention_lse_f32(const rtkv_qk_desc& q, float* lse, hipStream_t st) {
@@ -506,6 +620,27 @@ int launch_qk_head_f32(const rtkv_qk_desc& q, int P, float* part, hipStream_t st
                    q.k_stride_h % 4 == 0 && q.k_stride_b % 4 == 0 && ((uintptr_t)q.q_dev % 16) == 0 &&
                    ((uintptr_t)q.k_dev % 16) == 0,
                "importance_qk_lse (fp32): Q/K rows must be 16-byte aligned");
+  // default: the split-bf16 kernel; RTKV_LSE_F32_EXACT also selects the exact f32-MFMA K1'
+  static const bool exact = getenv("RTKV_LSE_F32_EXACT") != nullptr;
+  if (!exact) {
+    constexpr size_t lds3 = (size_t)3 * 128 * 256 + 128 * sizeof(float);
+    // 16 waves per workgroup (four per SIMD; 6 registers spilled): 113.6 against 120.8 us per cfg3 fp32
+    // layer for 8 waves without spills (profiles/r05_qkf32_ab.json)
+    constexpr int nw = 16;
+    static bool attr3 = false;
+    if (!attr3) {
+      RTKV_HIP_CHECK(hipFuncSetAttribute((const void*)qk_head_f32x3_kernel<16>,
+                                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds3));
+      attr3 = true;
+    }
+    // rows per wave (16-row tiles): about 512 workgroups (two rounds of one per CU)
+    int rpw = 256;
+    while (rpw > 16 && (q.S + nw * rpw - 1) / (nw * rpw) * q.H * q.B < 512) rpw /= 2;
+    const dim3 grid((unsigned)((q.S + nw * rpw - 1) / (nw * rpw)), (unsigned)q.H, (unsigned)q.B);
+    hipLaunchKernelGGL(qk_head_f32x3_kernel<nw>, grid, dim3(64 * nw), lds3, st, q, P, part, rpw, t_begin);
+    RTKV_HIP_CHECK(hipGetLastError());
+    return RTKV_OK;
+  }
   constexpr size_t lds = (size_t)128 * kRB;
   static bool attr = false;
   if (!attr) {
