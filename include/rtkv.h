@@ -69,7 +69,12 @@ enum rtkv_layer_flag {
   RTKV_NO_SELECTION = 4,   /* keep every token (quantization only, BASELINE config 2) */
   RTKV_NO_FALLBACK = 8,    /* skip the top-10% emergency fallback (select_tokens_with_budget alone) */
   RTKV_SELECT_PIPELINE = 16, /* use the multi-workgroup selection pipeline even where the one-workgroup
-                              selection applies (B = 1, S <= 32768); same results, for cross-checks */
+                              selection applies (B = 1, S <= 65536); same results, for cross-checks */
+  RTKV_FINISH_EXACT = 32,  /* rtkv_compress_layer_finish: the caller sized its buffers EXACTLY from the published
+                              statistics — out_rows = max(S'_max, 1), packed_capacity = max(packed bytes, 1)
+                              rounded up to 256 — and any other size (a torn or stale read of the early line)
+                              raises RTKV_FLAG_OUTPUT_OVERFLOW (nothing written) instead of returning rows the
+                              device never wrote.  The drop-in sets it. */
   RTKV_TEST_WITHHOLD_SELECTION = 1 << 16, /* test only: the one-launch selection never publishes its
                               thresholds, so every waiting workgroup runs into its poll bound and the
                               layer reports RTKV_FLAG_SPIN_TIMEOUT instead of hanging */
@@ -319,7 +324,7 @@ int rtkv_compress_layer_events(const rtkv_kv_desc* kv, const rtkv_attn_desc* w,
  * writes them into `early_host` (host memory from rtkv_host_alloc) and then `seq`; the host spins on
  * that word (rtkv_wait_early) while the rest of K2 and all of K4 still run, and only score_m2 and
  * kept_score_sum must be read from stats_dev after the stream syncs.  *published = 1 when this call
- * will publish (the two-launch K2: B = 1, S <= 32768); 0: read stats_dev after a stream sync.
+ * will publish (the one-launch K2: B = 1, S <= 65536); 0: read stats_dev after a stream sync.
  * complete = 0 on publication means the top-10% fallback ran: read stats_dev after a sync too. */
 /* The published statistics are ONE 128-byte line (this struct's first 128 bytes, 128-byte aligned: the
  * start of an rtkv_host_alloc block) written by ONE wave store instruction (16 lanes x 8 bytes), with the
@@ -432,6 +437,24 @@ int rtkv_finalize_select(const float* A_dev, int a_dtype, int64_t B, int64_t S, 
                          const rtkv_layer_out* out, int64_t F, int kv_dtype, void* workspace_dev,
                          size_t workspace_bytes, void* stream);
 
+/* Step 1 that also clears what the same layer's rtkv_finalize_select_shard needs zeroed (the selection
+ * scratch in workspace_dev — sized by rtkv_workspace_size(B, S_total) — and out->stats_dev), so that call,
+ * with scratch_zeroed = 1 and the same params, runs without its two memset launches.  Same A as
+ * rtkv_attention_aggregation_shard. */
+int rtkv_attention_aggregation_shard_ws(const rtkv_attn_desc* w, int32_t prompt_len, int64_t row0,
+                                        int64_t S_total, float* A_dev, const rtkv_layer_params* p,
+                                        const rtkv_layer_out* out, void* workspace_dev, size_t workspace_bytes,
+                                        void* stream);
+
+/* Steps 3 and 4 in one call: rtkv_finalize_select on the gathered A (S = nranks·S_local tokens), then the
+ * rtkv_shard_ranges table of this layer.  Where the one-launch selection applies (B = 1, S <= 65536) its
+ * compaction phase writes the table itself: one launch instead of two (three with the memsets; none when
+ * scratch_zeroed = 1 after rtkv_attention_aggregation_shard_ws).  Same outputs as the separate calls. */
+int rtkv_finalize_select_shard(const float* A_dev, int a_dtype, int64_t B, int64_t S, const rtkv_layer_params* p,
+                               const rtkv_layer_out* out, int64_t F, int kv_dtype, int64_t S_local, int32_t nranks,
+                               int64_t* ranges_dev, int32_t scratch_zeroed, void* workspace_dev,
+                               size_t workspace_bytes, void* stream);
+
 /* rtkv_quantize_rows for the kept rows whose token lies in [row0, row0 + kv->S) (rank `rank` of
  * `nranks`); kv describes the local K/V rows (token row0 + i at local row i).  Packed codes and
  * scale/zero-point land at their global positions.  Dequantized rows: with ranges_dev (the
@@ -541,6 +564,54 @@ int rtkv_decode_attention_packed(const uint8_t* packed_k_dev, const uint8_t* pac
                                  int64_t row_capacity, const int64_t* rows_dev, int64_t Hkv, int64_t D, int dtype,
                                  const int32_t bits[3], const void* q_dev, int64_t Hq, float scale,
                                  float* out_dev, void* workspace_dev, size_t workspace_bytes, void* stream);
+
+/* ------------------------------------------------------------------------------------------------
+ * Extension "rtkv-gq/1": per-channel outlier detection + per-head group-wise 2/4/8-bit pack.
+ * NO REFERENCE COUNTERPART — the reference quantizes each token with one (scale, zero_point) over all H·D
+ * channels (dynamic_quantization.py:181-194).  Opt-in (rtkv.GroupQuantConfig; off by default, so the
+ * reference path and its goldens are untouched); parity UNPINNED: oracle/rtkv_oracle.c rtkvo_gq_* defines
+ * the mode and the kernels match it byte for byte.  B = 1, head_dim 128 (one group per head), K/V rows
+ * [S, H·128] with contiguous heads, H a multiple of 4, class widths 2/4/8 bits.
+ *   1. rtkv_gq_outlier_channels: every vote_stride-th kept row votes, per head, for its n_vote channels of
+ *      largest |x| (a wave arg-max by shuffles); the n_outlier channels with the most votes (at least
+ *      max(1, ceil(samples·min_votes_pm/1000))) are the layer's outlier channels of each head and tensor:
+ *      outlier_idx[2][H][n_outlier] (channel within the head, -1 = unused slot).
+ *   2. rtkv_gq_pack: per (kept row, tensor, head) the reference's per-token formulas (dynamic_quantization.py
+ *      :62-126, each op rounded to the dtype) over the head's non-outlier channels: codes of the row's class
+ *      width for every channel (outlier channels and NaN: code 0) at codes + row_offset[r] (the per-token
+ *      layout's row slots: F·w/8 bytes), meta[r][tensor][h] = {scale, zero_point} and raw[r][tensor][h][s] =
+ *      the outlier channels' input values, both in the K/V dtype.
+ *   3. rtkv_gq_unpack: the dequantized rows ((q − zp)·scale, outlier channels restored bit for bit).
+ *   4. rtkv_gq_decode_attention: decode attention over the format (as rtkv_decode_attention_packed).
+ * Rows: the first min(stats->kept, row_capacity) kept rows (kept_index, labels: the layer's per-token
+ * outputs). */
+typedef struct rtkv_gq_params {
+  int32_t n_outlier;      /* outlier channels per head and tensor, 0..16 */
+  int32_t n_vote;         /* channels each sampled row votes for, per head */
+  int32_t vote_stride;    /* every vote_stride-th kept row votes */
+  int32_t min_votes_pm;   /* votes a channel needs, per mille of the sampled rows (rounded up, at least 1) */
+} rtkv_gq_params;
+size_t rtkv_gq_workspace_size(int64_t H, int64_t D);
+int rtkv_gq_outlier_channels(const rtkv_kv_desc* kv, const int32_t* kept_index_dev, const uint8_t* labels_dev,
+                             const rtkv_layer_stats* stats_dev, const rtkv_gq_params* g, int64_t row_capacity,
+                             int16_t* outlier_idx_dev, void* workspace_dev, size_t workspace_bytes, void* stream);
+int rtkv_gq_pack(const rtkv_kv_desc* kv, const int32_t* kept_index_dev, const uint8_t* labels_dev,
+                 const rtkv_layer_stats* stats_dev, const int32_t bits[3], const rtkv_gq_params* g,
+                 const int16_t* outlier_idx_dev, const int64_t* row_offset_dev, uint8_t* codes_k_dev,
+                 uint8_t* codes_v_dev, int64_t codes_capacity, void* meta_dev, void* raw_dev, int64_t row_capacity,
+                 void* stream);
+int rtkv_gq_unpack(const rtkv_kv_desc* kv, const int32_t* kept_index_dev, const uint8_t* labels_dev,
+                   const rtkv_layer_stats* stats_dev, const int32_t bits[3], const rtkv_gq_params* g,
+                   const int16_t* outlier_idx_dev, const int64_t* row_offset_dev, const uint8_t* codes_dev,
+                   int64_t codes_capacity, const void* meta_dev, const void* raw_dev, int64_t row_capacity, int which,
+                   void* out_dev, void* stream);
+size_t rtkv_gq_decode_workspace_size(int64_t Hq, int64_t Hkv);
+int rtkv_gq_decode_attention(const rtkv_kv_desc* kv, const int32_t* kept_index_dev, const uint8_t* labels_dev,
+                             const rtkv_layer_stats* stats_dev, const int32_t bits[3], const rtkv_gq_params* g,
+                             const int16_t* outlier_idx_dev, const int64_t* row_offset_dev, const uint8_t* codes_k_dev,
+                             const uint8_t* codes_v_dev, int64_t codes_capacity, const void* meta_dev,
+                             const void* raw_dev, int64_t row_capacity, const void* q_dev, int64_t Hq, float scale,
+                             float* out_dev, void* workspace_dev, size_t workspace_bytes, void* stream);
 
 /* Copy the kept rows of a row-major tensor (row r of batch b = src row kept_index[b*cap + r]), zero
  * rows for r in [kept_b, S'_max), rows of row_bytes bytes, into dst (batch stride dst_stride_b bytes,

@@ -57,6 +57,9 @@ def lib():
             [p, p, i32, i64, i64, i64, p, i32, i64, i64, i64, f, f, f, f, f, f, p, d, i32]
             + [p] * 13 + [p, i32])
         L.rtkvo_compress_layer.restype = i64
+        L.rtkvo_gq_votes.argtypes = [p, i32, i64, i32, i32, p, i64, i32, i32, p]
+        L.rtkvo_gq_select.argtypes = [p, i32, i32, i32, ctypes.c_uint32, p]
+        L.rtkvo_gq_pack.argtypes = [p, i32, i64, i32, i32, p, i64, p, p, i32, p, p, p, p, p]
         _lib = L
     return _lib
 
@@ -218,3 +221,41 @@ def compress_layer(K, V, kvdt, W, wdt, P, alpha, beta, gamma, w_l, theta_h, thet
                 packed_k=pk[:total] if packed else None, packed_v=pv[:total] if packed else None,
                 row_offset=row_offset[:, :smax], kept=kept, cost_units=units, fallback=fb,
                 class_count=cc, max_kept=int(smax))
+
+
+# ----------------------------------------------------------------------------- extension: rtkv-gq/1
+# Per-channel outlier detection + per-head group-wise pack (no reference counterpart: parity UNPINNED;
+# oracle/rtkv_oracle.c defines the mode).  x: [S, F] rows (float32, or uint16 bits for half types).
+def gq_votes(x: np.ndarray, dt: int, H: int, D: int, tok: np.ndarray, n_vote: int, vote_stride: int) -> np.ndarray:
+    x = _c(x)
+    votes = np.zeros(H * D, np.uint32)
+    tok = _c(tok, np.int32)
+    lib().rtkvo_gq_votes(_ptr(x), dt, x.shape[-1], H, D, _ptr(tok), tok.size, n_vote, vote_stride, _ptr(votes))
+    return votes
+
+
+def gq_select(votes: np.ndarray, H: int, D: int, k: int, min_votes: int) -> np.ndarray:
+    idx = np.zeros((H, k), np.int16)
+    lib().rtkvo_gq_select(_ptr(_c(votes, np.uint32)), H, D, k, int(min_votes), _ptr(idx))
+    return idx
+
+
+def gq_pack(x: np.ndarray, dt: int, H: int, D: int, tok: np.ndarray, row_bits: np.ndarray, idx: np.ndarray,
+            row_offset: np.ndarray):
+    """-> (codes [bytes], meta [rows, H, 2], raw [rows, H, k], deq [rows, F]) in the storage types."""
+    x = _c(x)
+    tok = _c(tok, np.int32)
+    rows = tok.size
+    F = H * D
+    k = idx.shape[1]
+    store = np.float32 if dt == F32 else np.uint16
+    row_bits = _c(row_bits, np.int32)
+    row_offset = _c(row_offset, np.int64)
+    nbytes = int(row_offset[-1]) + (F * int(row_bits[-1]) + 7) // 8 if rows else 0
+    codes = np.zeros(max(nbytes, 1), np.uint8)
+    meta = np.zeros((rows, H, 2), store)
+    raw = np.zeros((rows, H, k), store)
+    deq = np.zeros((rows, F), store)
+    lib().rtkvo_gq_pack(_ptr(x), dt, x.shape[-1], H, D, _ptr(tok), rows, _ptr(row_bits), _ptr(_c(idx, np.int16)), k,
+                        _ptr(row_offset), _ptr(codes), _ptr(meta), _ptr(raw), _ptr(deq))
+    return codes[:nbytes], meta, raw, deq

@@ -51,6 +51,12 @@ static int carve(void* ws, size_t bytes, int64_t B, int64_t S, Workspace& w) {
   return RTKV_OK;
 }
 
+// The early line is published by one 128-byte wave store and taken as complete when its first and last
+// words carry the call's seq: it must not straddle two 128-byte lines (rtkv_host_alloc blocks are
+// page-aligned).
+static inline bool early_aligned(const void* early) { return ((uintptr_t)early & 127u) == 0; }
+static const char* const kEarlyAlignMsg = "early_host must be 128-byte aligned (allocate it with rtkv_host_alloc)";
+
 static int check_params(const rtkv_layer_params* p) {
   RTKV_REQUIRE(p != nullptr, "null params");
   for (int g = 0; g < 3; ++g) RTKV_REQUIRE(p->bits[g] >= 1 && p->bits[g] <= 16, "bits must be in [1, 16]");
@@ -228,6 +234,7 @@ static int compress_layer_impl(const rtkv_kv_desc* kv, const rtkv_attn_desc* w, 
   int rc = check_params(p);
   if (rc) return rc;
   RTKV_REQUIRE(kv && (w || qk) && out, "null descriptor");
+  RTKV_REQUIRE(early_aligned(early), kEarlyAlignMsg);
   if (w) RTKV_REQUIRE(kv->B == w->B && kv->S == w->S, "K/V and attention weights disagree on B or S");
   if (qk) RTKV_REQUIRE(kv->B == qk->B && kv->S == qk->S, "K/V and queries disagree on B or S");
   RTKV_REQUIRE(out->scores_dev && out->labels_dev && out->mask_dev && out->kept_index_dev && out->stats_dev,
@@ -376,6 +383,7 @@ int rtkv_compress_layer_finish(const rtkv_kv_desc* kv, const rtkv_layer_params* 
   RTKV_REQUIRE(kv && out && out->labels_dev && out->kept_index_dev && out->stats_dev,
                "compress_layer_finish needs the labels, kept_index and stats of rtkv_compress_layer_begin");
   RTKV_REQUIRE(out->row_capacity >= kv->S, "row_capacity must be the capacity rtkv_compress_layer_begin used (>= S)");
+  RTKV_REQUIRE(early_aligned(early_host), kEarlyAlignMsg);
   if (p->flags & RTKV_EMIT_PACKED)
     RTKV_REQUIRE(out->packed_k_dev && out->packed_v_dev && out->row_offset_dev && out->scale_zp_dev &&
                      out->packed_capacity >= 1,
@@ -387,12 +395,13 @@ int rtkv_compress_layer_finish(const rtkv_kv_desc* kv, const rtkv_layer_params* 
   Workspace ws;
   rc = carve(workspace_dev, workspace_bytes, kv->B, kv->S, ws);
   if (rc) return rc;
-  // the one-launch K2 (B = 1, S <= 32768) left each kept row's class in the workspace
+  // the one-launch K2 (B = 1, S <= 65536) left each kept row's class in the workspace
   const bool row_labels = select_fast_shape(kv->B, kv->S) && !(p->flags & RTKV_SELECT_PIPELINE);
   QuantArgs q = make_quant_args(kv, out->labels_dev, out->kept_index_dev, p, out, row_labels ? ws.labels : nullptr);
   // the buffers were sized on the host from the published statistics: K4 checks them on the device
   q.out_rows = (p->flags & RTKV_EMIT_DEQUANT) ? out_rows : ((int64_t)1 << 62);
   if (!(p->flags & RTKV_EMIT_PACKED)) q.out.packed_capacity = (int64_t)1 << 62;
+  q.exact_sizes = (p->flags & RTKV_FINISH_EXACT) ? 1 : 0;
   q.final_host = early_host;
   q.final_seq = seq;
   q.t_end = reinterpret_cast<unsigned long long*>(layer_times(out->stats_dev, kv->B)->end);
@@ -406,6 +415,7 @@ int rtkv_prefetch_kept_rows(const rtkv_kv_desc* kv, const rtkv_layer_out* out, i
 
 int rtkv_wait_early(const rtkv_early_stats* early_host, uint64_t seq, int64_t timeout_us) {
   RTKV_REQUIRE(early_host != nullptr, "null early-stats buffer");
+  RTKV_REQUIRE(early_aligned(early_host), kEarlyAlignMsg);
   const auto t0 = std::chrono::steady_clock::now();
   for (uint32_t it = 0;; ++it) {
     if (__atomic_load_n(&early_host->seq, __ATOMIC_ACQUIRE) == seq &&
@@ -423,6 +433,7 @@ int rtkv_wait_early(const rtkv_early_stats* early_host, uint64_t seq, int64_t ti
 
 int rtkv_wait_final(const rtkv_early_stats* early_host, uint64_t seq, int64_t timeout_us) {
   RTKV_REQUIRE(early_host != nullptr, "null early-stats buffer");
+  RTKV_REQUIRE(early_aligned(early_host), kEarlyAlignMsg);
   const auto t0 = std::chrono::steady_clock::now();
   for (uint32_t it = 0;; ++it) {
     if ((__atomic_load_n(&early_host->final_word, __ATOMIC_ACQUIRE) >> 16) == (seq & ((1ull << 48) - 1)))
@@ -496,6 +507,76 @@ int rtkv_attention_aggregation_shard(const rtkv_attn_desc* w, int32_t prompt_len
   x.row0 = row0;
   x.S_total = S_total;
   return launch_aggregation(*w, prompt_len, A_dev, (hipStream_t)stream, x);
+}
+
+// the selection scratch a finalize call needs zeroed: the one-launch K2's, or the pipeline's
+static size_t finalize_zero_bytes(int64_t B, int64_t S, const rtkv_layer_params* p) {
+  return (select_fast_shape(B, S) && !(p->flags & RTKV_SELECT_PIPELINE)) ? select_fast_zero_bytes() : select_zero_bytes(B);
+}
+
+int rtkv_attention_aggregation_shard_ws(const rtkv_attn_desc* w, int32_t prompt_len, int64_t row0, int64_t S_total,
+                                        float* A_dev, const rtkv_layer_params* p, const rtkv_layer_out* out,
+                                        void* workspace_dev, size_t workspace_bytes, void* stream) {
+  RTKV_REQUIRE(w != nullptr && p != nullptr && out != nullptr && out->stats_dev, "null descriptor, params or stats");
+  RTKV_REQUIRE(row0 >= 0 && S_total >= row0 + w->S, "shard rows [row0, row0 + S) must lie inside [0, S_total)");
+  Workspace ws;
+  int rc = carve(workspace_dev, workspace_bytes, w->B, S_total, ws);
+  if (rc) return rc;
+  AggExtras x;
+  x.row0 = row0;
+  x.S_total = S_total;
+  x.zero0 = ws.sel;  // what rtkv_finalize_select_shard(..., scratch_zeroed = 1) would otherwise memset
+  x.zero0_bytes = finalize_zero_bytes(w->B, S_total, p);
+  x.zero1 = out->stats_dev;
+  x.zero1_bytes = rtkv_stats_bytes(w->B);
+  return launch_aggregation(*w, prompt_len, A_dev, (hipStream_t)stream, x);
+}
+
+int rtkv_finalize_select_shard(const float* A_dev, int a_dtype, int64_t B, int64_t S, const rtkv_layer_params* p,
+                               const rtkv_layer_out* out, int64_t F, int kv_dtype, int64_t S_local, int32_t nranks,
+                               int64_t* ranges_dev, int32_t scratch_zeroed, void* workspace_dev, size_t workspace_bytes,
+                               void* stream) {
+  int rc = check_params(p);
+  if (rc) return rc;
+  RTKV_REQUIRE(A_dev && out && ranges_dev, "null argument");
+  RTKV_REQUIRE(B >= 1 && S >= 1 && F >= 1, "empty shape");
+  RTKV_REQUIRE(nranks >= 1 && S_local >= 1 && S_local * nranks == S, "S must be nranks * S_local");
+  RTKV_REQUIRE(out->scores_dev && out->labels_dev && out->mask_dev && out->kept_index_dev && out->stats_dev,
+               "finalize_select needs scores, labels, mask, kept_index and stats outputs");
+  RTKV_REQUIRE(out->row_capacity >= S, "row_capacity must be >= S (every token may be kept)");
+  if (p->flags & RTKV_EMIT_PACKED) {
+    RTKV_REQUIRE(out->row_offset_dev, "EMIT_PACKED needs row offsets");
+    for (int g = 0; g < 3; ++g)
+      RTKV_REQUIRE(field_width(kv_dtype, p->bits[g]) > 0, "packed codes unsupported for this dtype/bits");
+  }
+  Workspace ws;
+  rc = carve(workspace_dev, workspace_bytes, B, S, ws);
+  if (rc) return rc;
+  FinalizeArgs a = finalize_args(p, B, S);
+  a.A = A_dev;
+  a.a_dtype = a_dtype;
+  a.scores = out->scores_dev;
+  a.labels = out->labels_dev;
+  a.mask = out->mask_dev;
+  a.kept_index = out->kept_index_dev;
+  a.row_offset = out->row_offset_dev;
+  a.row_capacity = out->row_capacity;
+  a.F = F;
+  a.kv_dtype = kv_dtype;
+  a.stats = out->stats_dev;
+  a.mode_scores = 1;
+  a.mode_labels = 1;
+  a.mode_select = (p->flags & RTKV_NO_SELECTION) ? 2 : 1;
+  const bool fused = select_fast_eligible(a);
+  if (fused) {  // the one-launch K2's compaction writes the rank table (no rtkv_shard_ranges launch)
+    a.shard_ranges = ranges_dev;
+    a.shard_S_local = S_local;
+    a.shard_nranks = nranks;
+  }
+  rc = launch_select(a, ws.sel, scratch_zeroed != 0, (hipStream_t)stream);
+  if (rc || fused) return rc;
+  return launch_shard_ranges(out->kept_index_dev, out->row_offset_dev, out->stats_dev, B, out->row_capacity, S_local,
+                             nranks, ranges_dev, (hipStream_t)stream);
 }
 
 int rtkv_finalize_select(const float* A_dev, int a_dtype, int64_t B, int64_t S, const rtkv_layer_params* p,

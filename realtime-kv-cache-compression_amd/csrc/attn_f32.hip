@@ -277,7 +277,10 @@ constexpr int kX3Plane = kX3Keys * 256;  // one bf16 plane of a tile (16 KiB)
 
 __device__ __forceinline__ void split3(float x, __bf16& h, __bf16& l, __bf16& ll) {
   h = (__bf16)x;
-  const float r1 = __builtin_isfinite(x) ? x - (float)h : 0.f;  // exact (x and h share the leading bits)
+  // exact (x and h share the leading bits).  A value with no finite bf16 head (±inf, or finite above the
+  // bf16 maximum ≈ 3.39e38, which rounds to inf) keeps l = ll = 0: its products with the other operand's
+  // parts are ±inf or NaN, as the exact kernel's product with an overflowing operand is
+  const float r1 = __builtin_isfinite((float)h) ? x - (float)h : 0.f;
   l = (__bf16)r1;
   const float r2 = r1 - (float)l;                               // exact
   ll = (__bf16)r2;

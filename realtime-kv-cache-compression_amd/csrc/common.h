@@ -251,13 +251,18 @@ struct FinalizeArgs {
   uint8_t* row_label;      // optional [B][cap] class of each kept row, for K4 (fast path writes it)
   rtkv_early_stats* early = nullptr;  // optional host-mapped stats mirror (fast path only)
   uint64_t early_seq = 0;
+  // optional (fast path, B = 1): the rtkv_shard_ranges table of a sequence-sharded layer, written by the
+  // selection's compaction phase itself — rank j's first output row and packed byte at token j·shard_S_local
+  int64_t* shard_ranges = nullptr;
+  int64_t shard_S_local = 0;
+  int shard_nranks = 0;
 };
 // K2 pipeline (select.hip).  sel_ws: select_workspace_bytes(B, S) bytes; `zeroed` = its first
 // select_zero_bytes(B) bytes and the stats are already zero (K1 clears them in rtkv_compress_layer).
 size_t select_workspace_bytes(int64_t B, int64_t S);
 size_t select_zero_bytes(int64_t B);
 int launch_select(const FinalizeArgs& a, void* sel_ws, bool zeroed, hipStream_t st);
-// Two-launch K2 (select_fast.hip) for B = 1, S <= 32768; launch_select takes it whenever it is
+// One-launch K2 (select_fast.hip) for B = 1, S <= 65536; launch_select takes it whenever it is
 // eligible.  It needs select_fast_zero_bytes() of zeroed workspace (K1 clears them).
 bool select_fast_shape(int64_t B, int64_t S);
 bool select_fast_eligible(const FinalizeArgs& a);
@@ -289,6 +294,9 @@ struct QuantArgs {
   // with the device statistics first (RTKV_FLAG_OUTPUT_OVERFLOW, nothing written).  final_host: K4's first
   // lane publishes the layer's final flags + final_seq there.
   int64_t out_rows;
+  // RTKV_FINISH_EXACT: out_rows must be max(S'_max, 1) and out.packed_capacity max(packed bytes, 1) rounded up
+  // to 256 — any other size (a torn or stale read of the early line on the host) is flagged as an overflow
+  int32_t exact_sizes;
   rtkv_early_stats* final_host;
   uint64_t final_seq;
   // rtkv_layer_times.end of the fused driver's layer (atomic max over K4's workgroups), or null

@@ -470,8 +470,13 @@ __device__ __forceinline__ bool k4_layer_gate(const QuantArgs& a) {
   rtkv_layer_stats* st = const_cast<rtkv_layer_stats*>(a.stats);
   int flags = st->error_flags;
   const int64_t max_kept = st->max_kept, nbytes = st->total_packed_bytes;
-  const bool over = a.out_rows > 0 && ((a.out.k_out_dev && max_kept > a.out_rows) ||
-                                       (a.out.packed_k_dev && nbytes > a.out.packed_capacity));
+  // exact sizing (the drop-in): a size other than the one the device statistics give means the host read a
+  // torn or stale early line — raised, never written into
+  const int64_t rows_exact = max_kept > 1 ? max_kept : 1, bytes_exact = ((nbytes > 1 ? nbytes : 1) + 255) / 256 * 256;
+  const bool over = a.out_rows > 0 &&
+                    ((a.out.k_out_dev && (max_kept > a.out_rows || (a.exact_sizes && a.out_rows != rows_exact))) ||
+                     (a.out.packed_k_dev &&
+                      (nbytes > a.out.packed_capacity || (a.exact_sizes && a.out.packed_capacity != bytes_exact))));
   if (over) flags |= RTKV_FLAG_OUTPUT_OVERFLOW;
   if (blockIdx.x == 0 && threadIdx.x == 0) {
     if (over) atomicOr(&st->error_flags, (int)RTKV_FLAG_OUTPUT_OVERFLOW);
@@ -639,23 +644,36 @@ __global__ __launch_bounds__(256, PKW ? PKW : ((DT == RTKV_F32 && NCH == 8 && FU
   stamp_end(a.t_end, wrote);
 }
 
-// Split-row K4 for short layers (one batch row, contiguous rows of NSPLIT·NCHW·512 elements, no
-// shards): one workgroup of NSPLIT waves per (kept row, tensor), wave q owning chunks
+// Split-row K4 (one batch row, contiguous rows of NSPLIT·NCHW·512 elements; a sequence shard with its
+// rtkv_shard_ranges table too): one workgroup of NSPLIT waves per (kept row, tensor), wave q owning chunks
 // [q·NCHW·64, (q+1)·NCHW·64) of the row.  At S = 4096 quant_rows_kernel has ~1.2 waves of kept work
 // per wave slot, so its second, mostly empty round of whole-row waves (a full load → min/max →
 // store latency chain each) is a third of the kernel; here a task is NSPLIT times shorter.  The
 // row's min / max / min |x| / NaN flag are combined through LDS; fminf/fmaxf are order-independent
 // (a zero's sign reaches neither scale nor zero-point), so every output equals quant_rows_kernel's.
+// Shard (S_glob != 0, shard_ranges set): the rank's kept rows are the contiguous output rows
+// [first_row(rank), first_row(rank + 1)) of the global selection, so task t takes row first_row + t/2 and
+// the grid is sized by the rank's S_local tokens (a bound on its rows) instead of S_global: no task of
+// another rank's rows is launched.  The row's codes and scale/zero-point land at their global positions,
+// its dequantized row at local row r − first_row.
 template <int DT, int NCHW, int NSPLIT>
 __global__ __launch_bounds__(64 * NSPLIT) void quant_rows_split_kernel(QuantArgs a) {
   using S_ = typename Dt<DT>::S;
   const int lane = threadIdx.x & 63;
   const int q = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int S = (int)a.kv.S;
+  const bool shard = a.S_glob != 0;
+  const int S = shard ? (int)a.S_glob : (int)a.kv.S;  // tokens of the selection
+  const int Sl = (int)a.kv.S;                          // tokens of this launch's K/V rows
   const int cap = (int)a.out.row_capacity;
-  const int tasks = 2 * (a.kept_index ? (cap < S ? cap : S) : S);
+  const int tasks = 2 * (a.kept_index ? (cap < Sl ? cap : Sl) : Sl);
   const rtkv_batch_stats* bst = a.stats ? reinterpret_cast<const rtkv_batch_stats*>(a.stats + 1) : nullptr;
   if (k4_layer_gate<DT>(a)) return;  // buffer sizes, final flags, a timed-out selection
+  int r_first = 0, r_end = cap;
+  if (shard) {
+    r_first = (int)a.shard_ranges[2 * a.shard_rank];
+    r_end = (int)a.shard_ranges[2 * (a.shard_rank + 1)];
+  }
+  const int row0 = (int)a.row0;
   const bool emit_deq = a.out.k_out_dev != nullptr;
   const bool emit_pk = a.out.packed_k_dev != nullptr;
   __shared__ float xch[NSPLIT][4];
@@ -671,18 +689,19 @@ __global__ __launch_bounds__(64 * NSPLIT) void quant_rows_split_kernel(QuantArgs
   bool wrote = false;
   for (int t = blockIdx.x; t < tasks; t += gridDim.x) {  // every condition below is uniform per task
     const int which = t & 1;
-    const int r = t >> 1;
+    const int r = r_first + (t >> 1);
     const int rs = r < cap ? r : cap - 1;
     const int i_s = a.kept_index ? a.kept_index[rs] : r;
     const int l_s = a.row_label ? (int)a.row_label[rs] : 0;
     const int64_t roff = emit_pk ? a.out.row_offset_dev[rs] : 0;
     const int kept_b = a.kept_index ? (int)bst[0].kept : S;
-    if (r >= kept_b) continue;
+    if (r >= kept_b || r >= r_end) continue;
     if ((unsigned)i_s >= (unsigned)S) continue;  // never read outside the layer (corrupt kept_index)
+    if ((unsigned)(i_s - row0) >= (unsigned)Sl) continue;  // (shards) another rank's token: inconsistent ranges
     const int i = __builtin_amdgcn_readfirstlane(i_s);
     const int lab = __builtin_amdgcn_readfirstlane(a.row_label ? l_s : (int)a.labels[i]);
     S_* orow = emit_deq ? static_cast<S_*>(which ? a.out.v_out_dev : a.out.k_out_dev) +
-                              (int64_t)r * a.out.o_stride_s + qoff
+                              (int64_t)(r - r_first) * a.out.o_stride_s + qoff
                         : nullptr;
     const int64_t sz_idx = (int64_t)r * 4 + which * 2;
     if (lab > 2) {  // zero row (caller classes outside {0,1,2})
@@ -696,7 +715,7 @@ __global__ __launch_bounds__(64 * NSPLIT) void quant_rows_split_kernel(QuantArgs
     }
     const int bits = lab == 0 ? a.bits[0] : (lab == 1 ? a.bits[1] : a.bits[2]);
     const int w = field_width(DT, bits);
-    const S_* src = static_cast<const S_*>(which ? a.kv.v_dev : a.kv.k_dev) + (int64_t)i * a.kv.stride_s + qoff;
+    const S_* src = static_cast<const S_*>(which ? a.kv.v_dev : a.kv.k_dev) + (int64_t)(i - row0) * a.kv.stride_s + qoff;
     Chunk<DT> raw[NCHW];
 #pragma unroll
     for (int k = 0; k < NCHW; ++k) raw[k] = load_chunk_nt<DT>(src + off[k]);
@@ -892,16 +911,18 @@ int launch_quant_dt(const QuantArgs& a, hipStream_t st) {
   // K4 87.2 -> 82.5 us, S = 4096 29.0 -> 26.8 (against 4 waves), S = 65536 332 -> 317; bf16 cfg3 150.7
   // -> 142.0 (profiles/r05_k4_split2_ab.json).  fp32 (153.3 vs 154.6 us at cfg3, 43.9 vs 45.4 at
   // S = 4096) and fp16 packed-only (59.2 vs 59.9) keep theirs.  (F = 4096 rows: the measured shape.)
-  if (DT != RTKV_F32 && a.out.k_out_dev && split_env < 0 && contig && kv.B == 1 && a.S_glob == 0 && a.kept_index &&
-      nch == 512) {
-    hipLaunchKernelGGL((quant_rows_split_kernel<DT, 4, 2>), dim3((unsigned)tasks), dim3(128), 0, st, a);
+  // shards with their ranges table: the split-row kernel over the rank's own rows only (grid 2·S_local)
+  const bool split_ok = contig && kv.B == 1 && a.kept_index && (a.S_glob == 0 || a.shard_ranges);
+  const int64_t split_tasks = 2 * (a.out.row_capacity < kv.S ? a.out.row_capacity : kv.S);
+  if (DT != RTKV_F32 && a.out.k_out_dev && split_env < 0 && split_ok && nch == 512) {
+    hipLaunchKernelGGL((quant_rows_split_kernel<DT, 4, 2>), dim3((unsigned)split_tasks), dim3(128), 0, st, a);
     RTKV_HIP_CHECK(hipGetLastError());
     return RTKV_OK;
   }
   // (packed-only 2-byte rows over 2 waves, compile-time packed-only at 4 or 5 waves per SIMD: 60.3 / 60.5
   // against 59.7 us for the whole-row kernel at cfg3 fp16, profiles/r05_k4_split2_ab.json: not used)
-  if (contig && kv.B == 1 && a.S_glob == 0 && a.kept_index && Sg <= split_maxs && (nch % 64) == 0) {
-    const unsigned g = (unsigned)tasks;
+  if (split_ok && Sg <= split_maxs && (nch % 64) == 0) {
+    const unsigned g = (unsigned)split_tasks;
 #define RTKV_QS(NCHT, NCHW, NSPLIT)                                                                       \
     if (nch == (int64_t)NCHT * 64) {                                                                      \
       hipLaunchKernelGGL((quant_rows_split_kernel<DT, NCHW, NSPLIT>), dim3(g), dim3(64 * NSPLIT), 0, st, a); \

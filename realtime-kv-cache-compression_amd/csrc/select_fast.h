@@ -1,5 +1,5 @@
-// select_fast.h — K2 for one batch row (B = 1, S <= 32768: every reference configuration that
-// fits one GPU) in ONE launch instead of select.hip's four, with every per-token pass spread over
+// select_fast.h — K2 for one batch row (B = 1, S <= 65536: every reference configuration, and the
+// replicated global selection of the sequence-sharded prefill up to the north star's S = 64k) in ONE launch instead of select.hip's four, with every per-token pass spread over
 // the whole grid.  Same outputs, bit for bit (scores, classes, mask, kept_index, row_offset,
 // row_label, counts; the double statistics to 1e-12 relative).
 //
@@ -29,7 +29,7 @@
 // 3 compact Every workgroup, its token still in registers: keep decisions, all local (mode, T, cutoff
 //           per group); per-class ranks by wave ballots; the workgroup's kept counts per class
 //           published, its predecessors' summed (decoupled look-back: every count is published before
-//           any is awaited, and all G <= 32 workgroups are resident at once); mask, kept_index,
+//           any is awaited, and all G <= 64 workgroups are resident at once); mask, kept_index,
 //           row_label, row_offset; its kept-token statistics are added atomically.
 //
 // Hand-offs between workgroups are TAGGED 8-byte words (bit 63 set on a zeroed word: the region is
@@ -39,6 +39,8 @@
 // left is phase 1's: a workgroup's slot-list entries and score sums are complete (s_waitcnt
 // vmcnt(0)) before its tagged ready word, which every workgroup's phase 2 polls.
 #pragma once
+#include <type_traits>
+
 #include "common.h"
 
 #ifdef RTKV_SELECT_PROBE  // diagnostic build (tools/k2_probe.hip): phase timestamps (s_memrealtime, 100 MHz)
@@ -64,8 +66,8 @@ constexpr int kBinBits = 12;
 constexpr int kNBin = 1 << kBinBits;
 constexpr int kGrp = 4;            // classes LOW, MEDIUM, HIGH + "all tokens" (fallback)
 constexpr int kCap = 64;           // slot list entries per bin (one per lane of a wave)
-constexpr int kMaxS = 32 * kST;    // 32 tokens per thread in the rescan path
-constexpr int kMaxG = kMaxS / kST; // workgroups
+constexpr int kMaxS = 64 * kST;    // 64 tokens per thread in the rescan path (S = 65536: 64 workgroups)
+constexpr int kMaxG = kMaxS / kST; // workgroups (<= 64: one wave's lanes poll them all)
 constexpr uint64_t kTag = 1ull << 63;
 enum { M_NONE = 0, M_ALL = 1, M_PART = 2 };
 
@@ -136,23 +138,32 @@ __device__ __forceinline__ uint32_t wave_scan_dpp(uint32_t v) {
   return (uint32_t)x;
 }
 
-// Exclusive block scan of four packed 16-bit fields (block totals < 65536 each) as two 32-bit DPP
-// scans sharing one barrier: the threshold bins of every partially kept group in one pass.
-// `sh` is a [2][kSW] LDS array private to the call site.
-__device__ __forceinline__ uint64_t block_excl_scan16x4(uint64_t v, uint32_t (*sh)[kSW]) {
+// Exclusive block scans of four uint32 counters (block totals < 2^32: a group's count reaches S = 65536,
+// so 16-bit fields packed two to a word would carry into each other) as four DPP wave scans sharing one
+// barrier: the threshold bins of every partially kept group in one pass.  `sh` is a [kGrp][kSW] LDS
+// array private to the call site.
+__device__ __forceinline__ void block_excl_scan32x4(const uint32_t (&v)[kGrp], uint32_t (&ex)[kGrp],
+                                                    uint32_t (*sh)[kSW]) {
   const int lane = threadIdx.x & (kWave - 1), wid = threadIdx.x / kWave;
-  const uint32_t lo = (uint32_t)v, hi = (uint32_t)(v >> 32);
-  const uint32_t ilo = wave_scan_dpp(lo), ihi = wave_scan_dpp(hi);
-  if (lane == kWave - 1) { sh[0][wid] = ilo; sh[1][wid] = ihi; }
-  __syncthreads();
-  uint32_t wlo = sh[0][lane & (kSW - 1)], whi = sh[1][lane & (kSW - 1)];
+  uint32_t inc[kGrp];
 #pragma unroll
-  for (int o = 1; o < kSW; o <<= 1) {
-    const uint32_t nlo = __shfl_up(wlo, o, kWave), nhi = __shfl_up(whi, o, kWave);
-    if ((lane & (kSW - 1)) >= o) { wlo += nlo; whi += nhi; }
+  for (int q = 0; q < kGrp; ++q) inc[q] = wave_scan_dpp(v[q]);
+  if (lane == kWave - 1) {
+#pragma unroll
+    for (int q = 0; q < kGrp; ++q) sh[q][wid] = inc[q];
   }
-  const uint32_t blo = wid > 0 ? __shfl(wlo, wid - 1, kWave) : 0u, bhi = wid > 0 ? __shfl(whi, wid - 1, kWave) : 0u;
-  return ((uint64_t)(bhi + ihi - hi) << 32) | (uint64_t)(blo + ilo - lo);
+  __syncthreads();
+#pragma unroll
+  for (int q = 0; q < kGrp; ++q) {
+    uint32_t w = sh[q][lane & (kSW - 1)];
+#pragma unroll
+    for (int o = 1; o < kSW; o <<= 1) {
+      const uint32_t n = __shfl_up(w, o, kWave);
+      if ((lane & (kSW - 1)) >= o) w += n;
+    }
+    const uint32_t base = wid > 0 ? __shfl(w, wid - 1, kWave) : 0u;
+    ex[q] = base + inc[q] - v[q];
+  }
 }
 
 // Ranks in thread order of NF one-bit flags per thread, and their workgroup totals, from wave
@@ -184,25 +195,6 @@ __device__ __forceinline__ void block_flag_ranks(const bool (&f)[NF], uint32_t (
   }
 }
 
-// Exclusive block scan of a packed uint64 (independent 16-bit fields whose block totals stay
-// < 65536); *total = the block total.  `sh` is a [kSW] LDS array private to this call site.
-__device__ __forceinline__ uint64_t block_excl_scan(uint64_t v, uint64_t* sh, uint64_t* total) {
-  const int lane = threadIdx.x & (kWave - 1), wid = threadIdx.x / kWave;
-  const uint64_t inc = wave_inclusive_scan(v);
-  if (lane == kWave - 1) sh[wid] = inc;
-  __syncthreads();
-  // lanes 0..15 scan the 16 wave totals; lane wid-1 holds the base of this wave, lane 15 the total
-  uint64_t ws = sh[lane & (kSW - 1)];
-#pragma unroll
-  for (int o = 1; o < kSW; o <<= 1) {
-    const uint64_t n = __shfl_up(ws, o, kWave);
-    if ((lane & (kSW - 1)) >= o) ws += n;
-  }
-  *total = __shfl(ws, kSW - 1, kWave);
-  const uint64_t base = wid > 0 ? __shfl(ws, wid - 1, kWave) : 0ull;
-  return base + inc - v;
-}
-
 __device__ __forceinline__ int64_t row_bytes(const FinalizeArgs& a, int lab) {
   return (a.F * field_width(a.kv_dtype < 0 ? RTKV_F32 : a.kv_dtype, a.p.bits[lab]) + 7) / 8;
 }
@@ -227,13 +219,12 @@ __device__ __forceinline__ uint64_t to11(uint64_t v16, int n) {
     if (q < n) r |= (uint64_t)fld(v16, q) << (11 * q);
   return r;
 }
-__device__ __forceinline__ uint64_t from11(uint64_t v11, int n) {
-  uint64_t r = 0;
-#pragma unroll
-  for (int q = 0; q < 4; ++q)
-    if (q < n) r |= ((v11 >> (11 * q)) & 0x7ffull) << (16 * q);
-  return r;
+// 11-bit per-workgroup class counts -> 21-bit fields: a sum over the <= 64 workgroups of a row (up to
+// S = 65536 tokens in one class) never carries into the next field
+__device__ __forceinline__ uint64_t from11w(uint64_t v11) {
+  return (v11 & 0x7ffull) | (((v11 >> 11) & 0x7ffull) << 21) | (((v11 >> 22) & 0x7ffull) << 42);
 }
+__device__ __forceinline__ uint32_t fldw(uint64_t v, int g) { return (uint32_t)(v >> (21 * g)) & 0x1fffffu; }
 
 // A histogram increment whose return value is the token's slot, aggregated over the wave: lanes with
 // the same bin id v (< 2^14) share one atomic by the lowest of them, and each takes base + its rank
@@ -299,47 +290,54 @@ __device__ __forceinline__ uint64_t poll_tagged(const uint64_t* words, int strid
 
 // ------------------------------------------------------------------------------------ rescan path
 // Exact threshold of every group in `heavy` (a threshold bin with more than kCap tokens: heavy
-// ties) from all S keys held in registers: candidates = the group's tokens in its threshold bin,
-// then ≤ 3 rounds of key-range LDS histograms (span −12 bits per round).  need[q]: tokens to take
-// from the candidates on entry, tokens at the threshold key on exit.
+// ties) from all S keys: candidates = the group's tokens in its threshold bin, then ≤ 3 rounds of
+// key-range LDS histograms (span −12 bits per round).  need[q]: tokens to take from the candidates on
+// entry, tokens at the threshold key on exit.  Thread t owns tokens [t·TPT, (t+1)·TPT) (TPT = S/1024
+// rounded up to 16, 32 or 64).  The scores are reloaded (from L2) in chunks of 8 for every pass, so nothing
+// per token stays live: the rare heavy-tie path pays the reloads instead of the whole kernel paying TPT
+// registers of keys (held in registers, the keys spilled 15 VGPRs at TPT = 16 and 110 at TPT = 32 once the
+// scans went to 32 bits; streamed, the kernel takes 99-100 VGPRs at every TPT and spills none).
 template <int TPT>
 __device__ __forceinline__ void rescan_thresholds(const FastArgs& g, uint32_t* hist_lds, int heavy, bool fallback,
                                                   const int (&bstar)[kGrp], int (&need)[kGrp], uint32_t (&thr)[kGrp],
                                                   uint32_t (&cut)[kGrp]) {
+  constexpr int kCh = 8;  // tokens per load batch
+  using Mask = typename std::conditional<(TPT > 32), uint64_t, uint32_t>::type;
   const FinalizeArgs& a = g.f;
-  __shared__ uint64_t s_scan[4][kSW];
+  __shared__ uint32_t s_scan[4][kGrp][kSW];
   __shared__ uint32_t s_key[2 * kGrp][kSW];
   __shared__ uint32_t s_pick[2][kGrp][2];
-  __shared__ uint32_t s_cs[2][kSW];
+  __shared__ uint32_t s_cs[kGrp][kSW];
   __shared__ uint32_t s_cut[kGrp];
   const int t = threadIdx.x, lane = t & (kWave - 1), wid = t / kWave;
   const int S = (int)a.S;
   const int i0 = t * TPT;
   const int nv = S - i0 < 0 ? 0 : (S - i0 > TPT ? TPT : S - i0);
-  float sv[TPT];
-#pragma unroll
-  for (int k = 0; k < TPT; ++k) sv[k] = ld_sc1(a.scores + (i0 + k < S ? i0 + k : S - 1));
-  uint32_t key[TPT];
-  uint64_t grp = 0;  // 2 bits per token: its group
-  uint32_t cand = 0;
+  // a token's group, and whether it is a candidate of group q (q heavy, the token in q's threshold bin)
+  auto group_of = [&](float s) { return fallback ? 3 : class_of(s, a.p); };
+  auto cand_q = [&](float s, int e, int k, int q) {
+    return (k < nv) & (e == q) & (((heavy >> q) & 1) != 0) & (bin_of(s, g.bin_lo[q], g.bin_inv[q]) == bstar[q]);
+  };
   uint32_t kmn[kGrp], kmx[kGrp];
 #pragma unroll
   for (int q = 0; q < kGrp; ++q) { kmn[q] = 0xffffffffu; kmx[q] = 0u; }
+#pragma unroll 1
+  for (int k0 = 0; k0 < TPT; k0 += kCh) {
+    float sv[kCh];
 #pragma unroll
-  for (int k = 0; k < TPT; ++k) {
-    const float s = sv[k];
-    const int e = fallback ? 3 : class_of(s, a.p);
-    grp |= (uint64_t)e << (2 * k);
-    key[k] = score_key(s);
-    bool c = false;
+    for (int j = 0; j < kCh; ++j) sv[j] = ld_sc1(a.scores + (i0 + k0 + j < S ? i0 + k0 + j : S - 1));
 #pragma unroll
-    for (int q = 0; q < kGrp; ++q) {
-      const bool cq = (k < nv) & (e == q) & (((heavy >> q) & 1) != 0) & (bin_of(s, g.bin_lo[q], g.bin_inv[q]) == bstar[q]);
-      kmn[q] = cq ? min(kmn[q], key[k]) : kmn[q];
-      kmx[q] = cq ? max(kmx[q], key[k]) : kmx[q];
-      c |= cq;
+    for (int j = 0; j < kCh; ++j) {
+      const float s = sv[j];
+      const int e = group_of(s);
+      const uint32_t kk = score_key(s);
+#pragma unroll
+      for (int q = 0; q < kGrp; ++q) {
+        const bool cq = cand_q(s, e, k0 + j, q);
+        kmn[q] = cq ? min(kmn[q], kk) : kmn[q];
+        kmx[q] = cq ? max(kmx[q], kk) : kmx[q];
+      }
     }
-    cand |= (uint32_t)c << k;
   }
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1)
@@ -378,41 +376,47 @@ __device__ __forceinline__ void rescan_thresholds(const FastArgs& g, uint32_t* h
       sh[q] = bl > kBinBits ? bl - kBinBits : 0;
     }
     if (!act) break;
-    opaque(grp);
     for (int w = t; w < kGrp * kNBin / 4; w += kST) reinterpret_cast<uint4*>(hist_lds)[w] = make_uint4(0u, 0u, 0u, 0u);
     if (t < kGrp) { s_pick[round & 1][t][0] = 0u; s_pick[round & 1][t][1] = 0u; }
     __syncthreads();
+    // each candidate token into its group's key-range histogram (per-group compares combined by masks: no
+    // per-token indexing)
+#pragma unroll 1
+    for (int k0 = 0; k0 < TPT; k0 += kCh) {
+      float sv[kCh];
 #pragma unroll
-    for (int k = 0; k < TPT; ++k) {
-      const int e = (int)((grp >> (2 * k)) & 3u);
-      bool in = false;
-      uint32_t off = 0u;
+      for (int j = 0; j < kCh; ++j) sv[j] = ld_sc1(a.scores + (i0 + k0 + j < S ? i0 + k0 + j : S - 1));
 #pragma unroll
-      for (int q = 0; q < kGrp; ++q) {  // per-group compares combined by masks: no per-token indexing
-        const bool iq = (((cand >> k) & 1u) != 0) & (e == q) & (((act >> q) & 1) != 0) & (key[k] >= lo[q]) &
-                        (key[k] <= hi[q]);
-        in |= iq;
-        off = iq ? (uint32_t)(q * kNBin) + ((key[k] - lo[q]) >> sh[q]) : off;
+      for (int j = 0; j < kCh; ++j) {
+        const int e = group_of(sv[j]);
+        const uint32_t kk = score_key(sv[j]);
+        bool in = false;
+        uint32_t off = 0u;
+#pragma unroll
+        for (int q = 0; q < kGrp; ++q) {
+          const bool iq = cand_q(sv[j], e, k0 + j, q) & (((act >> q) & 1) != 0) & (kk >= lo[q]) & (kk <= hi[q]);
+          in |= iq;
+          off = iq ? (uint32_t)(q * kNBin) + ((kk - lo[q]) >> sh[q]) : off;
+        }
+        if (in) atomicAdd(&hist_lds[off], 1u);
       }
-      if (in) atomicAdd(&hist_lds[off], 1u);
     }
     __syncthreads();
     uint32_t c[kGrp][4];
-    uint64_t pk = 0;
+    uint32_t pk[kGrp], ex[kGrp];
 #pragma unroll
     for (int q = 0; q < kGrp; ++q) {
       const uint4 h4 = (act >> q) & 1 ? reinterpret_cast<const uint4*>(hist_lds + q * kNBin)[kNBin / 4 - 1 - t]
                                       : make_uint4(0u, 0u, 0u, 0u);
       c[q][0] = h4.w; c[q][1] = h4.z; c[q][2] = h4.y; c[q][3] = h4.x;
-      pk |= (uint64_t)(c[q][0] + c[q][1] + c[q][2] + c[q][3]) << (16 * q);
+      pk[q] = c[q][0] + c[q][1] + c[q][2] + c[q][3];
     }
-    uint64_t tot;
-    const uint64_t ex = block_excl_scan(pk, s_scan[round], &tot);
+    block_excl_scan32x4(pk, ex, s_scan[round]);
 #pragma unroll
     for (int q = 0; q < kGrp; ++q) {
       if (!((act >> q) & 1)) continue;
-      int run = (int)fld(ex, q);
-      if (run < need[q] && need[q] <= run + (int)fld(pk, q)) {
+      int run = (int)ex[q];
+      if (run < need[q] && need[q] <= run + (int)pk[q]) {
         bool found = false;
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
@@ -440,7 +444,7 @@ __device__ __forceinline__ void rescan_thresholds(const FastArgs& g, uint32_t* h
   // that key in token order (thread t holds tokens i0..i0+TPT-1, so a block scan of per-thread tie
   // counts is in token order): the cutoff is the index of the last one taken
   // (the scores are reloaded, 4 at a time, so that no per-token key stays live past the rounds)
-  uint32_t atm[kGrp] = {0u, 0u, 0u, 0u};
+  Mask atm[kGrp] = {0, 0, 0, 0};
   opaque(heavy);
 #pragma unroll 1
   for (int k0 = 0; k0 < TPT; k0 += 4) {
@@ -450,23 +454,23 @@ __device__ __forceinline__ void rescan_thresholds(const FastArgs& g, uint32_t* h
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const uint32_t kk = score_key(s4[j]);
-      const int e = fallback ? 3 : class_of(s4[j], a.p);
+      const int e = group_of(s4[j]);
 #pragma unroll
       for (int q = 0; q < kGrp; ++q)
-        atm[q] |= (uint32_t)((k0 + j < nv) & (e == q) & (((heavy >> q) & 1) != 0) & (kk == lo[q])) << (k0 + j);
+        atm[q] |= (Mask)((k0 + j < nv) & (e == q) & (((heavy >> q) & 1) != 0) & (kk == lo[q])) << (k0 + j);
     }
   }
-  uint64_t pc = 0;
+  uint32_t pc[kGrp], exc[kGrp];
 #pragma unroll
-  for (int q = 0; q < kGrp; ++q) pc |= (uint64_t)__popc(atm[q]) << (16 * q);
-  const uint64_t ex = block_excl_scan16x4(pc, s_cs);
+  for (int q = 0; q < kGrp; ++q) pc[q] = (uint32_t)__popcll((uint64_t)atm[q]);
+  block_excl_scan32x4(pc, exc, s_cs);
 #pragma unroll
   for (int q = 0; q < kGrp; ++q) {
-    const int base = (int)fld(ex, q);
-    if (((heavy >> q) & 1) && base < need[q] && need[q] <= base + (int)fld(pc, q)) {
-      uint32_t m = atm[q];
-      for (int j = base + 1; j < need[q]; ++j) m &= m - 1u;  // drop the ties taken before the last one
-      s_cut[q] = (uint32_t)(i0 + __ffs((int)m) - 1);
+    const int base = (int)exc[q];
+    if (((heavy >> q) & 1) && base < need[q] && need[q] <= base + (int)pc[q]) {
+      Mask m = atm[q];
+      for (int j = base + 1; j < need[q]; ++j) m &= m - 1;  // drop the ties taken before the last one
+      s_cut[q] = (uint32_t)(i0 + __ffsll((unsigned long long)m) - 1);
     }
   }
   __syncthreads();
@@ -539,7 +543,7 @@ template <int TPT>
 __device__ __forceinline__ void select_thresholds(const FastArgs& g, uint32_t* hist_lds, uint64_t* s_selw,
                                                   bool publish) {
   const FinalizeArgs& a = g.f;
-  __shared__ uint32_t s_scan32[2][kSW];
+  __shared__ uint32_t s_scan32[kGrp][kSW];
   __shared__ uint32_t s_pick[kGrp][3];
   __shared__ uint32_t s_thr[kGrp];
   __shared__ uint32_t s_cutw[kGrp];
@@ -553,13 +557,13 @@ __device__ __forceinline__ void select_thresholds(const FastArgs& g, uint32_t* h
   K2_PROBE(0);
   if (wid == 0) {
     // ---- every workgroup's class counts (tagged words published from registers), the quotas: the
-    // greedy in closed form (selective_propagation.py:93-131), lane l reading workgroup l (G <= 32)
+    // greedy in closed form (selective_propagation.py:93-131), lane l reading workgroup l (G <= 64)
     const uint64_t w = poll_tagged(g.L.head->part, 1, G, g.spin_limit, a.stats);
-    uint64_t cnt = lane < G ? from11(w & ~kTag, 3) : 0ull;
+    uint64_t cnt = lane < G ? from11w(w & ~kTag) : 0ull;
 #pragma unroll
     for (int o = kWave / 2; o > 0; o >>= 1) cnt += __shfl_xor(cnt, o, kWave);
     if (lane == 0) {
-      // In 32-bit integers: N <= S <= 2^15 and bits <= 32, so every product and quotient that can
+      // In 32-bit integers: N <= S <= 2^16 and bits <= 16, so every product and quotient that can
       // decide n fits; the budget U = floor(8·S·ratio) (int64 in the reference) is compared as a
       // double, exact below 2^53 (beyond, every class fits whole).
       const double u8 = 8.0 * ((double)S * a.p.propagation_ratio);
@@ -567,7 +571,7 @@ __device__ __forceinline__ void select_thresholds(const FastArgs& g, uint32_t* h
       int used = 0, kept = 0;
       int md[kGrp];
       for (int k = 2; k >= 0; --k) {
-        const int N = (int)fld(cnt, k), bb = a.p.bits[k];
+        const int N = (int)fldw(cnt, k), bb = a.p.bits[k];
         int n;
         if (a.mode_select == 2) n = N;
         else if (!(u8 >= 0.0)) n = 0;  // U = -1 (selective_propagation.py: nothing fits)
@@ -664,19 +668,18 @@ __device__ __forceinline__ void select_thresholds(const FastArgs& g, uint32_t* h
   K2_PROBE(5);
   if (part) {
     // ---- the bin holding each partial group's threshold: every partial group's bin counts in one
-    // packed scan (16 bits per group: a group's total is at most S <= 32768)
+    // scan (four 32-bit DPP scans, one barrier)
     if (t < kGrp) { s_pick[t][0] = 0u; s_pick[t][1] = 0u; s_pick[t][2] = 0u; }
-    uint64_t pk = 0;
+    uint32_t pk[kGrp], ex[kGrp];
 #pragma unroll
-    for (int q = 0; q < kGrp; ++q)
-      if ((part >> q) & 1) pk |= (uint64_t)(c[q][0] + c[q][1] + c[q][2] + c[q][3]) << (16 * q);
-    const uint64_t ex = block_excl_scan16x4(pk, s_scan32);
+    for (int q = 0; q < kGrp; ++q) pk[q] = ((part >> q) & 1) ? c[q][0] + c[q][1] + c[q][2] + c[q][3] : 0u;
+    block_excl_scan32x4(pk, ex, s_scan32);
     K2_PROBE(6);
 #pragma unroll
     for (int q = 0; q < kGrp; ++q) {
       if (!((part >> q) & 1)) continue;
-      const uint32_t sum = fld(pk, q);
-      int run = (int)fld(ex, q);
+      const uint32_t sum = pk[q];
+      int run = (int)ex[q];
       if (run < need[q] && need[q] <= run + (int)sum) {
         bool found = false;
 #pragma unroll
@@ -797,7 +800,7 @@ __device__ __forceinline__ void compact_phase(const FastArgs& g, float s, int l,
     if (lane == 0 && !(g.withhold == 2 && blk == 0)) st_sc1(&g.L.head->agg[blk], kTag | to11(kept_tot, 3));
     K2_WG(6);
     const uint64_t w0 = poll_tagged(&g.L.head->agg[0], 1, blk, g.spin_limit, a.stats);
-    const uint64_t ps = wave_sum(lane < blk ? from11(w0 & ~kTag, 3) : 0ull);
+    const uint64_t ps = wave_sum(lane < blk ? from11w(w0 & ~kTag) : 0ull);
     if (lane == 0) s_base = ps;
   }
   __syncthreads();
@@ -807,11 +810,32 @@ __device__ __forceinline__ void compact_phase(const FastArgs& g, float s, int l,
   int64_t rb[3];
 #pragma unroll
   for (int q = 0; q < 3; ++q) rb[q] = row_bytes(a, q);
+  if (a.shard_ranges) {
+    // rtkv_shard_ranges in this launch (sequence shards): rank j's first output row / packed byte = the kept
+    // rows before token j·S_local (r3: this workgroup's kept tokens of each class before this thread, kept or
+    // not), and the row's end after the last workgroup's tokens
+    const int64_t Sl = a.shard_S_local;
+    const int G = ((int)a.S + kST - 1) / kST;
+    // (a thread can be both a rank's first token and the row's end writer: thread 0 of the last workgroup)
+    for (int end = 0; end < 2; ++end) {
+      if (end ? !(blk == G - 1 && t == 0) : !(valid && (int64_t)i % Sl == 0)) continue;
+      int64_t nr = 0, nb = 0;
+#pragma unroll
+      for (int q = 0; q < 3; ++q) {
+        const int64_t k = (int64_t)fldw(kept_before, q) + (end ? t3[q] : r3[q]);
+        nr += k;
+        nb += k * rb[q];
+      }
+      const int64_t j = end ? (int64_t)a.shard_nranks : (int64_t)i / Sl;
+      a.shard_ranges[2 * j] = nr;
+      a.shard_ranges[2 * j + 1] = a.row_offset ? nb : 0;
+    }
+  }
   if (valid) {
     a.mask[i] = kept ? 1 : 0;
     if (kept) {
-      const int64_t k0 = (int64_t)r3[0] + fld(kept_before, 0), k1 = (int64_t)r3[1] + fld(kept_before, 1),
-                    k2 = (int64_t)r3[2] + fld(kept_before, 2);
+      const int64_t k0 = (int64_t)r3[0] + fldw(kept_before, 0), k1 = (int64_t)r3[1] + fldw(kept_before, 1),
+                    k2 = (int64_t)r3[2] + fldw(kept_before, 2);
       const int64_t row = k0 + k1 + k2;
       if (row < a.row_capacity) {
         a.kept_index[row] = i;
@@ -907,6 +931,16 @@ __device__ __forceinline__ void amin_amax(const FinalizeArgs& a, float& mn, floa
   mx = -INFINITY;
   if (a.A_part) {
     for (int k = t; k < a.A_nparts; k += kST) { mn = fminf(mn, a.A_part[2 * k]); mx = fmaxf(mx, a.A_part[2 * k + 1]); }
+  } else if ((a.S & 3) == 0 && ((uintptr_t)a.A & 15) == 0) {
+    // the whole row (a gathered A of a sequence-sharded layer, no K1 partials): 16-byte loads, 4 in flight
+    const float4* A4 = reinterpret_cast<const float4*>(a.A);
+    const int n4 = (int)(a.S >> 2);
+#pragma unroll 4
+    for (int k = t; k < n4; k += kST) {
+      const float4 v = A4[k];
+      mn = fminf(mn, fminf(fminf(v.x, v.y), fminf(v.z, v.w)));
+      mx = fmaxf(mx, fmaxf(fmaxf(v.x, v.y), fmaxf(v.z, v.w)));
+    }
   } else {
     for (int k = t; k < (int)a.S; k += kST) { mn = fminf(mn, a.A[k]); mx = fmaxf(mx, a.A[k]); }
   }
@@ -1105,7 +1139,7 @@ __global__ __launch_bounds__(kST) void fsel_quant_kernel(FastArgs g) {
   // ---- the predecessors' counts (wave 0) while the others store the per-token outputs
   if (wid == 0) {
     const uint64_t w = poll_tagged(g.L.head->part, 1, blk, g.spin_limit, a.stats);
-    const uint64_t ps = wave_sum(lane < blk ? from11(w & ~kTag, 3) : 0ull);
+    const uint64_t ps = wave_sum(lane < blk ? from11w(w & ~kTag) : 0ull);
     if (lane == 0) s_base = ps;
   }
   if (valid) {
@@ -1147,8 +1181,20 @@ __global__ __launch_bounds__(kST) void fsel_quant_kernel(FastArgs g) {
   __syncthreads();
   if (lane == 0) s_d[wid] = m2w;
   if (valid && a.row_offset && i < a.row_capacity)
-    a.row_offset[i] = ((int64_t)r3[0] + fld(s_base, 0)) * rb[0] + ((int64_t)r3[1] + fld(s_base, 1)) * rb[1] +
-                      ((int64_t)r3[2] + fld(s_base, 2)) * rb[2];
+    a.row_offset[i] = ((int64_t)r3[0] + fldw(s_base, 0)) * rb[0] + ((int64_t)r3[1] + fldw(s_base, 1)) * rb[1] +
+                      ((int64_t)r3[2] + fldw(s_base, 2)) * rb[2];
+  if (a.shard_ranges) {  // rtkv_shard_ranges in this launch: every token is kept, so rank j's first row is j·S_local
+    const int64_t Sl = a.shard_S_local;
+    for (int end = 0; end < 2; ++end) {  // (thread 0 of the last workgroup may write both entries)
+      if (end ? !(blk == G - 1 && t == 0) : !(valid && (int64_t)i % Sl == 0)) continue;
+      int64_t nb = 0;
+#pragma unroll
+      for (int q = 0; q < 3; ++q) nb += ((int64_t)fldw(s_base, q) + (end ? t3[q] : r3[q])) * rb[q];
+      const int64_t j = end ? (int64_t)a.shard_nranks : (int64_t)i / Sl;
+      a.shard_ranges[2 * j] = end ? (int64_t)S : (int64_t)i;
+      a.shard_ranges[2 * j + 1] = a.row_offset ? nb : 0;
+    }
+  }
   __syncthreads();
   if (wid == 0) {
     double m2 = s_d[lane & (kSW - 1)];
@@ -1167,7 +1213,7 @@ __global__ __launch_bounds__(kST) void fsel_quant_kernel(FastArgs g) {
   if (blk != G - 1 || wid != 0) return;
   // ---- the last workgroup: every workgroup's counts and partials → the layer statistics
   const uint64_t wc = poll_tagged(g.L.head->part, 1, G, g.spin_limit, a.stats);
-  const uint64_t cnt = wave_sum(lane < G ? from11(wc & ~kTag, 3) : 0ull);
+  const uint64_t cnt = wave_sum(lane < G ? from11w(wc & ~kTag) : 0ull);
   (void)poll_tagged(g.L.head->ready, 1, G, g.spin_limit, a.stats);
   double ps = 0.0, pm2 = 0.0;
   uint32_t pmn = 0xffffffffu, pmx = 0u;
@@ -1194,7 +1240,7 @@ __global__ __launch_bounds__(kST) void fsel_quant_kernel(FastArgs g) {
   if (lane == 0) {
     rtkv_layer_stats* hs = a.stats;
     rtkv_batch_stats* bs = reinterpret_cast<rtkv_batch_stats*>(hs + 1);
-    const int64_t ccount[3] = {(int64_t)fld(cnt, 0), (int64_t)fld(cnt, 1), (int64_t)fld(cnt, 2)};
+    const int64_t ccount[3] = {(int64_t)fldw(cnt, 0), (int64_t)fldw(cnt, 1), (int64_t)fldw(cnt, 2)};
     publish_stats(g, false, ssum, pmn, pmx, ccount, ccount, s_line);
     hs->score_m2 = M2;
     bs->kept_score_sum = ssum;

@@ -56,7 +56,7 @@ int launch_select_fast(const FinalizeArgs& f, void* ws, bool zeroed, hipStream_t
     RTKV_HIP_CHECK(hipMemsetAsync(ws, 0, select_fast_zero_bytes(), st));
     RTKV_HIP_CHECK(hipMemsetAsync(f.stats, 0, rtkv_stats_bytes(f.B), st));
   }
-  // All G <= 32 workgroups (1024 threads, 64 KB of LDS: one per CU) are resident at once, which the
+  // All G <= 64 workgroups (1024 threads, 64 KB of LDS: one per CU) are resident at once, which the
   // waits of phases 2 and 3 rely on; a busy GPU only delays the last ones.
   const int G = (int)((f.S + kST - 1) / kST);
   // quantization only (RTKV_NO_SELECTION): scores, classes and row offsets, no selection phases
@@ -64,7 +64,8 @@ int launch_select_fast(const FinalizeArgs& f, void* ws, bool zeroed, hipStream_t
   static const bool quant_full = getenv("RTKV_SELECT_QUANT_FULL") != nullptr;
   if (f.mode_select == 2 && !quant_full) return f.T2 ? launch_fsel_quant<true>(g, G, st) : launch_fsel_quant<false>(g, G, st);
   if (f.S <= 16 * kST) return f.T2 ? launch_fsel_dt<16, true>(g, G, st) : launch_fsel_dt<16, false>(g, G, st);
-  return f.T2 ? launch_fsel_dt<32, true>(g, G, st) : launch_fsel_dt<32, false>(g, G, st);
+  if (f.S <= 32 * kST) return f.T2 ? launch_fsel_dt<32, true>(g, G, st) : launch_fsel_dt<32, false>(g, G, st);
+  return f.T2 ? launch_fsel_dt<64, true>(g, G, st) : launch_fsel_dt<64, false>(g, G, st);
 }
 
 }  // namespace rtkv

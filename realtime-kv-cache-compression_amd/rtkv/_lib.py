@@ -17,7 +17,7 @@ ROOT = os.path.dirname(_PKG_DIR)
 LIB_PATH = os.environ.get("RTKV_LIB", os.path.join(ROOT, "librtkv.so"))
 
 F32, F16, BF16 = 0, 1, 2
-EMIT_DEQUANT, EMIT_PACKED, NO_SELECTION, NO_FALLBACK, SELECT_PIPELINE = 1, 2, 4, 8, 16
+EMIT_DEQUANT, EMIT_PACKED, NO_SELECTION, NO_FALLBACK, SELECT_PIPELINE, FINISH_EXACT = 1, 2, 4, 8, 16, 32
 TEST_WITHHOLD_SELECTION, TEST_WITHHOLD_LOOKBACK = 1 << 16, 1 << 17
 FLAG_F16_QMAX_OVERFLOW, FLAG_SPIN_TIMEOUT, FLAG_OUTPUT_OVERFLOW = 1, 2, 4
 ERR_NAMES = {-1: "RTKV_ERR_INVALID", -2: "RTKV_ERR_UNSUPPORTED", -3: "RTKV_ERR_HIP", -4: "RTKV_ERR_WORKSPACE",
@@ -129,6 +129,16 @@ _SIGS = {
     "rtkv_selfcheck_division_f32": ([c_i64, c_i64, c_i32, c_i32, c_i32, c_p, c_p], c_i32),
     "rtkv_attention_aggregation_shard": ([c_p, c_i32, c_i64, c_i64, c_p, c_p], c_i32),
     "rtkv_finalize_select": ([c_p, c_i32, c_i64, c_i64, c_p, c_p, c_i64, c_i32, c_p, c_sz, c_p], c_i32),
+    "rtkv_attention_aggregation_shard_ws": ([c_p, c_i32, c_i64, c_i64, c_p, c_p, c_p, c_p, c_sz, c_p], c_i32),
+    "rtkv_finalize_select_shard": ([c_p, c_i32, c_i64, c_i64, c_p, c_p, c_i64, c_i32, c_i64, c_i32, c_p, c_i32, c_p,
+                                    c_sz, c_p], c_i32),
+    "rtkv_gq_workspace_size": ([c_i64, c_i64], c_sz),
+    "rtkv_gq_outlier_channels": ([c_p, c_p, c_p, c_p, c_p, c_i64, c_p, c_p, c_sz, c_p], c_i32),
+    "rtkv_gq_pack": ([c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_i64, c_p, c_p, c_i64, c_p], c_i32),
+    "rtkv_gq_unpack": ([c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_i64, c_p, c_p, c_i64, c_i32, c_p, c_p], c_i32),
+    "rtkv_gq_decode_workspace_size": ([c_i64, c_i64], c_sz),
+    "rtkv_gq_decode_attention": ([c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_i64, c_p, c_p, c_i64, c_p, c_i64,
+                                  c_f, c_p, c_p, c_sz, c_p], c_i32),
     "rtkv_quantize_rows_shard": ([c_p, c_i64, c_i64, c_i32, c_i32, c_p, c_p, c_p, c_p, c_p, c_p], c_i32),
     "rtkv_shard_ranges": ([c_p, c_p, c_p, c_i64, c_i64, c_i64, c_i32, c_p, c_p], c_i32),
     "rtkv_importance_qk_lse": ([c_p, c_i32, c_p, c_p], c_i32),

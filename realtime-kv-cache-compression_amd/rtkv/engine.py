@@ -203,10 +203,10 @@ class EarlyStatsBuffer:
         (rtkv_wait_final); past the timeout the device is synchronised and the mirror re-read."""
         rc = self._lib.rtkv_wait_final(self.ptr, seq, self.TIMEOUT_US)
         if rc == L.ERR_TIMEOUT:
+            # a queue slower than the timeout, or a K4 that never published: after a device sync the flags
+            # are either in the mirror or (None) read from the statistics block by the caller
             torch.cuda.synchronize(device)
-            flags = self.final_flags(seq)
-            if flags is not None:
-                return flags
+            return self.final_flags(seq)
         L.check(rc, "rtkv_wait_final")
         return int(self._view.final_word & 0xffff)
 
@@ -539,7 +539,10 @@ class PendingLayer(LayerResult):
         final flags, and return them; a layer without an early buffer syncs its stream instead."""
         if self._early is None or not self.finished:
             return self.final_stats_unchecked().error_flags
-        return self._early.wait_final(self._seq, self.bufs.device)
+        flags = self._early.wait_final(self._seq, self.bufs.device)
+        if flags is None:  # timed out and not in the mirror after the sync: the layer's own statistics block
+            flags = self.final_stats_unchecked().error_flags
+        return flags
 
     def _patch_out(self, kp, vp, pkp, pvp, n):
         out = self._out

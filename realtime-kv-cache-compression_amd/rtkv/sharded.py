@@ -53,11 +53,23 @@ class HipShardStages:
     def _stream(self):
         return L.stream_ptr(self.device)
 
-    def aggregate(self, W, P: int, row0: int, S_total: int, A_out: torch.Tensor):
+    def aggregate(self, W, P: int, row0: int, S_total: int, A_out: torch.Tensor, params=None,
+                  bufs: Optional["ShardBuffers"] = None):
+        """K1 on this rank's W rows.  With the layer's params and buffers it also clears the selection scratch
+        and statistics that finalize_ranges(..., zeroed=True) then uses without its memsets
+        (rtkv_attention_aggregation_shard_ws)."""
         L.require_device(W, A_out)
         wd = attn_desc(W)
-        L.check(L.lib().rtkv_attention_aggregation_shard(ctypes.byref(wd), P, row0, S_total, A_out.data_ptr(),
-                                                          self._stream()), "rtkv_attention_aggregation_shard")
+        if params is None:
+            L.check(L.lib().rtkv_attention_aggregation_shard(ctypes.byref(wd), P, row0, S_total, A_out.data_ptr(),
+                                                              self._stream()), "rtkv_attention_aggregation_shard")
+            return
+        ws = self.ws.get(bufs.B, bufs.S_total)
+        out = bufs.out_struct()
+        L.check(L.lib().rtkv_attention_aggregation_shard_ws(ctypes.byref(wd), P, row0, S_total, A_out.data_ptr(),
+                                                             ctypes.byref(params), ctypes.byref(out), ws.data_ptr(),
+                                                             ws.numel(), self._stream()),
+                "rtkv_attention_aggregation_shard_ws")
 
     def finalize(self, A, a_dtype: int, params, bufs: "ShardBuffers"):
         ws = self.ws.get(bufs.B, bufs.S_total)
@@ -65,6 +77,17 @@ class HipShardStages:
         L.check(L.lib().rtkv_finalize_select(A.data_ptr(), a_dtype, bufs.B, bufs.S_total, ctypes.byref(params),
                                               ctypes.byref(out), bufs.F, L.TORCH_DTYPE_CODE[bufs.dtype],
                                               ws.data_ptr(), ws.numel(), self._stream()), "rtkv_finalize_select")
+
+    def finalize_ranges(self, A, a_dtype: int, params, bufs: "ShardBuffers", world: int, zeroed: bool = False):
+        """finalize + ranges in one call (rtkv_finalize_select_shard): the one-launch selection writes the rank
+        table itself; zeroed: the layer's aggregate(..., params, bufs) cleared the scratch."""
+        ws = self.ws.get(bufs.B, bufs.S_total)
+        out = bufs.out_struct()
+        L.check(L.lib().rtkv_finalize_select_shard(A.data_ptr(), a_dtype, bufs.B, bufs.S_total, ctypes.byref(params),
+                                                    ctypes.byref(out), bufs.F, L.TORCH_DTYPE_CODE[bufs.dtype],
+                                                    bufs.S_local, world, bufs.ranges.data_ptr(), int(bool(zeroed)),
+                                                    ws.data_ptr(), ws.numel(), self._stream()),
+                "rtkv_finalize_select_shard")
 
     def ranges(self, bufs: "ShardBuffers", world: int):
         L.check(L.lib().rtkv_shard_ranges(bufs.g.kept_index.data_ptr(), L.ptr(bufs.g.row_offset),
@@ -222,8 +245,13 @@ class ShardedPrefillCompressor:
         p = params if params is not None else self.params(layer_idx, S_total)
         bufs = self.buffers(layer_idx, B, S_local, F, K.dtype)
         A_local = self._A_buffers(B, S_local)[0]
-        self.stages.aggregate(W, P, row0, S_total, A_local)
-        return self._select_and_quantize(K, V, layout, layer_idx, p, bufs, L.TORCH_DTYPE_CODE[W.dtype])
+        # stages with the fused finalize + ranges: K1 also clears the layer's selection scratch (no memsets)
+        zeroed = hasattr(self.stages, "finalize_ranges")
+        if zeroed:
+            self.stages.aggregate(W, P, row0, S_total, A_local, params=p, bufs=bufs)
+        else:
+            self.stages.aggregate(W, P, row0, S_total, A_local)
+        return self._select_and_quantize(K, V, layout, layer_idx, p, bufs, L.TORCH_DTYPE_CODE[W.dtype], zeroed)
 
     def enqueue_layer_qk(self, K, V, Q, lse, layer_idx: int, layout: str = "bsf", params=None,
                          causal: bool = True) -> ShardBuffers:
@@ -250,7 +278,9 @@ class ShardedPrefillCompressor:
             kp = self._prompt_keys[(B, P, F, K.dtype)] = torch.empty(B, P, F, dtype=K.dtype, device=self.device)
         if self.rank == 0:
             kp.copy_(K[:, :P])
-        if self._host:
+        if self.world == 1:
+            pass  # the prompt keys are this rank's own
+        elif self._host:
             kh = kp.cpu()
             dist.broadcast(kh, src=self._peer_rank(0), group=self.group)
             kp.copy_(kh)
@@ -272,6 +302,8 @@ class ShardedPrefillCompressor:
         """Step 2: the all-gather of every rank's A [B, S_local] into token order [B, S_total]."""
         S_total = S_local * self.world
         A_local, A_parts, A = self._A_buffers(B, S_local)
+        if self.world == 1:
+            return A_local  # one rank: its A is the whole row, nothing to gather
         if self.comm is not None:
             self.comm.allgather_rows(A_local, A)  # straight into token order, any B
             return A
@@ -286,20 +318,24 @@ class ShardedPrefillCompressor:
         A.copy_(A_parts.permute(1, 0, 2).reshape(B, S_total))
         return A
 
-    def _select_and_quantize(self, K, V, layout: str, layer_idx: int, p, bufs: ShardBuffers, a_dtype: int):
+    def _select_and_quantize(self, K, V, layout: str, layer_idx: int, p, bufs: ShardBuffers, a_dtype: int,
+                             zeroed: bool = False):
         """Steps 2-5 of a layer once this rank's A is computed: all-gather, global selection, bounds,
         local quantization, and the (overlapped) exchange bookkeeping."""
         B, S_local = bufs.B, bufs.S_local
-        S_total = S_local * self.world
         row0 = self.rank * S_local
         A_glob = self.gather_A(B, S_local)
-        self.stages.finalize(A_glob, a_dtype, p, bufs)
-        self.stages.ranges(bufs, self.world)
+        fr = getattr(self.stages, "finalize_ranges", None)
+        if fr is not None:  # one launch: the selection writes the rank table (B = 1, S_total <= 65536)
+            fr(A_glob, a_dtype, p, bufs, self.world, zeroed=zeroed)
+        else:
+            self.stages.finalize(A_glob, a_dtype, p, bufs)
+            self.stages.ranges(bufs, self.world)
         self.stages.quantize(K, V, layout, row0, self.rank, self.world, p, bufs)
-        if self.overlap:
+        if self.overlap and self.world > 1:
             self._queue(layer_idx, bufs)
             self._issue(keep=self.lag)
-        else:
+        else:  # (one rank: nothing to exchange; the host views are made at exchange())
             self._pending.append(layer_idx)
         return bufs
 
@@ -392,14 +428,9 @@ class ShardedPrefillCompressor:
             if self._xstream is not None:
                 torch.cuda.current_stream(self.device).wait_stream(self._xstream)
             out, self._issued, self._works = self._issued, [], []
-            return out
-        layers = list(self._pending)
-        self._pending = []
-        if not layers:
-            return []
-        host = torch.stack([self._bufs[l].ranges for l in layers]).cpu()  # the single sync
-        out = [ShardLayer(l, self._bufs[l], host[k]) for k, l in enumerate(layers)]
-        if self.world == 1 or not self.emit_packed or not transfer:
+            return out + self._pending_views()  # (one rank: its layers were never queued)
+        out = self._pending_views()
+        if not out or self.world == 1 or not self.emit_packed or not transfer:
             return out
         if self.xcomm is not None:
             for sl in out:
@@ -412,6 +443,15 @@ class ShardedPrefillCompressor:
         for w in works:
             w.wait()
         return out
+
+    def _pending_views(self) -> List[ShardLayer]:
+        """Host views of the layers enqueued without an overlapped exchange: one host read of every layer's
+        rank bounds (the single sync)."""
+        layers, self._pending = list(self._pending), []
+        if not layers:
+            return []
+        host = torch.stack([self._bufs[l].ranges for l in layers]).cpu()
+        return [ShardLayer(l, self._bufs[l], host[k]) for k, l in enumerate(layers)]
 
     # ------------------------------------------------------------------ reference-named entry point
     def compress_layer_kv_cache(self, key_states, value_states, attention_weights, input_ids, layer_idx):

@@ -134,7 +134,7 @@ class RealTimePrefillCompressor:
         LSE (rtkv_compress_layer_qk) — within tolerance of the W path, not bit-exact.
         key_padding_bias [B,S] (fp32, 0 real key / -inf padding key): the key-padding part of the
         model's attention_mask in that mode (the same bias the lse was computed with)."""
-        start_time = time.time()
+        start_time = time.perf_counter()  # unified_compressor.py:118 (time.time(); a monotonic clock here)
         fused = attention_weights is None
         if fused and (query_states is None or attention_lse is None):
             raise ValueError("attention_weights=None needs query_states and attention_lse (fused importance mode)")
@@ -158,7 +158,9 @@ class RealTimePrefillCompressor:
             if K.dtype == torch.float16 and any((1 << b) - 1 > 65504 for b in bits):
                 emit_packed = False
             self._packable[(K.dtype, bits, self.emit_packed)] = emit_packed
-        flags = L.EMIT_DEQUANT | (L.EMIT_PACKED if emit_packed else 0) | self._test_flags
+        # FINISH_EXACT: K4 raises (OUTPUT_OVERFLOW) unless the outputs are exactly the size the device's own
+        # statistics give, so a torn or stale read of the early line can never return unwritten rows
+        flags = L.EMIT_DEQUANT | (L.EMIT_PACKED if emit_packed else 0) | L.FINISH_EXACT | self._test_flags
         params = params_from_config(self.config, layer_idx, P, ratio, flags)
         # per-token buffers only: K'/V' and the packed codes are allocated at their exact sizes once S' is
         # known (rtkv_compress_layer_begin / _finish), so a layer retains 2·S'·F elements + its codes
@@ -235,18 +237,16 @@ class RealTimePrefillCompressor:
         def std_score():
             m2 = res.final_stats().score_m2
             return (m2 / (n - 1)) ** 0.5 if n > 1 else float("nan")
-        host_time = time.time() - start_time
-        # processing_time: the layer's device time, K1's first block start to K4's last workgroup end (the
-        # GPU's real-time counter, stamped by the kernels: rtkv_layer_times; read, with its wait, on first
-        # access — no events on the stream: a timing event before K1 cost ~4.6 µs of device idle per
-        # layer, profiles/r04i_*).  The reference's is the host wall time of its synchronous
-        # call (unified_compressor.py:118,148), which on the device path is exactly that span plus its
-        # Python overhead; the device span is what this call costs the caller's stream.  host_return_time:
-        # when this call returned (K4 still running).
+        # processing_time is the reference's quantity (unified_compressor.py:118,148): the caller-visible wall
+        # time of this call, entry to return, so Σ processing_time is LongBench's TTFT (longbench_eval.py:160).
+        # The call returns once the layer's outputs are enqueued (strict: once K4 has started), so the last
+        # layer's K4 tail is the only device time outside the sum.  device_processing_time (extension): the
+        # layer's device span, K1's first block to K4's last row on the GPU's real-time counter
+        # (rtkv_layer_times, stamped by the kernels: no event on the stream), read with its wait on access.
         compression_info = _LazyDict({
             "layer_idx": layer_idx,
-            "processing_time": _Lazy(res.device_seconds),
-            "host_return_time": host_time,
+            "processing_time": None,  # set at the return below
+            "device_processing_time": _Lazy(res.device_seconds),
             "original_shape": key_states.shape,
             "compressed_shape": selected_keys.shape,
             "compression_ratio": compression_ratio,
@@ -274,6 +274,7 @@ class RealTimePrefillCompressor:
             })
         res.k_out = res.v_out = None  # the caller owns K'/V'; nothing kept here pins them
         self.layer_states[layer_idx] = compression_info
+        compression_info["processing_time"] = time.perf_counter() - start_time
         return selected_keys, selected_values, compression_info
 
     def _verify_previous(self, device):

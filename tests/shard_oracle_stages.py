@@ -54,7 +54,7 @@ class OracleShardStages:
         A_out.copy_(torch.from_numpy(qk_mass(Q.float().numpy(), K_prompt.float().numpy(), lse.float().numpy(), P,
                                              row0, causal)))
 
-    def aggregate(self, W, P, row0, S_total, A_out):
+    def aggregate(self, W, P, row0, S_total, A_out, params=None, bufs=None):
         A_out.copy_(torch.from_numpy(orc.attention_aggregation(storage(W), _CODE[W.dtype], P)))
 
     def finalize(self, A, a_dtype, params, bufs):

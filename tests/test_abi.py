@@ -87,3 +87,16 @@ def test_no_gpu_means_loud_failure():
     K = torch.zeros(1, 8, 16)
     with pytest.raises(RuntimeError, match="ROCm"):
         comp.compress_layer_kv_cache(K, K, torch.zeros(1, 2, 8, 8), torch.zeros(1, 8, dtype=torch.long), 0)
+
+
+def test_early_line_must_be_128_byte_aligned(lib):
+    """The early statistics line is one 128-byte store checked by its first and last words: a buffer that
+    straddles two lines is refused by every entry point that takes it (host-only calls here)."""
+    buf = ctypes.create_string_buffer(1024)
+    base = (ctypes.addressof(buf) + 127) // 128 * 128
+    lib.rtkv_wait_early.restype = ctypes.c_int
+    assert lib.rtkv_wait_early(ctypes.c_void_p(base + 8), ctypes.c_uint64(1), ctypes.c_int64(0)) == -1
+    assert "128-byte aligned" in lib.rtkv_last_error().decode()
+    assert lib.rtkv_wait_final(ctypes.c_void_p(base + 64), ctypes.c_uint64(1), ctypes.c_int64(0)) == -1
+    # aligned: a plain timeout (nothing published)
+    assert lib.rtkv_wait_early(ctypes.c_void_p(base), ctypes.c_uint64(1), ctypes.c_int64(0)) == -5

@@ -31,7 +31,8 @@ CASES = [  # dtype, B, S, H, D, ratio, expect: "complete" | "fallback" | "unpubl
     ("bfloat16", 1, 777, 4, 64, 0.4, "complete"),
     ("float16", 1, 2000, 4, 32, 0.0001, "fallback"),    # U = 1 bit: nothing fits, the top-10% fallback
     ("float16", 2, 1024, 4, 32, 0.6, "unpublished"),    # B > 1: the pipeline K2
-    ("float16", 1, 40000, 4, 32, 0.6, "unpublished"),   # S > 32768: the pipeline K2
+    ("float16", 1, 40000, 4, 32, 0.6, "complete"),      # 64 tokens per thread: the one-launch K2 up to S = 65536
+    ("float16", 1, 70000, 4, 32, 0.6, "unpublished"),   # S > 65536: the pipeline K2
     ("float32", 1, 16384, 32, 128, 1.0, "quant"),       # RTKV_NO_SELECTION: the quantization-only K2
     ("bfloat16", 1, 3001, 4, 64, 1.0, "quant"),
 ]
@@ -365,3 +366,43 @@ def test_prefetch_and_start_event_leave_the_outputs_unchanged():
     end.record()
     end.synchronize()
     assert ev.elapsed_time(end) > 0 and 0 < res.device_seconds() < ev.elapsed_time(end) / 1e3 + 1e-5
+
+
+def test_finish_exact_rejects_oversized_outputs():
+    """RTKV_FINISH_EXACT (the drop-in's flag): buffers LARGER than the device statistics give — what a
+    torn or stale read of the early line would produce (an S' or byte count from another layer) — are
+    flagged RTKV_FLAG_OUTPUT_OVERFLOW and nothing is written; the exact sizes pass (advisor, round 5)."""
+    import ctypes
+    import rtkv
+    from rtkv import _lib as L
+    from rtkv.engine import EarlyStatsBuffer, compress_layer_begin
+    S, F, P, cfg, Kd, Vd, Wd = _lookback_inputs()
+    p = rtkv.params_from_config(cfg, 0, P, 0.6, L.EMIT_DEQUANT | L.EMIT_PACKED | L.FINISH_EXACT)
+    for case in ("exact", "rows", "bytes"):
+        ws, early = rtkv.Workspace("cuda"), EarlyStatsBuffer()
+        bufs = rtkv.LayerBuffers(1, S, F, Kd.dtype, "cuda", (2, 4, 8), outputs=False)
+        res = compress_layer_begin(Kd, Vd, Wd, p, bufs, ws, early)
+        st = res.stats()
+        n, nb = st.max_kept, st.total_packed_bytes
+        rows = n + 1 if case == "rows" else n
+        cap = (nb + 255) // 256 * 256 + (256 if case == "bytes" else 0)
+        kv = torch.full((2, 1, n + 1, F), 7.0, dtype=Kd.dtype, device="cuda")
+        codes = torch.full((2, cap), 0xAB, dtype=torch.uint8, device="cuda")
+        out = res._out
+        out.k_out_dev, out.v_out_dev = kv[0].data_ptr(), kv[1].data_ptr()
+        out.packed_k_dev, out.packed_v_dev = codes[0].data_ptr(), codes[1].data_ptr()
+        out.packed_capacity = cap
+        L.check(L.lib().rtkv_compress_layer_finish(ctypes.byref(res._kd), ctypes.byref(p), ctypes.byref(out), rows,
+                                                   ws.buf.data_ptr(), ws.buf.numel(), L.stream_ptr(Kd.device),
+                                                   early.ptr, res._seq), "finish")
+        ws.pending = None
+        torch.cuda.synchronize()
+        if case == "exact":
+            assert early.final_flags(res._seq) == 0
+            assert not bool((kv[:, :, :n] == 7.0).all())
+            res.final_stats()
+        else:
+            assert early.final_flags(res._seq) & L.FLAG_OUTPUT_OVERFLOW
+            assert bool((kv == 7.0).all()) and bool((codes == 0xAB).all())
+            with pytest.raises(RuntimeError, match="RTKV_FLAG_OUTPUT_OVERFLOW"):
+                res.final_stats()

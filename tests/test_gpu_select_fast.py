@@ -1,11 +1,11 @@
-"""GPU: the two-launch selection (select_fast.hip, taken for B = 1 and S <= 32768) against the
+"""GPU: the one-launch selection (select_fast.hip, taken for B = 1 and S <= 65536) against the
 multi-workgroup pipeline (select.hip, forced with RTKV_SELECT_PIPELINE) and against the oracle.
 
 Both paths must agree byte for byte on scores, classes, mask, kept indices, row offsets, packed
 codes, scale/zero-point and the dequantized rows, and exactly on every integer statistic; the
 double sums (score_sum, score_m2, kept_score_sum) agree to 1e-12 relative (different summation
 trees).  Cases cover the row-length edges of the 1024-token workgroups (S = 1, 2, 17,
-4097, 16383..16385, 32768), the emergency fallback, quantization-only, heavy score ties (β = 0
+4097, 16383..16385, 32768, 40000, 65536), the emergency fallback, quantization-only, heavy score ties (β = 0
 and a 3-valued attention mass) and all three dtypes."""
 import numpy as np
 import pytest
@@ -84,6 +84,14 @@ CASES = [
     # heavy ties in the 32-tokens-per-thread rescan (16384 < S <= 32768): the tie cutoff index
     (24576, "float32", 0.4, dict(beta=0.0), "tie"),
     (32768, "bfloat16", 0.6, dict(beta=0.0), "const"),
+    # 64 tokens per thread (32768 < S <= 65536: 33..64 workgroups; the north star's S = 64k and the sharded
+    # prefill's replicated global selection), incl. heavy ties and class counts of exactly 65536
+    (40000, "float16", 0.6, {}, "rand"),
+    (65536, "float32", 0.6, {}, "rand"),
+    (65535, "bfloat16", 0.4, {}, "rand"),
+    (49153, "float16", 0.4, dict(beta=0.0), "tie"),
+    (65536, "bfloat16", 0.6, dict(beta=0.0), "const"),
+    (65536, "float16", 0.0002, {}, "rand"),      # emergency fallback over 65536 tokens
 ]
 
 
@@ -133,6 +141,7 @@ def test_single_matches_pipeline_and_oracle(S, dtype, ratio, over, kind):
 @pytest.mark.parametrize("S,dtype,over", [(8192, "float16", {}), (1, "float32", {}), (17, "bfloat16", {}),
                                           (1024, "float16", {}), (1025, "float32", {}), (4096, "float32", {}),
                                           (16385, "bfloat16", {}), (32768, "float16", {}),
+                                          (65536, "float32", {}), (50001, "float16", {}),
                                           (4096, "float32", dict(low_precision_bits=4, medium_precision_bits=8,
                                                                  high_precision_bits=16)),
                                           (5000, "float16", dict(beta=0.0))])

@@ -32,9 +32,18 @@ def _dev(a, dtype):
     ("bfloat16", 3000, 3, 8, 64, 0.8),     # P = 128, S_total*P not a multiple of 32 per shard boundary
     ("float32", 1500, 5, 4, 64, 0.3),
     ("float16", 640, 8, 4, 32, 0.05),      # tiny budget: the top-10% fallback across shards
-    ("float16", 32768, 2, 8, 64, 0.5),     # S_total above the single-workgroup K2 limit
+    ("float16", 32768, 2, 8, 64, 0.5),
+    ("float32", 65536, 4, 4, 128, 0.4),     # the one-launch K2 at its 64-workgroup limit
+    ("float16", 81920, 8, 4, 64, 0.6),      # S_total above it: the pipeline K2 + the ranges kernel
+    ("bfloat16", 8192, 4, 8, 64, -1.0),     # quantization only (RTKV_NO_SELECTION): the quant-only K2
+    ("float16", 640, 1, 4, 32, 0.3),        # one rank
 ])
-def test_shards_union_equals_single_gpu(dtype, S_total, world, H, D, ratio):
+@pytest.mark.parametrize("fused", [False, True], ids=["separate", "fused"])
+def test_shards_union_equals_single_gpu(dtype, S_total, world, H, D, ratio, fused):
+    """The union of N simulated ranks equals the single-GPU layer byte for byte.  separate: the stage calls
+    one by one (K1, finalize, ranges, K4); fused: the driver's calls — K1 that also clears the layer's
+    selection scratch (rtkv_attention_aggregation_shard_ws), finalize + rank table in one call
+    (rtkv_finalize_select_shard, scratch_zeroed = 1), then the split-row K4 over the rank's own rows."""
     import rtkv
     from rtkv import _lib as L
     from rtkv.sharded import HipShardStages, ShardBuffers
@@ -46,8 +55,8 @@ def test_shards_union_equals_single_gpu(dtype, S_total, world, H, D, ratio):
     cfg = rtkv.CompressionConfig(alpha=0.8, beta=0.1, gamma=0.1, theta_h=0.4, theta_m=0.25, num_hidden_layers=1,
                                  layer_weights=[1.0], high_precision_bits=8, medium_precision_bits=4,
                                  low_precision_bits=2)
-    flags = L.EMIT_DEQUANT | L.EMIT_PACKED
-    params = rtkv.params_from_config(cfg, 0, P, ratio, flags)
+    flags = L.EMIT_DEQUANT | L.EMIT_PACKED | (L.NO_SELECTION if ratio < 0 else 0)
+    params = rtkv.params_from_config(cfg, 0, P, abs(ratio), flags)
     bits = (2, 4, 8)
     # single GPU reference run
     ref = rtkv.LayerBuffers(1, S_total, F, Kd.dtype, "cuda", bits)
@@ -66,9 +75,14 @@ def test_shards_union_equals_single_gpu(dtype, S_total, world, H, D, ratio):
         stages.aggregate(Wd[:, :, sl], P, j * S_local, S_total, A[:, sl])
     bufs = [ShardBuffers(1, S_local, world, F, Kd.dtype, "cuda", bits) for _ in range(world)]
     for j in range(world):
-        stages.finalize(A, L.TORCH_DTYPE_CODE[Wd.dtype], params, bufs[j])
-        stages.ranges(bufs[j], world)
         sl = slice(j * S_local, (j + 1) * S_local)
+        if fused:  # rank j's K1 again (the same A rows), now clearing the scratch its finalize uses
+            bufs[j].g.stats.fill_(0x5A)  # must be cleared by the K1 call
+            stages.aggregate(Wd[:, :, sl], P, j * S_local, S_total, A[:, sl], params=params, bufs=bufs[j])
+            stages.finalize_ranges(A, L.TORCH_DTYPE_CODE[Wd.dtype], params, bufs[j], world, zeroed=True)
+        else:
+            stages.finalize(A, L.TORCH_DTYPE_CODE[Wd.dtype], params, bufs[j])
+            stages.ranges(bufs[j], world)
         stages.quantize(Kd[:, sl].contiguous(), Vd[:, sl].contiguous(), "bsf", j * S_local, j, world, params, bufs[j])
     torch.cuda.synchronize()
     n = st.max_kept
@@ -229,7 +243,7 @@ def test_rtkv_collectives_single_rank():
 ])
 def test_shards_union_equals_single_gpu_at_config_size(name, dtype, S_total, world, H, D, ratio):
     """The 8-way sequence-shard split at BASELINE's multi-GPU sizes (inputs generated on the device):
-    S_total = 65536 takes the pipeline selection in rtkv_finalize_select (S > 32768) on every rank, and
+    S_total = 65536 takes the one-launch selection in rtkv_finalize_select (64 workgroups) on every rank, and
     rtkv_shard_ranges / rtkv_quantize_rows_shard split it 8 ways; the union equals the single-GPU
     rtkv_compress_layer byte for byte."""
     import rtkv
