@@ -232,6 +232,8 @@ __global__ __launch_bounds__(256) void gq_pack_kernel(GqArgs a) {
       if ((lane & 15) == 0) {
         static_cast<S_*>(a.meta)[mrow * 2] = Dt<DT>::store(rp.scale);
         static_cast<S_*>(a.meta)[mrow * 2 + 1] = Dt<DT>::store(rp.zp);
+        for (int s = 0; s < a.n_out; ++s)  // unused outlier slots of the head hold zero
+          if (a.idx[((int64_t)t * H + h) * a.n_out + s] < 0) store_bits<DT>(a.raw, mrow * a.n_out + s, 0u);
       }
       uint32_t q[8];
 #pragma unroll

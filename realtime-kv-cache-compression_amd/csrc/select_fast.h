@@ -46,7 +46,7 @@
 #ifdef RTKV_SELECT_PROBE  // diagnostic build (tools/k2_probe.hip): phase timestamps (s_memrealtime, 100 MHz)
 __device__ unsigned long long g_k2_probe[16];   // the selecting workgroup's phases
 __device__ unsigned long long g_k2_clock[16];
-__device__ unsigned long long g_k2_wg[32][10];  // per workgroup phase timestamps
+__device__ unsigned long long g_k2_wg[64][10];  // per workgroup phase timestamps (G <= 64)
 __device__ int g_k2_rep;  // the probe's second pass over phase 2 (warm instruction cache) records at k + 8
 #define K2_PROBE(k) do { if (threadIdx.x == 0 && blockIdx.x == (unsigned)((g.f.S + kST - 1) / kST - 1)) { g_k2_probe[(k) + 8 * g_k2_rep] = __builtin_amdgcn_s_memrealtime(); g_k2_clock[(k) + 8 * g_k2_rep] = __builtin_amdgcn_s_memtime(); } } while (0)
 #define K2_WG(k) do { if (threadIdx.x == 0) g_k2_wg[blockIdx.x][k] = __builtin_amdgcn_s_memrealtime(); } while (0)

@@ -9,6 +9,7 @@ from .base_config import CompressionConfig
 from .compression_layers import (AdaptiveQuantization, CompressedKVCache, decode_attention, load_packed, save_packed,
                                  unpack_layer)
 from .dynamic_quantization import DynamicPrecisionQuantizer
+from .group_quant import GroupQuantConfig, GroupQuantKVCache, gq_compress
 from .engine import (LayerBuffers, LayerResult, Workspace, attention_lse, compress_layer, compress_layer_qk,
                      importance_qk_lse, params_from_config, prompt_length)
 from .model_side import CompressedPrefillAttention
@@ -22,7 +23,7 @@ __all__ = [
     "SelectiveTokenPropagator", "CompressedKVCache", "AdaptiveQuantization", "unpack_layer", "decode_attention",
     "save_packed", "load_packed", "CompressedPrefillAttention",
     "LayerBuffers", "LayerResult", "Workspace", "compress_layer", "compress_layer_qk", "importance_qk_lse", "attention_lse",
-    "params_from_config", "prompt_length",
+    "params_from_config", "prompt_length", "GroupQuantConfig", "GroupQuantKVCache", "gq_compress",
 ]
 
 __version__ = "0.1.0"

@@ -262,10 +262,11 @@ class LayerBuffers:
     the tensor views (a few µs of host time each) are made on first access."""
 
     def __init__(self, B: int, S: int, F: int, dtype: torch.dtype, device, bits, emit_dequant=True, emit_packed=True,
-                 outputs: bool = True):
+                 outputs: bool = True, row_offsets: bool = False):
         """outputs=False: only the per-token buffers (scores, classes, mask, kept indices, row offsets,
         scale/zero-points, statistics); the caller supplies exactly-sized K'/V' and packed buffers to
-        finish() (rtkv_compress_layer_begin / _finish)."""
+        finish() (rtkv_compress_layer_begin / _finish).  row_offsets: the kept rows' code offsets even
+        without packed codes (the group-wise extension uses the per-token row slots)."""
         self.B, self.S, self.F, self.dtype = B, S, F, dtype
         self.emit_dequant, self.emit_packed = emit_dequant, emit_packed
         dev = self.device = torch.device(device)
@@ -279,10 +280,10 @@ class LayerBuffers:
                 ("stats", L.stats_bytes(B), torch.uint8, (L.stats_bytes(B),))]
         if emit_dequant and outputs:
             plan += [("k_out", B * S * F * esz, dtype, (B * S * F,)), ("v_out", B * S * F * esz, dtype, (B * S * F,))]
-        if emit_packed:
-            if outputs:
-                plan += [("packed_k", max(cap, 1), torch.uint8, (max(cap, 1),)),
-                         ("packed_v", max(cap, 1), torch.uint8, (max(cap, 1),))]
+        if emit_packed and outputs:
+            plan += [("packed_k", max(cap, 1), torch.uint8, (max(cap, 1),)),
+                     ("packed_v", max(cap, 1), torch.uint8, (max(cap, 1),))]
+        if emit_packed or row_offsets:
             plan += [("row_offset", B * S * 8, torch.int64, (B, S)), ("scale_zp", B * S * 16, torch.float32, (B, S, 4))]
         offs, total = {}, 0
         for name, n, dt, shape in plan:

@@ -75,14 +75,21 @@ class _LazyDict(dict):
 class RealTimePrefillCompressor:
     """Prompt-guided importance → dynamic precision → selective propagation, per layer."""
 
-    def __init__(self, config, model_config=None, emit_packed: bool = True, strict: Optional[bool] = None):
+    def __init__(self, config, model_config=None, emit_packed: bool = True, strict: Optional[bool] = None,
+                 group_quant=None):
         """strict (extension): wait in each call until the layer's K4 has published the final flags
         (rtkv_wait_final: K2's end, no stream sync) and raise in THAT call when its selection failed after
         the early statistics — the reference's synchronous call fails in the failing layer, where the
         caller's try/except falls back for that layer (modified_llama.py:144-149).  strict=False returns
         on the early statistics and reports such a layer at the next call on the device, in
         get_overall_compression_stats, reset_compression_state or verify_pending_layers.  Default:
-        RTKV_STRICT (1 unless set to 0)."""
+        RTKV_STRICT (1 unless set to 0).
+
+        group_quant (extension, default None = off): a rtkv.GroupQuantConfig; each layer's info then also
+        holds ``group_quant``, a GroupQuantKVCache of the same kept rows with per-head group-wise codes and
+        the layer's per-channel outliers kept exactly (rtkv-gq/1, no reference counterpart: the returned
+        K'/V' stay the reference's).  Layers outside its envelope (B > 1, head_dim != 128, widths other
+        than 2/4/8) are compressed as usual without it."""
         self.config = config
         self.model_config = model_config
         self.importance_tracker = LayerWiseImportanceTracker(config)
@@ -107,6 +114,7 @@ class RealTimePrefillCompressor:
         self.prefetch_bytes = int(float(os.environ.get("RTKV_DROPIN_PREFETCH_MB", "24")) * (1 << 20))
         self._packable: Dict[tuple, bool] = {}  # (dtype, bits, emit_packed) → whether the codes are emitted
         self.strict = (os.environ.get("RTKV_STRICT", "1") != "0") if strict is None else bool(strict)
+        self.group_quant = group_quant
 
     # ------------------------------------------------------------------ reference API
     def identify_prompt_tokens(self, input_ids: torch.Tensor, special_tokens: Optional[List[int]] = None):
@@ -164,7 +172,10 @@ class RealTimePrefillCompressor:
         params = params_from_config(self.config, layer_idx, P, ratio, flags)
         # per-token buffers only: K'/V' and the packed codes are allocated at their exact sizes once S' is
         # known (rtkv_compress_layer_begin / _finish), so a layer retains 2·S'·F elements + its codes
-        bufs = LayerBuffers(B, S, F, K.dtype, K.device, bits, emit_dequant=True, emit_packed=emit_packed, outputs=False)
+        gq = self.group_quant is not None and B == 1 and F % 512 == 0 and F // 128 <= 64 and \
+            all(b in (2, 4, 8) for b in bits) and K.stride(1) == F
+        bufs = LayerBuffers(B, S, F, K.dtype, K.device, bits, emit_dequant=True, emit_packed=emit_packed, outputs=False,
+                            row_offsets=gq)
         ws = self._workspaces.get(K.device)
         if ws is None:
             ws = self._workspaces[K.device] = Workspace(K.device)
@@ -272,6 +283,11 @@ class RealTimePrefillCompressor:
                 "dtype": K.dtype,
                 "feature_dim": F,
             })
+        if gq:  # the extension's group-wise pack of the same kept rows, stream-ordered after the layer
+            from .group_quant import gq_compress
+            compression_info["group_quant"] = gq_compress(
+                K, V, bufs.kept_index[0], bufs.labels[0], bufs.row_offset[0], bufs.stats, Sp, st.total_packed_bytes,
+                bits, self.group_quant)
         res.k_out = res.v_out = None  # the caller owns K'/V'; nothing kept here pins them
         self.layer_states[layer_idx] = compression_info
         compression_info["processing_time"] = time.perf_counter() - start_time

@@ -304,6 +304,9 @@ LAYER_CASES = [
     ("cfg3_b16_l25", PUB16, 32, 25, 1, 32, 32, 128, 16384, "float32"),
     ("cfg3_b16_l12", PUB16, 32, 12, 1, 32, 32, 128, 16384, "bfloat16"),
     ("cfg4_s65536_b16_l20", PUB16, 32, 20, 1, 32, 32, 128, 65536, "float32"),
+    # round 6: BASELINE cfg2 (7B, S = 4096, quantization only) in the reference model's fp32, the launch the
+    # bench's cfg2_s4096_quant leg times (rtkv_compress_layer with RTKV_NO_SELECTION)
+    ("cfg2_quant", COVERAGE, 32, 0, 1, 32, 32, 128, 4096, "float32"),
 ]
 
 

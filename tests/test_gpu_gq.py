@@ -1,0 +1,192 @@
+"""GPU: the rtkv-gq/1 extension (per-channel outlier detection + per-head group-wise pack; include/rtkv.h
+rtkv_gq_*, csrc/outlier.hip) against its definition, oracle/rtkv_oracle.c rtkvo_gq_*.
+
+There is NO reference counterpart (the reference keeps one scale/zero-point per token over all H·D channels,
+dynamic_quantization.py:181-194), so parity is UNPINNED: the oracle defines the mode and these tests check
+the kernels against it byte for byte — outlier channel lists, packed codes, per-head scale/zero-points, raw
+outlier values, the unpacked rows — and decode attention over the format against torch fp32 within a
+stated tolerance.  The mode is opt-in: the drop-in's K'/V' with it on equal the default's byte for byte.
+The reconstruction-error comparison against the per-token scheme runs at BASELINE config 5's shape (13B:
+40 KV heads of 128, S = 32768) with per-channel key outliers injected."""
+import math
+
+import numpy as np
+import pytest
+import torch
+
+import rtkv_oracle as orc
+import synth
+
+pytestmark = pytest.mark.gpu
+
+TD = {"float32": torch.float32, "float16": torch.float16, "bfloat16": torch.bfloat16}
+ODT = {"float32": orc.F32, "float16": orc.F16, "bfloat16": orc.BF16}
+
+
+@pytest.fixture(scope="module", autouse=True)
+def gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no ROCm device")
+
+
+def _dev(a, dtype):
+    if dtype == "float32":
+        return torch.from_numpy(np.ascontiguousarray(a, np.float32)).cuda()
+    return torch.from_numpy(np.ascontiguousarray(a, np.uint16).view(np.int16)).cuda().view(TD[dtype])
+
+
+def _host(t):
+    t = t.detach().cpu()
+    return t.numpy() if t.dtype == torch.float32 else t.view(torch.int16).numpy().view(np.uint16)
+
+
+def _inputs(seed, S, H, dtype, outlier_ch=(3, 77, 130, 300), gain=25.0):
+    """K/V rows [1, S, H*128] with a few per-channel outliers (KV-cache keys have fixed large channels)."""
+    F = H * 128
+    K, V = synth.kv(seed, 1, S, F, "float32")
+    K, V = K.copy(), V.copy()
+    for c in outlier_ch:
+        if c < F:
+            K[..., c] *= gain
+            V[..., (c * 7) % F] *= gain / 5
+    W = synth.attention_slice(seed, 1, 8, S, min(S // 5, 128) or 1, "float32")
+    return synth.cast(K, dtype), synth.cast(V, dtype), synth.cast(W, dtype)
+
+
+def _layer(K, V, W, dtype, ratio, cfg_gq):
+    """The drop-in with the extension on: (K', V', info) plus the per-token buffers' host copies."""
+    import rtkv
+    S = K.shape[1]
+    cfg = rtkv.CompressionConfig(alpha=0.8, beta=0.1, gamma=0.1, theta_h=0.4, theta_m=0.25, num_hidden_layers=4,
+                                 high_precision_bits=8, medium_precision_bits=4, low_precision_bits=2,
+                                 early_layer_ratio=ratio, middle_layer_ratio=ratio, later_layer_ratio=ratio)
+    comp = rtkv.RealTimePrefillCompressor(cfg, group_quant=cfg_gq)
+    ids = torch.zeros(1, S, dtype=torch.long, device="cuda")
+    k, v, info = comp.compress_layer_kv_cache(_dev(K, dtype), _dev(V, dtype), _dev(W, dtype), ids, 1)
+    return comp, k, v, info
+
+
+def _oracle(K, V, dtype, gqc, kept, labels, row_offset, bits3):
+    H = K.shape[-1] // 128
+    rows = kept.size
+    bits = np.array([bits3[l] for l in labels[kept]], np.int32)
+    out = []
+    for x in (K[0], V[0]):
+        votes = orc.gq_votes(x, ODT[dtype], H, 128, kept, gqc.n_vote, gqc.vote_stride)
+        idx = orc.gq_select(votes, H, 128, gqc.n_outlier, gqc.min_votes(rows)) if gqc.n_outlier else \
+            np.full((H, 1), -1, np.int16)
+        codes, meta, raw, deq = orc.gq_pack(x, ODT[dtype], H, 128, kept, bits, idx, row_offset)
+        out.append(dict(idx=idx, codes=codes, meta=meta, raw=raw, deq=deq))
+    return out
+
+
+CASES = [  # dtype, S, H, ratio, n_outlier
+    ("float16", 2048, 8, 0.6, 4),
+    ("bfloat16", 3000, 4, 0.5, 2),
+    ("float32", 4096, 32, 0.4, 4),
+    ("float16", 16384, 32, 0.6, 8),
+    ("bfloat16", 1000, 12, 0.8, 0),      # no outlier channels: pure per-head groups
+    ("float16", 5000, 40, 0.3, 16),      # 13B head count, the largest outlier budget
+]
+
+
+@pytest.mark.parametrize("dtype,S,H,ratio,n_out", CASES)
+def test_gq_matches_oracle(dtype, S, H, ratio, n_out):
+    import rtkv
+    gqc = rtkv.GroupQuantConfig(n_outlier=n_out, n_vote=4, vote_stride=3, min_votes_pm=250)
+    K, V, W = _inputs(500 + S, S, H, dtype)
+    comp, k, v, info = _layer(K, V, W, dtype, ratio, gqc)
+    c = info["group_quant"]
+    torch.cuda.synchronize()
+    rows = k.shape[1]
+    assert c.rows == rows
+    p = info["packed"]
+    kept = p["kept_index"][0].cpu().numpy().astype(np.int32)
+    labels = p["labels"][0].cpu().numpy()
+    ro = p["row_offset"][0].cpu().numpy()
+    o = _oracle(K, V, dtype, gqc, kept, labels, ro, (2, 4, 8))
+    nb = o[0]["codes"].size
+    for t, (codes, ref) in enumerate(((c.codes_k, o[0]), (c.codes_v, o[1]))):
+        if n_out:
+            assert np.array_equal(c.outlier_idx[t].cpu().numpy(), ref["idx"]), f"tensor {t} outlier channels"
+        assert np.array_equal(codes[:nb].cpu().numpy(), ref["codes"]), f"tensor {t} codes"
+        assert np.array_equal(_host(c.meta[:, t]), ref["meta"]), f"tensor {t} scale/zero-point"
+        if n_out:
+            assert np.array_equal(_host(c.raw[:, t]), ref["raw"]), f"tensor {t} raw outlier values"
+    kq, vq = c.dequantize()
+    assert np.array_equal(_host(kq[0]), o[0]["deq"]) and np.array_equal(_host(vq[0]), o[1]["deq"])
+    if n_out and H >= 8:  # the injected key outlier channels are found (channel 3 of head 0, 77 of head 0, ...)
+        ki = c.outlier_idx[0].cpu().numpy()
+        assert 3 in ki[0] and 77 in ki[0] and 2 in ki[1]
+
+
+def test_gq_is_opt_in_and_leaves_the_reference_outputs_alone():
+    """group_quant on: K'/V', packed codes and every statistic equal the default compressor's."""
+    import rtkv
+    dtype, S, H = "float16", 4096, 8
+    K, V, W = _inputs(9, S, H, dtype)
+    _, k0, v0, i0 = _layer(K, V, W, dtype, 0.5, None)
+    _, k1, v1, i1 = _layer(K, V, W, dtype, 0.5, rtkv.GroupQuantConfig())
+    assert "group_quant" not in i0 and "group_quant" in i1
+    assert torch.equal(k0.view(torch.int16), k1.view(torch.int16)) and torch.equal(v0.view(torch.int16), v1.view(torch.int16))
+    assert torch.equal(i0["packed"]["codes_k"], i1["packed"]["codes_k"])
+    assert i0["compression_ratio"] == i1["compression_ratio"]
+
+
+@pytest.mark.parametrize("dtype,S,H,Hq", [("float16", 4096, 8, 8), ("bfloat16", 3000, 4, 16), ("float32", 2048, 8, 32)])
+def test_gq_decode_attention_matches_torch(dtype, S, H, Hq):
+    """Decode attention read straight from the gq codes = softmax(q·K'ᵀ/√128)·V' over the unpacked rows in
+    torch fp32 (tolerance 2e-3 relative to the output's scale: fp32 accumulation order and exp)."""
+    import rtkv
+    K, V, W = _inputs(77 + S, S, H, dtype)
+    _, k, v, info = _layer(K, V, W, dtype, 0.6, rtkv.GroupQuantConfig(n_outlier=4))
+    c = info["group_quant"]
+    g = torch.Generator(device="cuda").manual_seed(5)
+    q = torch.randn(1, Hq, 128, device="cuda", generator=g).to(TD[dtype])
+    out = c.attend(q)
+    kq, vq = c.dequantize()
+    G = Hq // H
+    kk = kq[0].float().view(-1, H, 128).repeat_interleave(G, dim=1)  # [rows, Hq, 128]
+    vv = vq[0].float().view(-1, H, 128).repeat_interleave(G, dim=1)
+    s = torch.einsum("hd,rhd->hr", q[0].float(), kk) / math.sqrt(128)
+    ref = torch.einsum("hr,rhd->hd", torch.softmax(s, -1), vv)
+    err = (out[0] - ref).abs().max().item()
+    assert err <= 2e-3 * max(1.0, ref.abs().max().item()), err
+
+
+@pytest.mark.parametrize("dtype", ["float16", "bfloat16"])
+def test_gq_reconstruction_error_at_cfg5_shape(dtype):
+    """BASELINE config 5's shape (Llama-2-13B: 40 KV heads of 128, S = 32768) with per-channel key
+    outliers: the group-wise pack with outlier channels reconstructs the kept rows with a lower error than
+    the reference's per-token scheme (the K'/V' the drop-in returns), at identical code widths.  The
+    numbers are printed for DESIGN.md (the extension's parity is unpinned; this is its measured effect)."""
+    import rtkv
+    S, H = 32768, 40
+    F = H * 128
+    g = torch.Generator(device="cuda").manual_seed(13)
+    Kd = torch.randn(1, S, F, device="cuda", generator=g)
+    Vd = torch.randn(1, S, F, device="cuda", generator=g)
+    ch = torch.randperm(F, generator=g, device="cuda")[: 2 * H]  # ~2 outlier channels per head
+    Kd[..., ch] *= 20.0
+    Kd, Vd = Kd.to(TD[dtype]), Vd.to(TD[dtype])
+    P = 128
+    W = torch.rand(1, 8, S, P, device="cuda", generator=g).to(TD[dtype])
+    cfg = rtkv.CompressionConfig(alpha=0.8, beta=0.1, gamma=0.1, theta_h=0.4, theta_m=0.25, num_hidden_layers=40,
+                                 high_precision_bits=8, medium_precision_bits=4, low_precision_bits=2)
+    comp = rtkv.RealTimePrefillCompressor(cfg, group_quant=rtkv.GroupQuantConfig(n_outlier=4))
+    ids = torch.zeros(1, S, dtype=torch.long, device="cuda")
+    k, v, info = comp.compress_layer_kv_cache(Kd, Vd, W, ids, 20)
+    c = info["group_quant"]
+    kept = info["packed"]["kept_index"][0].long()
+    kq, vq = c.dequantize()
+    res = {}
+    for name, x, ref_t, gq_t in (("K", Kd, k, kq), ("V", Vd, v, vq)):
+        src = x[0, kept].float()
+        e_tok = ((ref_t[0].float() - src) ** 2).mean().item()
+        e_gq = ((gq_t[0].float() - src) ** 2).mean().item()
+        res[name] = (e_tok, e_gq)
+    print(f"gq reconstruction MSE ({dtype}, 13B shape, S={S}, rows={c.rows}): per-token K {res['K'][0]:.4g} -> "
+          f"gq {res['K'][1]:.4g}; V {res['V'][0]:.4g} -> {res['V'][1]:.4g}; packed bytes per token "
+          f"{c.nbytes() / max(c.rows, 1):.0f}")
+    assert res["K"][1] < 0.5 * res["K"][0]   # the outlier channels no longer set every channel's step
+    assert res["V"][1] < res["V"][0]         # per-head groups alone already narrow the range

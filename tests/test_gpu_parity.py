@@ -459,6 +459,44 @@ def test_compress_layer_kv_cache(case):
             assert np.array_equal(pk["row_offset"].cpu().numpy(), o["row_offset"])
 
 
+@pytest.mark.parametrize("case", [c for c in by_kind("layer") if c["spec"]["no_selection"]], ids=lambda c: c["name"])
+def test_quant_only_fused_launch_matches_reference_golden(case):
+    """BASELINE config 2 (quantization only) through the launch the bench's cfg2_s4096_quant leg times:
+    rtkv_compress_layer with RTKV_NO_SELECTION — the quantization-only K2 (fsel_quant_kernel: scores,
+    classes, row offsets) and K4 — byte for byte against the reference's
+    apply_mixed_precision_quantization output on the same inputs (dynamic_quantization.py:128-196;
+    tests/golden/gen_golden.py cfg2_quant, fp32 = the reference model's dtype and fp16)."""
+    import rtkv
+    from rtkv import _lib as L
+    s = case["spec"]
+    arrays = load_case(case)
+    K, V, W = layer_inputs(s)
+    B, S, F = s["B"], s["S"], s["Hkv"] * s["D"]
+    cfg = layer_config(s)
+    p = rtkv.params_from_config(cfg, s["layer"], s["P"], 1.0, L.EMIT_DEQUANT | L.EMIT_PACKED | L.NO_SELECTION)
+    td = {"float32": torch.float32, "float16": torch.float16, "bfloat16": torch.bfloat16}[s["dtype"]]
+    bufs = rtkv.LayerBuffers(B, S, F, td, "cuda", tuple(s["bits"]))
+    res = rtkv.compress_layer(dev(K, s["dtype"]), dev(V, s["dtype"]), dev(W, s["dtype"]), p, bufs, rtkv.Workspace("cuda"))
+    st = res.final_stats()
+    assert st.max_kept == S and case["scalars"]["max_selected"] == S
+    k2, v2 = res.kv()
+    assert_matches(case, "scores", bufs.scores.cpu().numpy(), arrays)
+    assert_matches(case, "labels", bufs.labels.cpu().numpy(), arrays)
+    assert_matches(case, "mask", bufs.mask.cpu().numpy(), arrays)
+    assert_matches(case, "k_out", host(k2), arrays)
+    assert_matches(case, "v_out", host(v2), arrays)
+    cc = st.batch[0]["class_count"]
+    assert [cc[2], cc[1], cc[0]] == [case["scalars"]["high"], case["scalars"]["medium"], case["scalars"]["low"]]
+    assert torch.equal(bufs.kept_index[0].cpu(), torch.arange(S, dtype=torch.int32))
+    # the packed codes decode to the same rows
+    n = st.total_packed_bytes
+    dk, dv = rtkv.unpack_layer(dict(codes_k=bufs.packed_k[:n], codes_v=bufs.packed_v[:n], row_offset=bufs.row_offset,
+                                    scale_zp=bufs.scale_zp, kept_index=bufs.kept_index, labels=bufs.labels, rows=[S],
+                                    bits=tuple(s["bits"]), dtype=td, feature_dim=F))
+    iv = torch.int16 if td != torch.float32 else torch.int32
+    assert torch.equal(dk.view(iv), k2.view(iv)) and torch.equal(dv.view(iv), v2.view(iv))
+
+
 def test_native_bhsd_layout_matches_bsf():
     """[B,H,S,D] input (no transpose copy) gives the same outputs as the [B,S,H*D] API layout."""
     import rtkv

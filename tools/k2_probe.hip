@@ -47,7 +47,7 @@ int main(int argc, char** argv) {
   CK(hipMalloc(&dmask, S));
   CK(hipMalloc(&dki, S * 4));
   CK(hipMalloc(&dro, S * 8));
-  CK(hipMalloc(&dst, 4096));
+  CK(hipMalloc(&dst, rtkv_stats_bytes(1)));  // header + batch row + rtkv_layer_times (the memset covers it all)
   CK(hipMalloc(&ws, wsb));
   CK(hipMemcpy(dA, A.data(), S * 4, hipMemcpyHostToDevice));
   CK(hipMemcpy(dT2, T2.data(), S * 4, hipMemcpyHostToDevice));
@@ -105,7 +105,7 @@ int main(int argc, char** argv) {
           CK(hipMemcpyFromSymbol(ck, HIP_SYMBOL(g_k2_clock), sizeof(ck)));
           if (r == reps + 4) printf("  shader clock over the selecting workgroup: %.0f MHz\n", (double)(ck[3] - ck[0]) / ((double)(pr[3] - pr[0]) * 0.01));
           for (int k = 1; k < 16; ++k) { const unsigned long long b0 = k >= 8 ? pr[8] : pr[0]; if (k != 8) ph[k] += (pr[k] > b0 ? (double)(pr[k] - b0) : 0.0) * 0.01; }  // µs
-          unsigned long long wg[32][10];
+          unsigned long long wg[64][10];
           CK(hipMemcpyFromSymbol(wg, HIP_SYMBOL(g_k2_wg), sizeof(wg)));
           const int G = (int)((S + 1023) / 1024);
           unsigned long long t0 = wg[0][0], mx[10] = {0};
