@@ -208,10 +208,10 @@ def parse():
     ap.add_argument("--no-packed", action="store_true", help="skip the packed-code output")
     ap.add_argument("--no-dequant", action="store_true", help="skip the dequantized K'/V' output (packed only)")
     ap.add_argument("--legs", default="f16,packed_only,f16_packed_only,bits16,drop_in,s4096,cfg2_s4096_quant,s65536,"
-                                      "independent_layers,prefill_7b,prefill_7b_f32",
+                                      "independent_layers,prefill_7b,prefill_7b_f32,gq",
                     help="extra single-GPU legs after the main line: comma list of f16, packed_only, f16_packed_only, "
                          "bits16, drop_in, s4096, cfg2_s4096_quant, s65536, independent_layers, prefill_7b, "
-                         "prefill_7b_f32 (or 'none')")
+                         "prefill_7b_f32, gq (or 'none')")
     ap.add_argument("--prefill-dtype", default="float16", choices=["float16", "bfloat16", "float32"],
                     help="dtype of the prefill_7b leg's random-init model")
     ap.add_argument("--prefill-modes", default="none,fused,eager",
@@ -530,6 +530,60 @@ def drop_in_leg(args, job, steps, warmup):
             "modes": out, "steps": steps,
             "path": "rtkv.RealTimePrefillCompressor.compress_layer_kv_cache (dequant + packed, one host wait "
                     "per layer for the output shape; strict = the default)"}
+
+
+def gq_leg(args, job, steps, warmup):
+    """Extension rtkv-gq/1 (opt-in; per-channel outlier voting + per-head group-wise pack, csrc/outlier.hip) on
+    the main line's layers: each layer is compressed as usual, then gq_compress (votes, outlier select, pack)
+    runs on its kept rows, timed by events around the gq launches alone.  Algorithmic bytes per layer: the
+    kept K/V rows read by the pack (plus every vote_stride-th row by the vote), the codes, per-head
+    scale/zero-points and outlier values written.  Also the reconstruction MSE of K' and V' on the last
+    layer: the reference's per-token scheme (the drop-in's K'/V') against gq, same kept rows and widths."""
+    import rtkv
+    if args.importance != "w" or job.F % 512 or not job.emit_packed or not job.emit_dequant:
+        return {"skipped": "needs the W path with dequantized and packed outputs, F a multiple of 512"}
+    cfg = rtkv.GroupQuantConfig()
+    acct = job.accounting()
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.layers)]
+    tot, n, c = 0.0, 0, None
+    for it in range(warmup + steps):
+        for l in range(args.layers):
+            job._step_one(l)
+            K, V = job.inputs[l % job.in_slots][:2]
+            b = job.bufs[l % job.slots]
+            Sp, pk = acct[l]
+            ev[l][0].record()
+            c = rtkv.gq_compress(K, V, b.kept_index[0], b.labels[0], b.row_offset[0], b.stats, Sp, pk, job.bits, cfg)
+            ev[l][1].record()
+        torch.cuda.synchronize(job.device)
+        if it >= warmup:
+            tot += sum(a.elapsed_time(z) for a, z in ev)
+            n += args.layers
+    us = tot / n * 1e3
+    e, H = job.elem(), job.F // 128
+    nb = 0
+    for Sp, pk in acct:
+        nb += 2 * Sp * job.F * e + 2 * (Sp // cfg.vote_stride) * job.F * e  # pack reads + vote reads
+        nb += 2 * pk + Sp * 2 * H * (2 + cfg.n_outlier) * e                   # codes + meta + outlier values
+    nb /= len(acct)
+    # reconstruction on the last layer (its buffers and K/V are still resident)
+    l = args.layers - 1
+    K, V = job.inputs[l % job.in_slots][:2]
+    b = job.bufs[l % job.slots]
+    Sp = acct[l][0]
+    kept = b.kept_index[0, :Sp].long()
+    kq, vq = c.dequantize()
+    mse = {}
+    for name, x, deq, gq in (("K", K, b.k_out, kq), ("V", V, b.v_out, vq)):
+        src = x[0, kept].float()
+        mse[name] = {"per_token": ((deq[: Sp * job.F].view(Sp, job.F).float() - src) ** 2).mean().item(),
+                     "gq": ((gq[0].float() - src) ** 2).mean().item()}
+    gbs = nb / (us / 1e6) / 1e9
+    return {"us_per_layer": round(us, 2), "algorithmic_bytes_per_layer": int(nb), "GBs": round(gbs, 1),
+            "hbm_frac": round(gbs / 8000.0, 4), "config": vars(cfg), "reconstruction_mse_last_layer": mse,
+            "note": "synthetic K/V ~ N(0,1) carry no outlier channels: the gq MSE gain here comes from the per-head "
+                    "groups alone (tests/test_gpu_gq.py measures it with injected key outliers at the 13B shape)",
+            "path": "rtkv.gq_compress after each layer's rtkv_compress_layer (events around the gq launches only)"}
 
 
 def union_inputs(args, device, world, dtype):
@@ -988,6 +1042,8 @@ def main():
                     from prefill_model import prefill_leg
                     legs["prefill_7b_f32"] = prefill_leg(device, S=job.S, dtype=torch.float32,
                                                          modes=tuple(args.prefill_modes.split(",")))
+                elif name == "gq":
+                    legs["gq"] = gq_leg(args, job, args.leg_steps, 2)
                 elif name == "drop_in":
                     legs["drop_in"] = drop_in_leg(args, job, args.leg_steps, 2)
                     legs["drop_in"]["raw_driver_ms_per_layer"] = round(ms_per_step / args.layers, 4)
