@@ -39,14 +39,16 @@ def _cfg():
 def _inputs(dtype, seed=2024):
     """Attention that looks at the prompt by a varying amount: each head's P prompt keys share a direction e,
     and each query carries a random gain along e, so the prompt mass A (and the scores) spread over all
-    three classes and the 0.8/0.6/0.4 budgets bind (with plain N(0, 1) queries every layer keeps every
+    three classes and the 0.8 and 0.4 budgets bind (with plain N(0, 1) queries every layer keeps every
     token and nothing is selected)."""
     import rtkv
     g = torch.Generator(device="cuda").manual_seed(seed)
     P = rtkv.prompt_length(S)
     e = torch.randn(1, H, 1, D, device="cuda", generator=g)
     e = e / e.norm(dim=-1, keepdim=True) * (0.5 * math.sqrt(D))
-    gain = torch.rand(1, H, S, 1, device="cuda", generator=g) ** 2 * 4.0
+    # most queries lean on the prompt (gain >= 1.85 puts a late token's prompt mass above θ_h's share), so
+    # about nine tokens in ten are HIGH and even layer 0's 0.8 budget (6.4 bits a token) binds
+    gain = 1.0 + 3.0 * torch.rand(1, H, S, 1, device="cuda", generator=g).sqrt()
     Q = (torch.randn(1, H, S, D, device="cuda", generator=g) + gain * e).to(dtype)
     K = torch.randn(1, S, H, D, device="cuda", generator=g)
     K[:, :P] += e.permute(0, 2, 1, 3)
@@ -127,12 +129,13 @@ def explain(ref, new, theta_h, theta_m, tol_rel=TOL):
     return dict(score_max_rel_err=float((d / np.maximum(np.abs(s0), 1e-6)).max()),
                 label_mismatches=int(lab.size), kept_mismatches=int(keep.size),
                 kept_mismatches_by_label_flip=n_flip, kept_mismatches_between_cutoffs=n_cut,
+                class_counts_ref=np.bincount(ref["labels"].astype(np.int64), minlength=3).tolist(),
                 kept_ref=int(ref["mask"].sum()), kept_new=int(new["mask"].sum()),
                 cutoff_ref=T0, cutoff_new=T1)
 
 
 @pytest.mark.parametrize("dtype", ["float32", "float16"])
-@pytest.mark.parametrize("layer", [0, 20])
+@pytest.mark.parametrize("layer", [0, 31])
 def test_fused_mode_mismatches_are_threshold_ties(dtype, layer):
     import rtkv
     td = getattr(torch, dtype)
@@ -167,7 +170,7 @@ np.savez(sys.argv[1], lse=lse.cpu().numpy(), **o)
 """
 
 
-@pytest.mark.parametrize("layer", [0, 20])
+@pytest.mark.parametrize("layer", [0, 31])
 def test_split_lse_layer_matches_the_exact_kernel_at_cfg3(tmp_path, layer):
     """The default fp32 LSE and K1' (three-way bf16 split on the bf16 matrix cores) against the exact
     f32-MFMA kernels (RTKV_LSE_F32_EXACT, in a child process: the knob is read once per process) on the same

@@ -19,6 +19,7 @@ import sys
 
 SIMDS, XCDS = 1024, 8
 PEAK_GHZ = 2.4  # MI355X peak engine clock (MI355X_MICROARCH.md chip parameters)
+DENSE_BF16_TFLOPS = 2500.0  # dense f16/bf16 MFMA peak at PEAK_GHZ (MI355X_MICROARCH.md)
 
 
 def load(path):
@@ -67,16 +68,20 @@ def main():
                 if k in m:
                     rec[k] = m[k]
             if m.get("SQ_WAVE_CYCLES"):  # shares of wave time (all quad-cycle counters)
-                for k, name in (("SQ_WAIT_ANY", "wait_any_pct"), ("SQ_WAIT_INST_ANY", "wait_inst_any_pct"),
-                                ("SQ_ACTIVE_INST_VALU", "valu_active_pct"), ("SQ_ACTIVE_INST_LDS", "lds_active_pct"),
-                                ("SQ_ACTIVE_INST_VMEM", "vmem_active_pct")):
+                for k, share in (("SQ_WAIT_ANY", "wait_any_pct"), ("SQ_WAIT_INST_ANY", "wait_inst_any_pct"),
+                                 ("SQ_ACTIVE_INST_VALU", "valu_active_pct"), ("SQ_ACTIVE_INST_LDS", "lds_active_pct"),
+                                 ("SQ_ACTIVE_INST_VMEM", "vmem_active_pct")):
                     if k in m:
-                        rec[name] = round(100 * m[k] / m["SQ_WAVE_CYCLES"], 1)
+                        rec[share] = round(100 * m[k] / m["SQ_WAVE_CYCLES"], 1)
             if "SQ_LDS_BANK_CONFLICT" in m and m.get("SQ_LDS_IDX_ACTIVE"):
                 rec["lds_bank_conflict_pct"] = round(100 * m["SQ_LDS_BANK_CONFLICT"] / m["SQ_LDS_IDX_ACTIVE"], 2)
             mops = m.get("SQ_INSTS_VALU_MFMA_MOPS_F16", 0.0) + m.get("SQ_INSTS_VALU_MFMA_MOPS_BF16", 0.0)
             if mops:
                 rec["mfma_flops"] = mops * 512
+                # achieved rate against the dense f16/bf16 peak (2.5 PFLOP/s at 2.4 GHz, no sparsity)
+                rate = mops * 512 / (m["ns"] * 1e-9) / 1e12
+                rec["mfma_tflops"] = round(rate, 1)
+                rec["frac_of_dense_bf16_peak"] = round(rate / DENSE_BF16_TFLOPS, 4)
             out[f"{wl}: {name} grid={grid}"] = rec
     doc = {"source": "rocprofv3 --pmc passes of tools/mfma_pmc.sh (tools/lse_bench.py: S = 4096 and 16384; "
                      "bench.py --importance qk --dtype float16, 4 cfg3 layers)",
