@@ -17,7 +17,7 @@ import json
 import os
 import sys
 
-SIMDS, XCDS = 1024, 8
+SIMDS, XCDS, SES = 1024, 8, 32
 PEAK_GHZ = 2.4  # MI355X peak engine clock (MI355X_MICROARCH.md chip parameters)
 DENSE_BF16_TFLOPS = 2500.0  # dense f16/bf16 MFMA peak at PEAK_GHZ (MI355X_MICROARCH.md)
 
@@ -62,6 +62,13 @@ def main():
                 if "SQ_VALU_MFMA_BUSY_CYCLES" in m:
                     util = 100 * m["SQ_VALU_MFMA_BUSY_CYCLES"] / (m["ns"] * clk * SIMDS)
                     rec["mfma_util_pct" if ok else "mfma_util_pct_lower_bound"] = round(util, 2)
+            if m.get("SQ_BUSY_CYCLES") and "SQ_VALU_MFMA_BUSY_CYCLES" in m:
+                # the same pass's SQ_BUSY_CYCLES (summed over the 32 shader engines) as the cycle base: a
+                # busy-time window per engine instead of the counter window's wall clock, so it holds for
+                # short dispatches too.  util = MFMA busy / (SQ busy x 1024 SIMDs / 32 engines)
+                rec["sq_busy_clock_GHz"] = round(m["SQ_BUSY_CYCLES"] / SES / m["ns"], 3)
+                rec["mfma_util_pct_sq_busy"] = round(100 * m["SQ_VALU_MFMA_BUSY_CYCLES"] * SES /
+                                                     (m["SQ_BUSY_CYCLES"] * SIMDS), 2)
             for k in ("SQ_INSTS_LDS", "SQ_LDS_BANK_CONFLICT", "SQ_LDS_IDX_ACTIVE", "SQ_WAVES", "SQ_INSTS_MFMA",
                       "SQ_WAVE_CYCLES", "SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_VALU", "SQ_ACTIVE_INST_LDS",
                       "SQ_ACTIVE_INST_VMEM", "SQ_WAIT_INST_LDS"):
@@ -88,7 +95,11 @@ def main():
            "definition": "mfma_util_pct = SQ_VALU_MFMA_BUSY_CYCLES / (kernel duration x clock x 1024 SIMDs), "
                          "clock = GRBM_GUI_ACTIVE/8 / duration when that is <= 2.4 GHz (the counter window is the "
                          "kernel's), else 2.4 GHz and the figure is reported as mfma_util_pct_lower_bound; "
-                         "lds_bank_conflict_pct = SQ_LDS_BANK_CONFLICT / SQ_LDS_IDX_ACTIVE",
+                         "lds_bank_conflict_pct = SQ_LDS_BANK_CONFLICT / SQ_LDS_IDX_ACTIVE; "
+                         "mfma_util_pct_sq_busy = SQ_VALU_MFMA_BUSY_CYCLES x 32 / (SQ_BUSY_CYCLES x 1024): the "
+                         "same pass's per-engine busy cycles as the base (32 shader engines), valid for short "
+                         "dispatches; on the long LSE dispatch it reads within 7 % of the clock-window figure; "
+                         "mfma_tflops / frac_of_dense_bf16_peak = MOPS x 512 / duration against 2.5 PFLOP/s",
            "kernels": out}
     here = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "profiles")
     with open(os.path.join(here, f"{tag}_mfma.json"), "w") as f:
