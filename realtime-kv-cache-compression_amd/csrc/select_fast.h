@@ -19,8 +19,10 @@
 //           atomic's return value, one atomic per bin and wave).
 // 2 select  EVERY workgroup (the same inputs, the same deterministic result, so no selection word
 //           travels between workgroups; workgroup G−1 publishes the statistics and the early host
-//           mirror): once every workgroup's counts and ready words are published, the quotas n_g from
-//           the class counts (the greedy in closed form), per partially kept class the bin where the
+//           mirror): once every workgroup's counts and score-sum/range words are published, the quotas
+//           n_g from the class counts (the greedy in closed form) and the statistics — a layer that keeps
+//           whole classes only is selected here, without waiting for any workgroup's drain; otherwise,
+//           once every ready word is in too, per partially kept class the bin where the
 //           count from the top reaches n_g (one packed scan for all classes), and the exact threshold
 //           from that bin's slot list (≤ 64 entries, one wave): key T and the tie CUTOFF, the index of
 //           the n_g-th token in (key desc, index asc) order.  A bin with more than 64 tokens (heavy
@@ -36,8 +38,8 @@
 // cleared before every launch), written with sc1 stores and polled with sc1 loads, so a consumer sees
 // data and flag in one round trip and producers need no drain between them (MI355X_MICROARCH.md
 // hand-off rows: each separate flag or drain costs a memory round trip, ≈1–2 µs).  The one drain
-// left is phase 1's: a workgroup's slot-list entries and score sums are complete (s_waitcnt
-// vmcnt(0)) before its tagged ready word, which every workgroup's phase 2 polls.
+// left is phase 1's: a workgroup's slot-list entries are complete (s_waitcnt vmcnt(0)) before its
+// tagged ready word, which phase 2 polls only when a class is partly kept.
 #pragma once
 #include <type_traits>
 
@@ -76,6 +78,8 @@ struct FastHead {                  // zeroed before the launch (K1 or a memset):
   uint64_t ready[kMaxG];           // phase 1, per workgroup: kTag once its slot entries, partials, scores and
                                    // classes are complete (drained)
   uint64_t agg[kMaxG];             // phase 3, per workgroup: kTag | kept tokens per class (3 x 11 bits)
+  uint64_t pst[kMaxG][4];          // phase 1, per workgroup, from registers: kTag | low / high half of the
+                                   // score sum's bits, kTag | score key min, kTag | score key max
 };
 struct FastPartial {               // phase 1, per workgroup (complete before its counts word)
   double ssum;
@@ -99,7 +103,8 @@ struct FastArgs {
   uint64_t early_seq;
   uint32_t spin_limit;             // polls before a hand-off wait gives up (poll_tagged)
   int withhold;                    // RTKV_TEST_WITHHOLD_SELECTION: workgroup G-1 never publishes its ready
-                                   // word (phase 2 times out everywhere); RTKV_TEST_WITHHOLD_LOOKBACK:
+                                   // word (phase 2 times out everywhere when a group is partly kept, the
+                                   // only case that reads the histograms); RTKV_TEST_WITHHOLD_LOOKBACK:
                                    // workgroup 0 never publishes its phase-3 counts (the look-back times out
                                    // AFTER the early statistics are out)
 };
@@ -539,124 +544,148 @@ __device__ __forceinline__ void publish_stats(const FastArgs& g, bool fallback, 
   }
 }
 
+// The greedy in closed form (selective_propagation.py:93-131) from a row's class counts N3: per group q
+// (LOW, MEDIUM, HIGH, then the fallback's "all tokens") q_mode[q] (M_NONE / M_ALL / M_PART) and
+// q_mode[kGrp + q] the tokens to keep (the fallback's k = max(1, int(0.1·S))), quota / ccount the int64
+// kept and class counts; returns whether a group is partly kept (a threshold search is needed).
+__device__ __forceinline__ bool quotas_closed_form(const FinalizeArgs& a, int S, const uint32_t (&N3)[3], int* q_mode,
+                                                   int64_t* quota, int64_t* ccount) {
+  // In 32-bit integers: N <= S <= 2^16 and bits <= 16, so every product and quotient that can decide n
+  // fits; the budget U = floor(8·S·ratio) (int64 in the reference) is compared as a double, exact below
+  // 2^53 (beyond, every class fits whole).
+  const double u8 = 8.0 * ((double)S * a.p.propagation_ratio);
+  const double Ud = u8 >= 9.0e18 ? 9.0e18 : floor(u8);
+  int used = 0, kept = 0;
+  bool partly = false;
+  for (int k = 2; k >= 0; --k) {
+    const int N = (int)N3[k], bb = a.p.bits[k];
+    int n;
+    if (a.mode_select == 2) n = N;
+    else if (!(u8 >= 0.0)) n = 0;  // U = -1 (selective_propagation.py: nothing fits)
+    else if (bb <= 0) n = N;
+    else {
+      const double x = Ud - (double)used;  // U - used >= 0
+      n = x >= (double)bb * (double)N ? N : (int)((uint32_t)x / (uint32_t)bb);
+    }
+    used += n * (bb > 0 ? bb : 0);
+    kept += n;
+    q_mode[kGrp + k] = n;
+    quota[k] = n;
+    ccount[k] = N;
+    const int md = (n == 0) ? M_NONE : (n == N ? M_ALL : M_PART);
+    q_mode[k] = md;
+    partly |= md == M_PART;
+  }
+  int64_t kf = (int64_t)((double)S * 0.1);
+  if (kf < 1) kf = 1;
+  const bool fb = a.mode_select == 1 && !(a.p.flags & RTKV_NO_FALLBACK) && kept == 0;
+  q_mode[kGrp + 3] = (int)kf;
+  const int md3 = !fb ? M_NONE : (kf >= S ? M_ALL : M_PART);
+  q_mode[3] = md3;
+  return partly || md3 == M_PART;
+}
+
+// Phase 2's shared state (LDS), written by select_quotas and read by select_thresholds and phase 3.
+struct SelShared {
+  double ssum;          // the row's score sum
+  uint32_t kr[2];       // the row's score key range
+  int q[2 * kGrp];      // per group: mode (M_NONE / M_ALL / M_PART), then the tokens to keep
+  int64_t cc[3], quota[3];
+  int partly;           // a group is partly kept: the threshold search (and phase 1's slot lists) run
+};
+
+// Phase 2a, EVERY workgroup: wave 0 waits for every workgroup's class counts and takes the quotas (the
+// greedy in closed form), wave 1 for their score sums and ranges — tagged words each workgroup publishes
+// from registers right after its scores, so nothing here waits for a drain.  Workgroup G−1 then publishes
+// the statistics and the early host mirror.  When no class is partly kept (most layers at ratio >= 0.6
+// keep whole classes) the selection is complete here: phase 1's slot lists are never written and no
+// ready word is awaited.
 template <int TPT>
-__device__ __forceinline__ void select_thresholds(const FastArgs& g, uint32_t* hist_lds, uint64_t* s_selw,
-                                                  bool publish) {
+__device__ __forceinline__ void select_quotas(const FastArgs& g, SelShared& sh, bool publish) {
   const FinalizeArgs& a = g.f;
-  __shared__ uint32_t s_scan32[kGrp][kSW];
-  __shared__ uint32_t s_pick[kGrp][3];
-  __shared__ uint32_t s_thr[kGrp];
-  __shared__ uint32_t s_cutw[kGrp];
-  __shared__ double s_ssum;
-  __shared__ uint32_t s_kr[2];
-  __shared__ int s_q[2 * kGrp];
-  __shared__ int64_t s_cc[3], s_quota[3];
   const int t = threadIdx.x, lane = t & (kWave - 1), wid = t / kWave;
   const int S = (int)a.S;
   const int G = (S + kST - 1) / kST;
+  (void)t;
   K2_PROBE(0);
   if (wid == 0) {
-    // ---- every workgroup's class counts (tagged words published from registers), the quotas: the
-    // greedy in closed form (selective_propagation.py:93-131), lane l reading workgroup l (G <= 64)
+    // ---- every workgroup's class counts, the quotas (selective_propagation.py:93-131), lane l reading
+    // workgroup l (G <= 64)
     const uint64_t w = poll_tagged(g.L.head->part, 1, G, g.spin_limit, a.stats);
     uint64_t cnt = lane < G ? from11w(w & ~kTag) : 0ull;
 #pragma unroll
     for (int o = kWave / 2; o > 0; o >>= 1) cnt += __shfl_xor(cnt, o, kWave);
     if (lane == 0) {
-      // In 32-bit integers: N <= S <= 2^16 and bits <= 16, so every product and quotient that can
-      // decide n fits; the budget U = floor(8·S·ratio) (int64 in the reference) is compared as a
-      // double, exact below 2^53 (beyond, every class fits whole).
-      const double u8 = 8.0 * ((double)S * a.p.propagation_ratio);
-      const double Ud = u8 >= 9.0e18 ? 9.0e18 : floor(u8);
-      int used = 0, kept = 0;
-      int md[kGrp];
-      for (int k = 2; k >= 0; --k) {
-        const int N = (int)fldw(cnt, k), bb = a.p.bits[k];
-        int n;
-        if (a.mode_select == 2) n = N;
-        else if (!(u8 >= 0.0)) n = 0;  // U = -1 (selective_propagation.py: nothing fits)
-        else if (bb <= 0) n = N;
-        else {
-          const double x = Ud - (double)used;  // U - used >= 0
-          n = x >= (double)bb * (double)N ? N : (int)((uint32_t)x / (uint32_t)bb);
-        }
-        used += n * (bb > 0 ? bb : 0);
-        kept += n;
-        s_q[kGrp + k] = n;
-        s_quota[k] = n;
-        s_cc[k] = N;
-        md[k] = (n == 0) ? M_NONE : (n == N ? M_ALL : M_PART);
-        s_q[k] = md[k];
-      }
-      int64_t kf = (int64_t)((double)S * 0.1);
-      if (kf < 1) kf = 1;
-      const bool fb = a.mode_select == 1 && !(a.p.flags & RTKV_NO_FALLBACK) && kept == 0;
-      s_q[kGrp + 3] = (int)kf;
-      md[3] = !fb ? M_NONE : (kf >= S ? M_ALL : M_PART);
-      s_q[3] = md[3];
+      const uint32_t N3[3] = {(uint32_t)fldw(cnt, 0), (uint32_t)fldw(cnt, 1), (uint32_t)fldw(cnt, 2)};
+      sh.partly = quotas_closed_form(a, S, N3, sh.q, sh.quota, sh.cc) ? 1 : 0;
     }
   } else if (wid == 1) {
-    // ---- every workgroup's phase-1 stores complete (slot lists, partials, scores, classes)
-    (void)poll_tagged(g.L.head->ready, 1, G, g.spin_limit, a.stats);
-  }
-  __syncthreads();
-  K2_PROBE(1);
-  // ---- every histogram load the thresholds may need (thread t owns descending bins 4t..4t+3), and
-  // wave 0 the score sums and ranges, in one round trip
-  const int ngrp = g.hist_fb ? 4 : 3;
-  double p_ss = 0.0;
-  uint32_t p_kmn = 0xffffffffu, p_kmx = 0u;
-  if (wid == 0 && lane < G) {
-    const FastPartial* pp = g.L.part + lane;
-    p_ss = ld_sc1(&pp->ssum);
-    p_kmn = ld_sc1(&pp->kmn);
-    p_kmx = ld_sc1(&pp->kmx);
-  }
-  uint32_t c[kGrp][4];
-  {
-    rtkv_u32x4 h[kGrp];
-#pragma unroll
-    for (int q = 0; q < kGrp; ++q) {
-      h[q] = rtkv_u32x4{0u, 0u, 0u, 0u};
-      if (q < ngrp) h[q] = ld16_sc1(g.L.hist + q * kNBin + (kNBin - 4 - 4 * t));
+    // ---- every workgroup's score sum and key range (four tagged words, polled together)
+    double p_ss = 0.0;
+    uint32_t p_kmn = 0xffffffffu, p_kmx = 0u;
+    if (lane < G) {
+      const uint64_t* pw = g.L.head->pst[lane];
+      uint64_t w0, w1, w2, w3;
+      for (uint32_t it = 0;; ++it) {
+        w0 = ld_sc1(pw);
+        w1 = ld_sc1(pw + 1);
+        w2 = ld_sc1(pw + 2);
+        w3 = ld_sc1(pw + 3);
+        if (w0 & w1 & w2 & w3 & kTag) break;
+        if (it >= g.spin_limit) {
+          atomicOr(&a.stats->error_flags, (int)RTKV_FLAG_SPIN_TIMEOUT);
+          w0 = w1 = w2 = 0ull;
+          w3 = 0ull;
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+      }
+      p_ss = __builtin_bit_cast(double, (w0 & 0xffffffffull) | ((w1 & 0xffffffffull) << 32));
+      if (w2 & kTag) p_kmn = (uint32_t)w2;
+      p_kmx = (uint32_t)w3;
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#pragma unroll
-    for (int q = 0; q < kGrp; ++q) { c[q][0] = h[q].w; c[q][1] = h[q].z; c[q][2] = h[q].y; c[q][3] = h[q].x; }
-  }
-  if (wid == 0) {
 #pragma unroll
     for (int o = kWave / 2; o > 0; o >>= 1) {  // lanes >= G hold the neutral values
       p_ss += __shfl_xor(p_ss, o, kWave);
       p_kmn = min(p_kmn, (uint32_t)__shfl_xor((int)p_kmn, o, kWave));
       p_kmx = max(p_kmx, (uint32_t)__shfl_xor((int)p_kmx, o, kWave));
     }
-    if (lane == 0) { s_ssum = p_ss; s_kr[0] = p_kmn; s_kr[1] = p_kmx; }
+    if (lane == 0) { sh.ssum = p_ss; sh.kr[0] = p_kmn; sh.kr[1] = p_kmx; }
   }
-#ifdef RTKV_SELECT_PROBE
-  {
-    uint32_t z = 0;
-#pragma unroll
-    for (int q = 0; q < kGrp; ++q) z += c[q][0] + c[q][1] + c[q][2] + c[q][3];
-    if (z == 0xffffffffu) g_k2_probe[15] = z;  // waits for the histogram loads
-    K2_PROBE(4);
-  }
-#endif
   __syncthreads();
+  K2_PROBE(1);
   // statistics known here; phase 3 adds the kept-token sums (stats zeroed before).  Published by the LAST wave
   // (its later vmcnt waits include the host store; wave 0 runs the thresholds and the look-back): lane 0
   // writes the device block and the line's words, the wave stores the host line in one instruction
   if (publish && wid == kSW - 1) {
     __shared__ uint64_t s_line[16];
     if (lane == 0) {
-      const int64_t ccount[3] = {s_cc[0], s_cc[1], s_cc[2]};
-      const int64_t quota[3] = {s_quota[0], s_quota[1], s_quota[2]};
-      publish_stats(g, s_q[3] != M_NONE, s_ssum, s_kr[0], s_kr[1], ccount, quota, s_line);
+      const int64_t ccount[3] = {sh.cc[0], sh.cc[1], sh.cc[2]};
+      const int64_t quota[3] = {sh.quota[0], sh.quota[1], sh.quota[2]};
+      publish_stats(g, sh.q[3] != M_NONE, sh.ssum, sh.kr[0], sh.kr[1], ccount, quota, s_line);
     }
     __builtin_amdgcn_wave_barrier();
     asm volatile("" ::: "memory");  // (the same wave: its LDS writes are read in order)
     if (g.early) host_line_store(reinterpret_cast<uint64_t*>(g.early), s_line);
   }
+}
+
+// Phase 2b, EVERY workgroup, after select_quotas (and, when a class is partly kept, after this workgroup's
+// slot lists are drained and its ready word is out): per partly kept group the bin where the count from
+// the top reaches its quota (one packed scan), and the exact threshold from that bin's slot list (or the
+// rescan rounds); then the selection words into s_selw (thread 0; the caller's barrier publishes them).
+template <int TPT>
+__device__ __forceinline__ void select_thresholds(const FastArgs& g, uint32_t* hist_lds, uint64_t* s_selw,
+                                                  const SelShared& sh) {
+  const FinalizeArgs& a = g.f;
+  __shared__ uint32_t s_scan32[kGrp][kSW];
+  __shared__ uint32_t s_pick[kGrp][3];
+  __shared__ uint32_t s_thr[kGrp];
+  __shared__ uint32_t s_cutw[kGrp];
+  const int t = threadIdx.x, lane = t & (kWave - 1), wid = t / kWave;
+  const int S = (int)a.S;
+  const int G = (S + kST - 1) / kST;
+  const int* s_q = sh.q;
   int mode[kGrp], need[kGrp];
 #pragma unroll
   for (int q = 0; q < kGrp; ++q) { mode[q] = s_q[q]; need[q] = s_q[kGrp + q]; }
@@ -667,6 +696,25 @@ __device__ __forceinline__ void select_thresholds(const FastArgs& g, uint32_t* h
   uint32_t thr[kGrp] = {0u, 0u, 0u, 0u}, cut[kGrp] = {0u, 0u, 0u, 0u};
   K2_PROBE(5);
   if (part) {
+    // ---- every workgroup's histogram atomics and slot entries complete (its ready word)
+    if (wid == 0) (void)poll_tagged(g.L.head->ready, 1, G, g.spin_limit, a.stats);
+    __syncthreads();
+    // ---- every histogram load the thresholds may need (thread t owns descending bins 4t..4t+3), in one
+    // round trip
+    const int ngrp = g.hist_fb ? 4 : 3;
+    uint32_t c[kGrp][4];
+    {
+      rtkv_u32x4 h[kGrp];
+#pragma unroll
+      for (int q = 0; q < kGrp; ++q) {
+        h[q] = rtkv_u32x4{0u, 0u, 0u, 0u};
+        if (q < ngrp) h[q] = ld16_sc1(g.L.hist + q * kNBin + (kNBin - 4 - 4 * t));
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+      for (int q = 0; q < kGrp; ++q) { c[q][0] = h[q].w; c[q][1] = h[q].z; c[q][2] = h[q].y; c[q][3] = h[q].x; }
+    }
+    K2_PROBE(4);
     // ---- the bin holding each partial group's threshold: every partial group's bin counts in one
     // scan (four 32-bit DPP scans, one barrier)
     if (t < kGrp) { s_pick[t][0] = 0u; s_pick[t][1] = 0u; s_pick[t][2] = 0u; }
@@ -737,13 +785,11 @@ __device__ __forceinline__ void select_thresholds(const FastArgs& g, uint32_t* h
       thr[q] = s_thr[q];
       cut[q] = s_cutw[q];
     }
-  } else {
-    __syncthreads();  // s_ssum / s_kr
   }
   K2_PROBE(3);
   if (t != 0) return;
-  // ---- the selection words (this workgroup's phase 3 reads them from LDS), then the statistics
-  const double ssum = s_ssum;
+  // ---- the selection words (this workgroup's phase 3 reads them from LDS)
+  const double ssum = sh.ssum;
   const double mean = ssum / (double)S;
   const uint64_t mb = __builtin_bit_cast(uint64_t, mean);
   for (int q = 0; q < kGrp; ++q) {
@@ -983,6 +1029,7 @@ __device__ __forceinline__ void k2_body(const FastArgs& g, uint32_t* hist_lds) {
   __shared__ double s_sum[kSW];
   __shared__ uint32_t s_c[5][kSW];
   __shared__ uint64_t s_selw[8];
+  __shared__ SelShared sh;
   const int t = threadIdx.x, lane = t & (kWave - 1), wid = t / kWave;
   const int S = (int)a.S;
   const int G = (S + kST - 1) / kST;
@@ -1053,15 +1100,17 @@ __device__ __forceinline__ void k2_body(const FastArgs& g, uint32_t* hist_lds) {
       m1 = max(m1, (uint32_t)__shfl_xor((int)m1, o, kWave));
       ss += __shfl_xor(ss, o, kWave);
     }
-    if (lane == 0) {
-      FastPartial* pp = g.L.part + blk;
-      st_sc1(&pp->ssum, ss);
-      st_sc1(&pp->kmn, m0);
-      st_sc1(&pp->kmx, m1);
+    if (lane == 0) {  // tagged words: phase 2 takes them without waiting for this workgroup's drain
+      const uint64_t sb = __builtin_bit_cast(uint64_t, ss);
+      uint64_t* w = g.L.head->pst[blk];
+      st_sc1(w + 0, (uint64_t)(kTag | (sb & 0xffffffffull)));
+      st_sc1(w + 1, (uint64_t)(kTag | (sb >> 32)));
+      st_sc1(w + 2, (uint64_t)(kTag | (uint64_t)m0));
+      st_sc1(w + 3, (uint64_t)(kTag | (uint64_t)m1));
     }
   }
   K2_WG(3);
-  if (hist) {  // the slot of the token in its bin's list
+  if (hist) {  // the slot of the token in its bin's list (stored now; awaited only if a class is partly kept)
     const uint64_t entry = ((uint64_t)score_key(s) << 32) | (uint32_t)i;
     const uint32_t slot = hist_slot_of(tk0);
     if (valid && slot < kCap) st_sc1(g.L.slots + (size_t)hb * kCap + slot, entry);
@@ -1071,25 +1120,19 @@ __device__ __forceinline__ void k2_body(const FastArgs& g, uint32_t* hist_lds) {
     }
   }
   K2_WG(4);
-  // ---- this workgroup's slot entries, partials, scores and classes are complete
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  // (RTKV_TEST_WITHHOLD_SELECTION: the last workgroup never reports ready, so every workgroup's phase-2
-  // wait runs into its poll bound)
-  if (t == 0 && !(g.withhold == 1 && blk == G - 1)) st_sc1(&g.L.head->ready[blk], kTag);
-  // ---- phase 2 in EVERY workgroup (the same inputs, the same deterministic result): no selection hand-off
-  // between workgroups; workgroup G−1 publishes the statistics and the early host mirror
-#ifdef RTKV_SELECT_PROBE
-  if (g_k2_twice && blk == G - 1) {
-    if (t == 0) g_k2_rep = 1;
+  // ---- phase 2a: the quotas and the statistics (every workgroup's counts and partials)
+  select_quotas<TPT>(g, sh, blk == G - 1);
+  if (sh.partly) {  // (workgroup-uniform) the threshold search reads every workgroup's histogram and slots
+    // ---- this workgroup's histogram atomics and slot entries are complete
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    select_thresholds<TPT>(g, hist_lds, s_selw, false);
-    __syncthreads();
-    if (t == 0) g_k2_rep = 0;
-    __syncthreads();
+    // (RTKV_TEST_WITHHOLD_SELECTION: the last workgroup never reports ready, so every workgroup's wait in
+    // phase 2b runs into its poll bound)
+    if (t == 0 && !(g.withhold == 1 && blk == G - 1)) st_sc1(&g.L.head->ready[blk], kTag);
   }
-#endif
-  select_thresholds<TPT>(g, hist_lds, s_selw, blk == G - 1);
+  // ---- phase 2b in EVERY workgroup (the same inputs, the same deterministic result): no selection hand-off
+  // between workgroups
+  select_thresholds<TPT>(g, hist_lds, s_selw, sh);
   __syncthreads();
   K2_WG(5);
   compact_phase(g, s, l, i, valid, s_selw);

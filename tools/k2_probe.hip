@@ -119,7 +119,7 @@ int main(int argc, char** argv) {
     }
     printf("%s: %.2f us/launch (events, incl. the memset of the zeroed scratch)\n", variant ? "pipeline" : "fast", tot / reps * 1e3);
     if (variant == 0) {
-      const char* nm[8] = {"start", "counts seen", "threshold bins", "selection published", "histogram loaded", "quotas", "bin scan", "bin pick"};
+      const char* nm[8] = {"start", "counts + partials (+ ready) seen", "threshold bins", "selection published", "histogram loaded", "stats published", "bin scan", "bin pick"};
       for (int k = 1; k < 8; ++k) printf("  t(%s) = %.2f us (from the selecting workgroup's phase-2 start)\n", nm[k], ph[k] / reps);
       for (int k = 9; k < 16; ++k) if (ph[k] != 0.0) printf("  cold pass: t(%s) = %.2f us\n", nm[k - 8], ph[k] / reps);
       const char* tn[11] = {"entry", "A min/max", "scores", "histogram slots", "partials", "selection seen",
