@@ -10,9 +10,9 @@
 //
 // The scheme (D = 128: one group per head):
 //   1 vote    every vote_stride-th kept row votes, per head, for its n_vote channels of largest |x| (a
-//             wave per (head, sampled row), lane l holding channels 2l and 2l+1: n_vote rounds of a wave
-//             arg-max over 64-bit (|x| bits, ~channel) keys by butterfly shuffles, the winner's lane
-//             counting the vote in a register; one atomic per channel and wave at the end).
+//             wave per (sampled row, tensor), a head on each 16-lane DPP row: n_vote rounds of a row
+//             arg-max — lane-local best, four row_ror max steps, the lowest lane by ballot — each vote an
+//             LDS atomic; one global atomic per channel and workgroup at the end).
 //   2 select  per (tensor, head) the n_outlier channels with the most votes (at least min_votes): the
 //             layer's outlier channels, fixed for every row (KVQuant-style dense-and-sparse split with a
 //             per-layer channel list instead of per-row coordinates).
@@ -71,10 +71,6 @@ __device__ __forceinline__ uint64_t wave_max_u64(uint64_t v) {
   return v;
 }
 
-__device__ __forceinline__ uint64_t gq_key(float v, int c) {
-  return ((uint64_t)(__float_as_uint(v) & 0x7fffffffu) << 32) | (uint64_t)(0xffffffffu - (uint32_t)c);
-}
-
 // two consecutive elements (2l, 2l+1) of a row as fp32
 template <int DT> __device__ __forceinline__ void load2(const typename Dt<DT>::S* p, float& x0, float& x1) {
   if constexpr (DT == RTKV_F32) {
@@ -89,36 +85,63 @@ template <int DT> __device__ __forceinline__ void load2(const typename Dt<DT>::S
 }
 
 // ------------------------------------------------------------------------------------ 1 vote
-template <int DT>
-__global__ __launch_bounds__(256) void gq_vote_kernel(GqArgs a) {
+// A wave per (sampled kept row, tensor), lane l owning 8-element chunks
+// k·64 + l like the pack, so chunk k holds heads 4k..4k+3 on the four 16-lane DPP rows, and the row is read
+// with 16-byte coalesced loads.  Per head and round: the lane's best untaken element (largest |x| bits + 1,
+// lowest element on ties), the row's maximum by four row_ror steps, the lowest lane of the row holding it
+// by a ballot — the oracle's order (larger |x|, then lower channel) — and that lane's vote into the
+// workgroup's LDS counters, flushed to the layer's counters once per workgroup.
+template <int DT, int NCH>
+__global__ __launch_bounds__(256, 2) void gq_vote_rows_kernel(GqArgs a) {
   using S_ = typename Dt<DT>::S;
+  constexpr int F = NCH * 512;
+  __shared__ uint32_t s_votes[2 * F];
   const int lane = threadIdx.x & 63;
-  const int h = blockIdx.x, t = blockIdx.z;
-  const int wv = blockIdx.y * 4 + (threadIdx.x >> 6), nwv = gridDim.y * 4;
+  for (int i = threadIdx.x; i < 2 * F; i += blockDim.x) s_votes[i] = 0u;
+  __syncthreads();
   const int rows = gq_rows(a);
   const int vs = a.vote_stride;
   const int nsamp = (rows + vs - 1) / vs;
-  const int c0 = 2 * lane, c1 = c0 + 1;
-  const S_* base = static_cast<const S_*>(t ? a.kv.v_dev : a.kv.k_dev) + (int64_t)h * a.kv.stride_h + c0;
-  uint32_t cnt0 = 0, cnt1 = 0;
-  for (int j = wv; j < nsamp; j += nwv) {
-    const int tok = a.kept_index[j * vs];
-    if ((unsigned)tok >= (unsigned)a.kv.S) continue;  // (wave-uniform)
-    float x0, x1;
-    load2<DT>(base + (int64_t)tok * a.kv.stride_s, x0, x1);
-    const uint64_t k0 = gq_key(x0, c0), k1 = gq_key(x1, c1);
-    bool t0 = false, t1 = false;
-    for (int m = 0; m < a.n_vote; ++m) {  // the row's n_vote largest |x| of the head, one per round
-      const uint64_t mine = (t0 ? 0ull : k0) > (t1 ? 0ull : k1) ? (t0 ? 0ull : k0) : (t1 ? 0ull : k1);
-      const uint64_t best = wave_max_u64(mine);
-      const int c = (int)(0xffffffffu - (uint32_t)best);
-      if (c == c0) { t0 = true; ++cnt0; }
-      if (c == c1) { t1 = true; ++cnt1; }
+  const int gw = blockIdx.x * 4 + (threadIdx.x >> 6), nw = gridDim.x * 4;
+  for (int task = gw; task < 2 * nsamp; task += nw) {
+    const int t = task & 1, j = task >> 1;
+    const int tok = __builtin_amdgcn_readfirstlane(a.kept_index[j * vs]);
+    if ((unsigned)tok >= (unsigned)a.kv.S) continue;
+    const S_* src = static_cast<const S_*>(t ? a.kv.v_dev : a.kv.k_dev) + (int64_t)tok * a.kv.stride_s;
+    Chunk<DT> rawc[NCH];
+#pragma unroll
+    for (int k = 0; k < NCH; ++k) rawc[k] = load_chunk_nt<DT>(src + (k * 64 + lane) * 8);
+#pragma unroll
+    for (int k = 0; k < NCH; ++k) {
+      float x[8];
+      chunk_to_f32<DT>(rawc[k], x);
+      uint32_t key[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) key[e] = (__float_as_uint(x[e]) & 0x7fffffffu) + 1u;
+      for (int m = 0; m < a.n_vote; ++m) {
+        uint32_t lb = 0u;
+        int le = 0;
+#pragma unroll
+        for (int e = 0; e < 8; ++e)
+          if (key[e] > lb) { lb = key[e]; le = e; }
+        uint32_t M = lb;
+        M = max(M, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)M, 0x128, 0xf, 0xf, false));  // row_ror:8
+        M = max(M, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)M, 0x124, 0xf, 0xf, false));  // row_ror:4
+        M = max(M, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)M, 0x122, 0xf, 0xf, false));  // row_ror:2
+        M = max(M, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)M, 0x121, 0xf, 0xf, false));  // row_ror:1
+        const uint64_t b = __ballot(lb == M);
+        const uint32_t rowbits = (uint32_t)(b >> (lane & 48)) & 0xffffu;
+        if ((int)(lane & 15) == __ffs(rowbits) - 1) {  // the row's winner: one vote, its element taken
+          atomicAdd(&s_votes[t * F + (k * 64 + lane) * 8 + le], 1u);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) key[e] = e == le ? 0u : key[e];
+        }
+      }
     }
   }
-  uint32_t* v = a.votes + (int64_t)t * a.kv.H * kGqD + (int64_t)h * kGqD;
-  if (cnt0) atomicAdd(v + c0, cnt0);
-  if (cnt1) atomicAdd(v + c1, cnt1);
+  __syncthreads();
+  for (int i = threadIdx.x; i < 2 * F; i += blockDim.x)
+    if (s_votes[i]) atomicAdd(a.votes + i, s_votes[i]);
 }
 
 // ------------------------------------------------------------------------------------ 2 select
@@ -146,24 +169,30 @@ __global__ __launch_bounds__(64) void gq_select_kernel(GqArgs a) {
 // ------------------------------------------------------------------------------------ 3 pack / unpack
 // The outlier positions of this lane's chunks of tensor t: bit e of mask[k] set when element e of chunk
 // k·64 + lane is an outlier channel, its slot in bits [4e, 4e + 4) of slots[k].
+// unused[k] (optional): bit s set when outlier slot s of the chunk's head holds no channel.
+// idx: the outlier lists [2][H][n_out] (staged in LDS by gq_stage_idx: a wave's NCH·n_out lookups were a
+// chain of dependent global loads at the start of every wave).
 template <int NCH>
-__device__ __forceinline__ void gq_masks(const GqArgs& a, int t, int lane, uint32_t (&mask)[NCH], uint32_t (&slots)[NCH]) {
+__device__ __forceinline__ void gq_masks(const GqArgs& a, const int16_t* idx, int t, int lane, uint32_t (&mask)[NCH],
+                                         uint32_t (&slots)[NCH], uint32_t* unused = nullptr) {
   const int H = (int)a.kv.H;
 #pragma unroll
   for (int k = 0; k < NCH; ++k) {
     const int c = k * 64 + lane, h = c >> 4, sub = c & 15;
-    uint32_t m = 0, sl = 0;
+    uint32_t m = 0, sl = 0, un = 0;
     if (h < H) {
       for (int s = 0; s < a.n_out; ++s) {
-        const int ch = a.idx[((int64_t)t * H + h) * a.n_out + s];
+        const int ch = idx[(t * H + h) * a.n_out + s];
         if (ch >= 0 && (ch >> 3) == sub) {
           m |= 1u << (ch & 7);
           sl |= (uint32_t)s << (4 * (ch & 7));
         }
+        if (ch < 0) un |= 1u << s;
       }
     }
     mask[k] = m;
     slots[k] = sl;
+    if (unused) unused[k] = un;
   }
 }
 
@@ -190,23 +219,82 @@ template <int DT> __device__ __forceinline__ float bits_f32(uint32_t b) {
   else return Dt<DT>::load((uint16_t)b);
 }
 
+// The outlier lists [2][H][n_out] (H <= 64, n_out <= 16) into LDS by the whole workgroup (a barrier).
+__device__ __forceinline__ void gq_stage_idx(const GqArgs& a, int16_t* s_idx) {
+  const int n = 2 * (int)a.kv.H * a.n_out;
+  for (int i = threadIdx.x; i < n; i += blockDim.x) s_idx[i] = a.idx[i];
+  __syncthreads();
+}
+
+// min / max / min-nonzero-|x| combined with the lane N places round in the same row of 16 (DPP row_ror:N)
+template <int N> __device__ __forceinline__ void row16_minmax(float& mn, float& mx, float& anz) {
+  constexpr int kCtl = 0x120 + N;  // row_ror:N
+  mn = fminf(mn, __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(mn), kCtl, 0xf, 0xf, false)));
+  mx = fmaxf(mx, __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(mx), kCtl, 0xf, 0xf, false)));
+  anz = fminf(anz, __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(anz), kCtl, 0xf, 0xf, false)));
+}
+
+// element u < 4 of a register array by selects (a runtime index into a private array goes to scratch)
+template <typename T> __device__ __forceinline__ T pick4(const T (&v)[4], int u) {
+  return u == 0 ? v[0] : (u == 1 ? v[1] : (u == 2 ? v[2] : v[3]));
+}
+
 template <int DT, int NCH>
-__global__ __launch_bounds__(256) void gq_pack_kernel(GqArgs a) {
+__global__ __launch_bounds__(256, NCH <= 8 ? 4 : 2) void gq_pack_kernel(GqArgs a) {
   using S_ = typename Dt<DT>::S;
   const int lane = threadIdx.x & 63;
   const int gw = blockIdx.x * 4 + (threadIdx.x >> 6), nw = gridDim.x * 4;
   const int t = gw & 1;  // this wave's tensor (0 = K, 1 = V): its outlier masks are built once
   const int H = (int)a.kv.H;
   const int rows = gq_rows(a);
-  uint32_t mask[NCH], slots[NCH];
-  gq_masks<NCH>(a, t, lane, mask, slots);
+  // this wave's outlier maps (mask, slots, unused per chunk) in LDS, read per chunk: 3·NCH fewer live VGPRs
+  // (the kernel holds a whole fp32 row in registers, 64 VGPRs, at 4 waves per SIMD)
+  __shared__ uint32_t s_maps[4][3][NCH][64];
+  __shared__ int16_t s_idx[2 * 64 * kGqMaxOut];
+  gq_stage_idx(a, s_idx);
+  {
+    const int wv = threadIdx.x >> 6;
+    uint32_t mask[NCH], slots[NCH], unused[NCH];
+    gq_masks<NCH>(a, s_idx, t, lane, mask, slots, unused);
+#pragma unroll
+    for (int k = 0; k < NCH; ++k) {
+      s_maps[wv][0][k][lane] = mask[k];
+      s_maps[wv][1][k][lane] = slots[k];
+      s_maps[wv][2][k][lane] = unused[k];
+    }
+  }
+  const uint32_t (*maps)[NCH][64] = s_maps[threadIdx.x >> 6];  // (wave-private: no barrier needed)
   const S_* base = static_cast<const S_*>(t ? a.kv.v_dev : a.kv.k_dev);
-  for (int r = gw >> 1; r < rows; r += nw >> 1) {
-    const int tok = a.kept_index[r];
-    if ((unsigned)tok >= (unsigned)a.kv.S) continue;
-    const int lab = a.labels[tok];
+  // kT rows per batch: their tokens, then their classes and packed offsets, all in flight together (two
+  // round trips per batch instead of two per row), then the rows one by one
+  constexpr int kT = 4;
+  const int step = nw >> 1;
+  for (int r0 = gw >> 1; r0 < rows; r0 += step * kT) {
+  int tokv[kT], labv[kT];
+  int64_t roffv[kT];
+#pragma unroll
+  for (int u = 0; u < kT; ++u) {
+    const int r = r0 + u * step;
+    tokv[u] = r < rows ? a.kept_index[r] : -1;
+    roffv[u] = r < rows ? a.row_offset[r] : -1;
+  }
+#pragma unroll
+  for (int u = 0; u < kT; ++u) {  // (wave-uniform values: scalar registers)
+    tokv[u] = __builtin_amdgcn_readfirstlane(tokv[u]);
+    roffv[u] = (int64_t)(((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(roffv[u] >> 32)) << 32) |
+                         (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)roffv[u]));
+  }
+#pragma unroll
+  for (int u = 0; u < kT; ++u)
+    labv[u] = __builtin_amdgcn_readfirstlane((unsigned)tokv[u] < (unsigned)a.kv.S ? (int)a.labels[tokv[u]] : 0);
+#pragma unroll 1
+  for (int u = 0; u < kT; ++u) {
+    const int r = r0 + u * step;
+    const int tok = pick4(tokv, u);
+    if (r >= rows || (unsigned)tok >= (unsigned)a.kv.S) continue;
+    const int lab = pick4(labv, u);
     const int bits = a.bits[lab > 2 ? 0 : lab];
-    const int64_t roff = a.row_offset[r];
+    const int64_t roff = pick4(roffv, u);
     if (roff < 0 || roff + (int64_t)H * kGqD * bits / 8 > a.codes_capacity) continue;
     const S_* src = base + (int64_t)tok * a.kv.stride_s;
     Chunk<DT> rawc[NCH];
@@ -216,30 +304,50 @@ __global__ __launch_bounds__(256) void gq_pack_kernel(GqArgs a) {
 #pragma unroll
     for (int k = 0; k < NCH; ++k) {
       const int c = k * 64 + lane, h = c >> 4;
+      const uint32_t mk = maps[0][k][lane], sk = maps[1][k][lane], uk = maps[2][k][lane];
       float x[8];
       chunk_to_f32<DT>(rawc[k], x);
-      float mn = INFINITY, mx = -INFINITY;
+      float mn = INFINITY, mx = -INFINITY, anz = INFINITY;  // anz: min |x| over the nonzero elements
 #pragma unroll
       for (int e = 0; e < 8; ++e)
-        if (!((mask[k] >> e) & 1u)) { mn = fminf(mn, x[e]); mx = fmaxf(mx, x[e]); }
-#pragma unroll
-      for (int o = 1; o < 16; o <<= 1) {  // the head's 16 lanes: a DPP row
-        mn = fminf(mn, __shfl_xor(mn, o, kWave));
-        mx = fmaxf(mx, __shfl_xor(mx, o, kWave));
-      }
-      const RowParams rp = row_params<DT>(mn, mx, bits);
+        if (!((mk >> e) & 1u)) {
+          mn = fminf(mn, x[e]);
+          mx = fmaxf(mx, x[e]);
+          if constexpr (DT != RTKV_F16) {  // (fp16's fast quotient needs no lower bound)
+            const float ax = __builtin_fabsf(x[e]);
+            anz = ax != 0.f ? fminf(anz, ax) : anz;
+          }
+        }
+      // the head's 16 lanes are a DPP row: rotations by 8, 4, 2, 1 within it leave every lane the row's value
+      row16_minmax<8>(mn, mx, anz);
+      row16_minmax<4>(mn, mx, anz);
+      row16_minmax<2>(mn, mx, anz);
+      row16_minmax<1>(mn, mx, anz);
+      const RowParams rp = row_params<DT>(mn, mx, bits, anz);
       const int64_t mrow = ((int64_t)r * 2 + t) * H + h;
       if ((lane & 15) == 0) {
         static_cast<S_*>(a.meta)[mrow * 2] = Dt<DT>::store(rp.scale);
         static_cast<S_*>(a.meta)[mrow * 2 + 1] = Dt<DT>::store(rp.zp);
-        for (int s = 0; s < a.n_out; ++s)  // unused outlier slots of the head hold zero
-          if (a.idx[((int64_t)t * H + h) * a.n_out + s] < 0) store_bits<DT>(a.raw, mrow * a.n_out + s, 0u);
+        for (uint32_t m = uk; m; m &= m - 1)  // unused outlier slots of the head hold zero
+          store_bits<DT>(a.raw, mrow * a.n_out + (__ffs(m) - 1), 0u);
       }
+      // the quotient x / scale: the proven fast form where the head's range admits it (fast_div_ok), else
+      // the IEEE division — the same value either way (quant_impl.h fast_quotient)
+      // (wave-uniform choice: the four heads of the chunk all admit it, as almost every head does)
+      const bool fast = __all(rp.fast && !(mn != mn) && !(mx != mx));
       uint32_t q[8];
+      if (fast) {
 #pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        const bool out = ((mask[k] >> e) & 1u) || x[e] != x[e];
-        q[e] = out ? 0u : (uint32_t)quant_code<DT>(x[e], rp);
+        for (int e = 0; e < 8; ++e) {
+          const bool out = ((mk >> e) & 1u) || x[e] != x[e];
+          q[e] = out ? 0u : (uint32_t)code_from_quotient<DT>(fast_quotient(x[e], rp.scale, rp.rcp), rp);
+        }
+      } else {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const bool out = ((mk >> e) & 1u) || x[e] != x[e];
+          q[e] = out ? 0u : (uint32_t)code_from_quotient<DT>(x[e] / rp.scale, rp);
+        }
       }
       uint8_t* dst = dst_row + (int64_t)c * bits;
       switch (bits) {
@@ -247,12 +355,13 @@ __global__ __launch_bounds__(256) void gq_pack_kernel(GqArgs a) {
         case 4: pack_store<4>(dst, q, true); break;
         default: pack_store<8>(dst, q, true); break;
       }
-      for (uint32_t m = mask[k]; m; m &= m - 1) {  // the outlier channels' raw values
+      for (uint32_t m = mk; m; m &= m - 1) {  // the outlier channels' raw values
         const int e = __ffs(m) - 1;
-        const int s = (int)((slots[k] >> (4 * e)) & 15u);
+        const int s = (int)((sk >> (4 * e)) & 15u);
         store_bits<DT>(a.raw, mrow * a.n_out + s, chunk_bits<DT>(rawc[k], e));
       }
     }
+  }
   }
 }
 
@@ -265,8 +374,10 @@ __global__ __launch_bounds__(256) void gq_unpack_kernel(GqArgs a) {
   const int t = a.which, H = (int)a.kv.H;
   const int64_t F = (int64_t)H * kGqD;
   const int rows = gq_rows(a);
+  __shared__ int16_t s_idx[2 * 64 * kGqMaxOut];
+  gq_stage_idx(a, s_idx);
   uint32_t mask[NCH], slots[NCH];
-  gq_masks<NCH>(a, t, lane, mask, slots);
+  gq_masks<NCH>(a, s_idx, t, lane, mask, slots);
   for (int r = gw; r < rows; r += nw) {
     const int tok = a.kept_index[r];
     if ((unsigned)tok >= (unsigned)a.kv.S) continue;
@@ -476,6 +587,20 @@ template <int DT> static int launch_gq_pack(const GqArgs& a, unsigned blocks, hi
   set_error("gq: H must be 4..32, 40, 48 or 64");
   return RTKV_ERR_UNSUPPORTED;
 }
+template <int DT> static int launch_gq_vote(const GqArgs& a, unsigned blocks, hipStream_t st) {
+  const int nch = (int)(a.kv.H * kGqD / 512);
+#define RTKV_GQ(N)                                                                      \
+  if (nch == N) {                                                                       \
+    hipLaunchKernelGGL((gq_vote_rows_kernel<DT, N>), dim3(blocks), dim3(256), 0, st, a); \
+    RTKV_HIP_CHECK(hipGetLastError());                                                  \
+    return RTKV_OK;                                                                     \
+  }
+  RTKV_GQ(1) RTKV_GQ(2) RTKV_GQ(3) RTKV_GQ(4) RTKV_GQ(5) RTKV_GQ(6) RTKV_GQ(7) RTKV_GQ(8) RTKV_GQ(10) RTKV_GQ(12)
+  RTKV_GQ(16)
+#undef RTKV_GQ
+  set_error("gq: H must be 4..32, 40, 48 or 64");
+  return RTKV_ERR_UNSUPPORTED;
+}
 template <int DT> static int launch_gq_unpack(const GqArgs& a, unsigned blocks, hipStream_t st) {
   const int nch = (int)(a.kv.H * kGqD / 512);
 #define RTKV_GQ(N)                                                                      \
@@ -514,17 +639,19 @@ int rtkv_gq_outlier_channels(const rtkv_kv_desc* kv, const int32_t* kept_index_d
   a.votes = static_cast<uint32_t*>(workspace_dev);
   a.idx = outlier_idx_dev;
   RTKV_HIP_CHECK(hipMemsetAsync(a.votes, 0, rtkv_gq_workspace_size(kv->H, kv->D), st));
-  // sampled rows spread over (heads × splits × 2 tensors) workgroups of 4 waves: ~16 rows per wave
+  // (sampled row, tensor) tasks over workgroups of 4 waves, ~2 tasks per wave: a wave is a latency chain
+  // (one row in flight, then its rounds), so the grid supplies the parallelism (each workgroup flushes
+  // its LDS counters once)
   const int64_t nsamp = (row_capacity + g->vote_stride - 1) / g->vote_stride;
-  int64_t splits = (nsamp + 63) / 64;
-  splits = splits < 1 ? 1 : (splits > 64 ? 64 : splits);
-  const dim3 grid((unsigned)kv->H, (unsigned)splits, 2u);
+  int64_t blocks = (2 * nsamp + 7) / 8;
+  blocks = blocks < 1 ? 1 : (blocks > 4096 ? 4096 : blocks);
+  int rc2 = RTKV_OK;
   switch (kv->dtype) {
-    case RTKV_F16: hipLaunchKernelGGL((gq_vote_kernel<RTKV_F16>), grid, dim3(256), 0, st, a); break;
-    case RTKV_BF16: hipLaunchKernelGGL((gq_vote_kernel<RTKV_BF16>), grid, dim3(256), 0, st, a); break;
-    default: hipLaunchKernelGGL((gq_vote_kernel<RTKV_F32>), grid, dim3(256), 0, st, a); break;
+    case RTKV_F16: rc2 = launch_gq_vote<RTKV_F16>(a, (unsigned)blocks, st); break;
+    case RTKV_BF16: rc2 = launch_gq_vote<RTKV_BF16>(a, (unsigned)blocks, st); break;
+    default: rc2 = launch_gq_vote<RTKV_F32>(a, (unsigned)blocks, st); break;
   }
-  RTKV_HIP_CHECK(hipGetLastError());
+  if (rc2) return rc2;
   hipLaunchKernelGGL(gq_select_kernel, dim3((unsigned)kv->H, 2u), dim3(64), 0, st, a);
   RTKV_HIP_CHECK(hipGetLastError());
   return RTKV_OK;
