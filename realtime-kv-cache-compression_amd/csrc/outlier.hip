@@ -23,6 +23,7 @@
 //             dtype, the outlier channels' raw values beside them.  A head's 16 chunks of 8 channels sit
 //             on 16 consecutive lanes, so its min/max is a 4-step xor butterfly inside a DPP row.
 // Bytes per kept row and tensor: F·w/8 codes + 2·H·e meta + H·n_outlier·e raw values.
+#include <cstdlib>
 #include <cstring>
 
 #include "quant_impl.h"
@@ -84,17 +85,42 @@ template <int DT> __device__ __forceinline__ void load2(const typename Dt<DT>::S
   }
 }
 
+// ---- DPP inside a 16-lane row (a head's 16 chunks of one pack chunk index): lane j ↔ j^8 (row_ror:8),
+// j ↔ j^7 (row_half_mirror), j ↔ j^2 / j^1 (quad_perm), and lane n broadcast to its row (row_newbcast:n)
+constexpr int kDppRor8 = 0x128, kDppHalfMirror = 0x141, kDppXor2 = 0x4E, kDppXor1 = 0xB1, kDppRowBcast = 0x150;
+template <int CTL> __device__ __forceinline__ uint32_t dppu(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTL, 0xf, 0xf, false);
+}
+template <int CTL> __device__ __forceinline__ float dppf(float v) { return __uint_as_float(dppu<CTL>(__float_as_uint(v))); }
+// lane 2c of the row to every lane of it (c compile-time after unrolling)
+__device__ __forceinline__ uint32_t row_bcast2(uint32_t v, int c) {
+  switch (c) {
+    case 0: return dppu<kDppRowBcast + 0>(v);
+    case 1: return dppu<kDppRowBcast + 2>(v);
+    case 2: return dppu<kDppRowBcast + 4>(v);
+    case 3: return dppu<kDppRowBcast + 6>(v);
+    case 4: return dppu<kDppRowBcast + 8>(v);
+    case 5: return dppu<kDppRowBcast + 10>(v);
+    case 6: return dppu<kDppRowBcast + 12>(v);
+    default: return dppu<kDppRowBcast + 14>(v);
+  }
+}
+
 // ------------------------------------------------------------------------------------ 1 vote
-// A wave per (sampled kept row, tensor), lane l owning 8-element chunks
-// k·64 + l like the pack, so chunk k holds heads 4k..4k+3 on the four 16-lane DPP rows, and the row is read
-// with 16-byte coalesced loads.  Per head and round: the lane's best untaken element (largest |x| bits + 1,
-// lowest element on ties), the row's maximum by four row_ror steps, the lowest lane of the row holding it
-// by a ballot — the oracle's order (larger |x|, then lower channel) — and that lane's vote into the
-// workgroup's LDS counters, flushed to the layer's counters once per workgroup.
+// A wave per (sampled kept row, tensor), lane l owning 8-element chunks k·64 + l like the pack, so chunk k
+// holds heads 4k..4k+3 on the four 16-lane DPP rows, and the row is read with 16-byte coalesced loads.  Per
+// head and round: the lane's best untaken element (largest |x| bits + 1, lowest element on ties), the row's
+// maximum by four row_ror steps, the lowest lane of the row holding it by a ballot — the oracle's order
+// (larger |x|, then lower channel) — and that lane's vote into the workgroup's LDS counters.  The rounds run
+// over 8 chunks at a time (a round of every chunk, then the next round), so eight independent DPP / ballot
+// chains interleave instead of one chunk's rounds running back to back.  1024-thread workgroups, one per
+// CU: the LDS counters are flushed to the layer's counters (one atomic per nonzero channel) once per 16
+// waves.
 template <int DT, int NCH>
-__global__ __launch_bounds__(256, 2) void gq_vote_rows_kernel(GqArgs a) {
+__global__ __launch_bounds__(1024) void gq_vote_rows_kernel(GqArgs a) {
   using S_ = typename Dt<DT>::S;
   constexpr int F = NCH * 512;
+  constexpr int kWaves = 16;
   __shared__ uint32_t s_votes[2 * F];
   const int lane = threadIdx.x & 63;
   for (int i = threadIdx.x; i < 2 * F; i += blockDim.x) s_votes[i] = 0u;
@@ -102,39 +128,100 @@ __global__ __launch_bounds__(256, 2) void gq_vote_rows_kernel(GqArgs a) {
   const int rows = gq_rows(a);
   const int vs = a.vote_stride;
   const int nsamp = (rows + vs - 1) / vs;
-  const int gw = blockIdx.x * 4 + (threadIdx.x >> 6), nw = gridDim.x * 4;
+  const int gw = blockIdx.x * kWaves + (threadIdx.x >> 6), nw = gridDim.x * kWaves;
   for (int task = gw; task < 2 * nsamp; task += nw) {
     const int t = task & 1, j = task >> 1;
     const int tok = __builtin_amdgcn_readfirstlane(a.kept_index[j * vs]);
     if ((unsigned)tok >= (unsigned)a.kv.S) continue;
-    const S_* src = static_cast<const S_*>(t ? a.kv.v_dev : a.kv.k_dev) + (int64_t)tok * a.kv.stride_s;
-    Chunk<DT> rawc[NCH];
+    const S_* src = static_cast<const S_*>(t ? a.kv.v_dev : a.kv.k_dev) + (int64_t)tok * a.kv.stride_s + lane * 8;
+    uint32_t* sv = s_votes + t * F + lane * 8;
+    if constexpr (DT != RTKV_F32) {
+      // 16-bit dtypes: composite keys (|x| bits + 1)·2^16 + (15 − lane % 16)·8 + (7 − e), unique within a head
+      // and ordered as the oracle's (larger |x|, then lower channel).  Round m's row maximum M_m is then the
+      // winner itself, and a lane's candidate for round m + 1 is its largest key below M_m: the smallest
+      // (M_m − 1 − key) over its elements, keys at or above M_m wrapping out of range — no taken flags, no
+      // arg-max bookkeeping, no ballot: 1.5 VALU per element and round instead of 5.
+      const uint32_t lp = (15u - (uint32_t)(lane & 15)) << 3;
 #pragma unroll
-    for (int k = 0; k < NCH; ++k) rawc[k] = load_chunk_nt<DT>(src + (k * 64 + lane) * 8);
+      for (int k0 = 0; k0 < NCH; k0 += 8) {
+        constexpr int kG = NCH < 8 ? NCH : 8;
+        uint32_t key[kG][8];
 #pragma unroll
-    for (int k = 0; k < NCH; ++k) {
-      float x[8];
-      chunk_to_f32<DT>(rawc[k], x);
-      uint32_t key[8];
+        for (int i = 0; i < kG; ++i) {
+          if (k0 + i < NCH) {
+            const Chunk<DT> c = load_chunk_nt<DT>(src + (k0 + i) * 512);
+            const uint32_t w4[4] = {c.a.x, c.a.y, c.a.z, c.a.w};
 #pragma unroll
-      for (int e = 0; e < 8; ++e) key[e] = (__float_as_uint(x[e]) & 0x7fffffffu) + 1u;
+            for (int e = 0; e < 8; ++e)
+              key[i][e] = ((((w4[e >> 1] >> (16 * (e & 1))) & 0x7fffu) + 1u) << 16) | lp | (7u - (uint32_t)e);
+          }
+        }
+        uint32_t bound[kG], won[kG];  // bound: the previous round's winner (exclusive)
+#pragma unroll
+        for (int i = 0; i < kG; ++i) { bound[i] = ~0u; won[i] = 0u; }
+        for (int m = 0; m < a.n_vote; ++m) {
+#pragma unroll
+          for (int i = 0; i < kG; ++i) {
+            if (k0 + i >= NCH) continue;
+            const uint32_t b1 = bound[i] - 1u;
+            uint32_t md = ~0u;
+#pragma unroll
+            for (int e = 0; e < 8; ++e) md = min(md, b1 - key[i][e]);
+            const uint32_t c = md <= b1 ? b1 - md : 0u;
+            uint32_t M = c;
+            M = max(M, dppu<0x128>(M));  // row_ror:8
+            M = max(M, dppu<0x124>(M));  // row_ror:4
+            M = max(M, dppu<0x122>(M));  // row_ror:2
+            M = max(M, dppu<0x121>(M));  // row_ror:1
+            won[i] |= (c == M && M != 0u) ? 1u << (7u - (M & 7u)) : 0u;
+            bound[i] = M != 0u ? M : 1u;  // (no key left in the row: later rounds find none either)
+          }
+        }
+#pragma unroll
+        for (int i = 0; i < kG; ++i)
+          if (k0 + i < NCH)
+            for (uint32_t w = won[i]; w; w &= w - 1) atomicAdd(sv + (k0 + i) * 512 + (__ffs(w) - 1), 1u);
+      }
+      continue;
+    }
+#pragma unroll
+    for (int k0 = 0; k0 < NCH; k0 += 8) {
+      constexpr int kG = NCH < 8 ? NCH : 8;
+      uint32_t key[kG][8];
+#pragma unroll
+      for (int i = 0; i < kG; ++i) {
+        if (k0 + i < NCH) {
+          float x[8];
+          chunk_to_f32<DT>(load_chunk_nt<DT>(src + (k0 + i) * 512), x);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) key[i][e] = (__float_as_uint(x[e]) & 0x7fffffffu) + 1u;
+        }
+      }
+      // fp32 (exact 32-bit |x| keys leave no room for the channel): per round the lane's best untaken
+      // element, the row maximum, the row's lowest lane holding it by ballot; the winner's vote to LDS.
+      // (A branch-free form of these rounds — the taken element masked out, votes kept as bits — issued 57
+      // instead of 41 VALU per chunk and round and measured 42 against 36 us at cfg3.)
       for (int m = 0; m < a.n_vote; ++m) {
-        uint32_t lb = 0u;
-        int le = 0;
 #pragma unroll
-        for (int e = 0; e < 8; ++e)
-          if (key[e] > lb) { lb = key[e]; le = e; }
-        uint32_t M = lb;
-        M = max(M, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)M, 0x128, 0xf, 0xf, false));  // row_ror:8
-        M = max(M, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)M, 0x124, 0xf, 0xf, false));  // row_ror:4
-        M = max(M, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)M, 0x122, 0xf, 0xf, false));  // row_ror:2
-        M = max(M, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)M, 0x121, 0xf, 0xf, false));  // row_ror:1
-        const uint64_t b = __ballot(lb == M);
-        const uint32_t rowbits = (uint32_t)(b >> (lane & 48)) & 0xffffu;
-        if ((int)(lane & 15) == __ffs(rowbits) - 1) {  // the row's winner: one vote, its element taken
-          atomicAdd(&s_votes[t * F + (k * 64 + lane) * 8 + le], 1u);
+        for (int i = 0; i < kG; ++i) {
+          if (k0 + i >= NCH) continue;
+          uint32_t lb = 0u;
+          int le = 0;
 #pragma unroll
-          for (int e = 0; e < 8; ++e) key[e] = e == le ? 0u : key[e];
+          for (int e = 0; e < 8; ++e)
+            if (key[i][e] > lb) { lb = key[i][e]; le = e; }
+          uint32_t M = lb;
+          M = max(M, dppu<0x128>(M));  // row_ror:8
+          M = max(M, dppu<0x124>(M));  // row_ror:4
+          M = max(M, dppu<0x122>(M));  // row_ror:2
+          M = max(M, dppu<0x121>(M));  // row_ror:1
+          const uint64_t b = __ballot(lb == M);
+          const uint32_t rowbits = (uint32_t)(b >> (lane & 48)) & 0xffffu;
+          if ((int)(lane & 15) == __ffs(rowbits) - 1) {  // the row's winner: one vote, its element taken
+            atomicAdd(sv + (k0 + i) * 512 + le, 1u);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) key[i][e] = e == le ? 0u : key[i][e];
+          }
         }
       }
     }
@@ -226,27 +313,138 @@ __device__ __forceinline__ void gq_stage_idx(const GqArgs& a, int16_t* s_idx) {
   __syncthreads();
 }
 
-// min / max / min-nonzero-|x| combined with the lane N places round in the same row of 16 (DPP row_ror:N)
-template <int N> __device__ __forceinline__ void row16_minmax(float& mn, float& mx, float& anz) {
-  constexpr int kCtl = 0x120 + N;  // row_ror:N
-  mn = fminf(mn, __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(mn), kCtl, 0xf, 0xf, false)));
-  mx = fmaxf(mx, __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(mx), kCtl, 0xf, 0xf, false)));
-  anz = fminf(anz, __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(anz), kCtl, 0xf, 0xf, false)));
-}
-
 // element u < 4 of a register array by selects (a runtime index into a private array goes to scratch)
 template <typename T> __device__ __forceinline__ T pick4(const T (&v)[4], int u) {
   return u == 0 ? v[0] : (u == 1 ? v[1] : (u == 2 ? v[2] : v[3]));
 }
 
+// A head's statistics over its non-outlier channels: min, max (NaN ignored, as fminf/fmaxf and the oracle's
+// `<` / `>`), and the smallest nonzero |x| as the key 2|x| − 1 (unsigned; zero → ~0u, NaN above every
+// number) for the fast-division gate.
+struct GqStat { float mn, mx; uint32_t az; };
+__device__ __forceinline__ GqStat gq_comb(const GqStat& a, const GqStat& b) {
+  return {fminf(a.mn, b.mn), fmaxf(a.mx, b.mx), a.az < b.az ? a.az : b.az};
+}
+template <int CTL> __device__ __forceinline__ GqStat gq_dpp(const GqStat& s) {
+  return {dppf<CTL>(s.mn), dppf<CTL>(s.mx), dppu<CTL>(s.az)};
+}
+__device__ __forceinline__ GqStat gq_pick(bool c, const GqStat& a, const GqStat& b) {
+  return {c ? a.mn : b.mn, c ? a.mx : b.mx, c ? a.az : b.az};
+}
+__device__ __forceinline__ float gq_anz(uint32_t az) { return az == ~0u ? INFINITY : __uint_as_float((az + 1u) >> 1); }
+
+// Transposed row reduction of 8 chunks' statistics: s[i] holds this lane's statistics of chunk i; on return
+// every lane j of a 16-lane row holds the ROW's statistics of chunk (j >> 1) & 7.  Each butterfly step
+// halves the chunks a lane carries (it keeps one half, sends the other to its partner): 4 + 2 + 1 + 1 DPP
+// operations per statistic instead of 8 chunks × 4 steps, and the row parameters are then computed once per
+// lane instead of once per chunk.  The partners (j^8, j^7, j^2, j^1) span all 16 lanes.
+__device__ __forceinline__ GqStat gq_row_transpose(GqStat (&s)[8], int lane) {
+  const bool b3 = lane & 8, b2 = lane & 4, b1 = lane & 2;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) s[i] = gq_comb(gq_pick(b3, s[i + 4], s[i]), gq_dpp<kDppRor8>(gq_pick(b3, s[i], s[i + 4])));
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+    s[i] = gq_comb(gq_pick(b2, s[i + 2], s[i]), gq_dpp<kDppHalfMirror>(gq_pick(b2, s[i], s[i + 2])));
+  s[0] = gq_comb(gq_pick(b1, s[1], s[0]), gq_dpp<kDppXor2>(gq_pick(b1, s[0], s[1])));
+  return gq_comb(s[0], gq_dpp<kDppXor1>(s[0]));
+}
+
+// The outlier channels of a chunk set to NaN (all-ones bits: a quiet NaN in every dtype), in place: the row
+// statistics then ignore them like any NaN, and their codes come out 0 like a NaN element's (the saturating
+// conversion of a NaN).  2 VALU per element (fp32) / per pair (16-bit).
+template <int DT> __device__ __forceinline__ void gq_nan_outliers(Chunk<DT>& c, uint32_t mk) {
+  auto m1 = [&](int e) { return (uint32_t)((int32_t)(mk << (31 - e)) >> 31); };  // v_bfe_i32
+  if constexpr (DT == RTKV_F32) {
+    c.a.x = __uint_as_float(__float_as_uint(c.a.x) | m1(0)); c.a.y = __uint_as_float(__float_as_uint(c.a.y) | m1(1));
+    c.a.z = __uint_as_float(__float_as_uint(c.a.z) | m1(2)); c.a.w = __uint_as_float(__float_as_uint(c.a.w) | m1(3));
+    c.b.x = __uint_as_float(__float_as_uint(c.b.x) | m1(4)); c.b.y = __uint_as_float(__float_as_uint(c.b.y) | m1(5));
+    c.b.z = __uint_as_float(__float_as_uint(c.b.z) | m1(6)); c.b.w = __uint_as_float(__float_as_uint(c.b.w) | m1(7));
+  } else {
+    auto m2 = [&](int j) { return (m1(2 * j) & 0xffffu) | (m1(2 * j + 1) & 0xffff0000u); };  // v_bfi_b32
+    c.a.x |= m2(0); c.a.y |= m2(1); c.a.z |= m2(2); c.a.w |= m2(3);
+  }
+}
+
+// This lane's statistics of one (outlier-free) chunk.
+template <int DT> __device__ __forceinline__ GqStat gq_chunk_stat(const Chunk<DT>& c) {
+  GqStat s{INFINITY, -INFINITY, ~0u};
+  if constexpr (DT == RTKV_F16) {  // packed f16 min/max (NaN ignored, as fminf); no |x| gate for fp16
+    const _Float16 pinf = (_Float16)INFINITY;
+    h2_t mn2 = {pinf, pinf}, mx2 = {-pinf, -pinf};
+    const uint32_t w4[4] = {c.a.x, c.a.y, c.a.z, c.a.w};
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      mn2 = __builtin_elementwise_min(mn2, as_h2(w4[j]));
+      mx2 = __builtin_elementwise_max(mx2, as_h2(w4[j]));
+    }
+    s.mn = fminf((float)mn2[0], (float)mn2[1]);
+    s.mx = fmaxf((float)mx2[0], (float)mx2[1]);
+  } else {
+    float x[8];
+    chunk_to_f32<DT>(c, x);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      s.mn = fminf(s.mn, x[e]);
+      s.mx = fmaxf(s.mx, x[e]);
+      const uint32_t k = (__float_as_uint(x[e]) << 1) - 1u;
+      s.az = k < s.az ? k : s.az;
+    }
+  }
+  return s;
+}
+
+// Codes of one chunk (outliers already NaN) at width W: clamp(rint(RN(RN(x / s) + zp)), 0, qmax) as in
+// dynamic_quantization.py:120-121, in integers — the saturating v_cvt_u32_f32 maps negative values, −0 and
+// NaN to 0 (the float clamp's result for them), then a min with qmax.  FAST: the proven quotient from the
+// head's reciprocal (quant_impl.h fast_quotient; without its e == 0 guard, which only keeps the sign of a
+// zero quotient that no code sees).  fp16 FAST: K4's native packed-f16 form (f16_chunk_codes).
+template <int DT, int W, bool FAST>
+__device__ __forceinline__ void gq_chunk_codes(const Chunk<DT>& c, float s, float r, float zp, uint32_t qmaxU,
+                                               uint8_t* dst) {
+  uint32_t q[8];
+  if constexpr (DT == RTKV_F16 && FAST) {
+    const _Float16 zph = (_Float16)zp;
+    const h2_t zp2 = {zph, zph};
+    uint32_t dq[4];
+    f16_chunk_codes<false>(c.a, s, r, zp2, zp2, (_Float16)(float)qmaxU, q, dq);
+  } else {
+    float x[8];
+    chunk_to_f32<DT>(c, x);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      float qd;
+      if constexpr (FAST) {
+        const float q0 = x[e] * r;
+        qd = __builtin_fmaf(__builtin_fmaf(-q0, s, x[e]), r, q0);
+      } else {
+        qd = x[e] / s;
+      }
+      const float t = __builtin_rintf(Dt<DT>::rnd(Dt<DT>::rnd(qd) + zp));
+      uint32_t u;
+      asm("v_cvt_u32_f32 %0, %1" : "=v"(u) : "v"(t));
+      q[e] = u < qmaxU ? u : qmaxU;
+    }
+  }
+  pack_store<W>(dst, q, true);
+}
+
+// A wave per (kept row, tensor), lane l owning 8-element chunks k·64 + l (16-byte coalesced loads); chunk k
+// holds heads 4k..4k+3 on the wave's four 16-lane rows.  Per row: the outlier channels' raw values stored and
+// set to NaN; per chunk the lane's statistics; per 8 chunks one transposed row reduction, so lane j of a row
+// holds the statistics of chunk 8g + ((j >> 1) & 7) and computes that head's (scale, zero-point, reciprocal)
+// once (row_params: the reference's formulas, dynamic_quantization.py:79-93); the parameters go back to every
+// lane of the row by row_newbcast; the codes of the row's width (compile-time per row) with the fast quotient
+// when every head of the row admits it (wave-uniform), else the IEEE division.
 template <int DT, int NCH>
 __global__ __launch_bounds__(256, NCH <= 8 ? 4 : 2) void gq_pack_kernel(GqArgs a) {
   using S_ = typename Dt<DT>::S;
+  constexpr int NG = (NCH + 7) / 8;  // groups of 8 chunks (one transposed reduction each)
   const int lane = threadIdx.x & 63;
   const int gw = blockIdx.x * 4 + (threadIdx.x >> 6), nw = gridDim.x * 4;
   const int t = gw & 1;  // this wave's tensor (0 = K, 1 = V): its outlier masks are built once
   const int H = (int)a.kv.H;
   const int rows = gq_rows(a);
+  const int cj = (lane >> 1) & 7;  // the chunk (within a group) whose head parameters this lane computes
   // this wave's outlier maps (mask, slots, unused per chunk) in LDS, read per chunk: 3·NCH fewer live VGPRs
   // (the kernel holds a whole fp32 row in registers, 64 VGPRs, at 4 waves per SIMD)
   __shared__ uint32_t s_maps[4][3][NCH][64];
@@ -298,68 +496,89 @@ __global__ __launch_bounds__(256, NCH <= 8 ? 4 : 2) void gq_pack_kernel(GqArgs a
     if (roff < 0 || roff + (int64_t)H * kGqD * bits / 8 > a.codes_capacity) continue;
     const S_* src = base + (int64_t)tok * a.kv.stride_s;
     Chunk<DT> rawc[NCH];
+    const S_* src_lane = src + lane * 8;
 #pragma unroll
-    for (int k = 0; k < NCH; ++k) rawc[k] = load_chunk_nt<DT>(src + (k * 64 + lane) * 8);
-    uint8_t* dst_row = a.codes[t] + roff;
+    for (int k = 0; k < NCH; ++k) rawc[k] = load_chunk_nt<DT>(src_lane + k * 512);
+    // this row and tensor's first head (32-bit indices: rows·2·H·max(2, n_out) < 2^31); the opaque copy of
+    // lane >> 4 keeps the per-chunk head offsets from being hoisted out of the row loop as 64-bit values
+    // (register spills)
+    const int mrow0 = (r * 2 + t) * H;
+    int hrow = lane >> 4;
+    asm volatile("" : "+v"(hrow));
+    // the outlier channels' raw values, bit for bit; then NaN in their place
 #pragma unroll
     for (int k = 0; k < NCH; ++k) {
-      const int c = k * 64 + lane, h = c >> 4;
-      const uint32_t mk = maps[0][k][lane], sk = maps[1][k][lane], uk = maps[2][k][lane];
-      float x[8];
-      chunk_to_f32<DT>(rawc[k], x);
-      float mn = INFINITY, mx = -INFINITY, anz = INFINITY;  // anz: min |x| over the nonzero elements
-#pragma unroll
-      for (int e = 0; e < 8; ++e)
-        if (!((mk >> e) & 1u)) {
-          mn = fminf(mn, x[e]);
-          mx = fmaxf(mx, x[e]);
-          if constexpr (DT != RTKV_F16) {  // (fp16's fast quotient needs no lower bound)
-            const float ax = __builtin_fabsf(x[e]);
-            anz = ax != 0.f ? fminf(anz, ax) : anz;
-          }
-        }
-      // the head's 16 lanes are a DPP row: rotations by 8, 4, 2, 1 within it leave every lane the row's value
-      row16_minmax<8>(mn, mx, anz);
-      row16_minmax<4>(mn, mx, anz);
-      row16_minmax<2>(mn, mx, anz);
-      row16_minmax<1>(mn, mx, anz);
-      const RowParams rp = row_params<DT>(mn, mx, bits, anz);
-      const int64_t mrow = ((int64_t)r * 2 + t) * H + h;
-      if ((lane & 15) == 0) {
-        static_cast<S_*>(a.meta)[mrow * 2] = Dt<DT>::store(rp.scale);
-        static_cast<S_*>(a.meta)[mrow * 2 + 1] = Dt<DT>::store(rp.zp);
-        for (uint32_t m = uk; m; m &= m - 1)  // unused outlier slots of the head hold zero
-          store_bits<DT>(a.raw, mrow * a.n_out + (__ffs(m) - 1), 0u);
-      }
-      // the quotient x / scale: the proven fast form where the head's range admits it (fast_div_ok), else
-      // the IEEE division — the same value either way (quant_impl.h fast_quotient)
-      // (wave-uniform choice: the four heads of the chunk all admit it, as almost every head does)
-      const bool fast = __all(rp.fast && !(mn != mn) && !(mx != mx));
-      uint32_t q[8];
-      if (fast) {
-#pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          const bool out = ((mk >> e) & 1u) || x[e] != x[e];
-          q[e] = out ? 0u : (uint32_t)code_from_quotient<DT>(fast_quotient(x[e], rp.scale, rp.rcp), rp);
-        }
-      } else {
-#pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          const bool out = ((mk >> e) & 1u) || x[e] != x[e];
-          q[e] = out ? 0u : (uint32_t)code_from_quotient<DT>(x[e] / rp.scale, rp);
+      __builtin_amdgcn_sched_barrier(0);  // one chunk's temporaries live at a time
+      const uint32_t mk = maps[0][k][lane];
+      if (mk) {
+        const uint32_t sk = maps[1][k][lane];
+        const int mrow = mrow0 + 4 * k + hrow;
+        for (uint32_t m = mk; m; m &= m - 1) {
+          const int e = __ffs(m) - 1;
+          store_bits<DT>(a.raw, mrow * a.n_out + (int)((sk >> (4 * e)) & 15u), chunk_bits<DT>(rawc[k], e));
         }
       }
-      uint8_t* dst = dst_row + (int64_t)c * bits;
-      switch (bits) {
-        case 2: pack_store<2>(dst, q, true); break;
-        case 4: pack_store<4>(dst, q, true); break;
-        default: pack_store<8>(dst, q, true); break;
+      gq_nan_outliers<DT>(rawc[k], mk);
+    }
+    // head parameters: lane j of a row owns chunk 8g + cj of each group g
+    float sc[NG], zp[NG], rc[NG];
+    bool fast = true;
+    const float qmax = (float)((1u << bits) - 1u);
+#pragma unroll
+    for (int g = 0; g < NG; ++g) {
+      GqStat st[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        __builtin_amdgcn_sched_barrier(0);
+        st[i] = 8 * g + i < NCH ? gq_chunk_stat<DT>(rawc[8 * g + i]) : GqStat{INFINITY, -INFINITY, ~0u};
       }
-      for (uint32_t m = mk; m; m &= m - 1) {  // the outlier channels' raw values
-        const int e = __ffs(m) - 1;
-        const int s = (int)((sk >> (4 * e)) & 15u);
-        store_bits<DT>(a.raw, mrow * a.n_out + s, chunk_bits<DT>(rawc[k], e));
+      const GqStat hs = gq_row_transpose(st, lane);
+      const RowParams rp = row_params<DT>(hs.mn, hs.mx, bits, gq_anz(hs.az));
+      sc[g] = rp.scale;
+      zp[g] = rp.zp;
+      rc[g] = rp.rcp;
+      fast = fast && rp.fast && !(hs.mn != hs.mn) && !(hs.mx != hs.mx);
+      const int k = 8 * g + cj;
+      if (k < NCH) {
+        const int mrow = mrow0 + 4 * k + hrow;
+        if (!(lane & 1)) {  // {scale, zero_point} of the head, in the dtype, one store
+          if constexpr (DT == RTKV_F32)
+            *reinterpret_cast<float2*>(static_cast<float*>(a.meta) + mrow * 2) = make_float2(rp.scale, rp.zp);
+          else
+            *reinterpret_cast<uint32_t*>(static_cast<S_*>(a.meta) + mrow * 2) =
+                (uint32_t)Dt<DT>::store(rp.scale) | ((uint32_t)Dt<DT>::store(rp.zp) << 16);
+        } else {  // unused outlier slots of the head hold zero
+          for (uint32_t m = maps[2][k][lane]; m; m &= m - 1) store_bits<DT>(a.raw, mrow * a.n_out + (__ffs(m) - 1), 0u);
+        }
       }
+    }
+    // the quotient x / scale: the proven fast form where every head of the row admits it (fast_div_ok),
+    // else the IEEE division — the same value either way
+    const bool all_fast = __builtin_amdgcn_ballot_w64(!fast) == 0ull;
+    uint8_t* dst_lane = a.codes[t] + roff;  // (+ lane·W + k·64·W: 32-bit lane offsets, constant chunk offsets)
+    const uint32_t qmaxU = (uint32_t)qmax;
+    (void)qmaxU;
+    auto emit = [&](auto wtag, auto ftag) {
+      constexpr int W = decltype(wtag)::value;
+      constexpr bool FAST = decltype(ftag)::value;
+#pragma unroll
+      for (int k = 0; k < NCH; ++k) {
+        __builtin_amdgcn_sched_barrier(0);  // one chunk's temporaries live at a time
+        const int g = k / 8, c = k % 8;
+        const float s = __uint_as_float(row_bcast2(__float_as_uint(sc[g]), c));
+        const float z = __uint_as_float(row_bcast2(__float_as_uint(zp[g]), c));
+        const float rr = FAST ? __uint_as_float(row_bcast2(__float_as_uint(rc[g]), c)) : 0.f;
+        gq_chunk_codes<DT, W, FAST>(rawc[k], s, rr, z, (uint32_t)((1u << W) - 1u), dst_lane + (uint32_t)(lane * W) + k * 64 * W);
+      }
+    };
+    auto by_fast = [&](auto wtag) {
+      if (all_fast) emit(wtag, std::true_type{});
+      else emit(wtag, std::false_type{});
+    };
+    switch (bits) {
+      case 2: by_fast(std::integral_constant<int, 2>{}); break;
+      case 4: by_fast(std::integral_constant<int, 4>{}); break;
+      default: by_fast(std::integral_constant<int, 8>{}); break;
     }
   }
   }
@@ -591,7 +810,7 @@ template <int DT> static int launch_gq_vote(const GqArgs& a, unsigned blocks, hi
   const int nch = (int)(a.kv.H * kGqD / 512);
 #define RTKV_GQ(N)                                                                      \
   if (nch == N) {                                                                       \
-    hipLaunchKernelGGL((gq_vote_rows_kernel<DT, N>), dim3(blocks), dim3(256), 0, st, a); \
+    hipLaunchKernelGGL((gq_vote_rows_kernel<DT, N>), dim3(blocks), dim3(1024), 0, st, a); \
     RTKV_HIP_CHECK(hipGetLastError());                                                  \
     return RTKV_OK;                                                                     \
   }
@@ -639,12 +858,11 @@ int rtkv_gq_outlier_channels(const rtkv_kv_desc* kv, const int32_t* kept_index_d
   a.votes = static_cast<uint32_t*>(workspace_dev);
   a.idx = outlier_idx_dev;
   RTKV_HIP_CHECK(hipMemsetAsync(a.votes, 0, rtkv_gq_workspace_size(kv->H, kv->D), st));
-  // (sampled row, tensor) tasks over workgroups of 4 waves, ~2 tasks per wave: a wave is a latency chain
-  // (one row in flight, then its rounds), so the grid supplies the parallelism (each workgroup flushes
-  // its LDS counters once)
+  // (sampled row, tensor) tasks over 1024-thread workgroups, at most one per CU (each flushes its LDS
+  // counters once: with 4-wave workgroups, ~900 of them at cfg3, the flush atomics were most of the kernel)
   const int64_t nsamp = (row_capacity + g->vote_stride - 1) / g->vote_stride;
-  int64_t blocks = (2 * nsamp + 7) / 8;
-  blocks = blocks < 1 ? 1 : (blocks > 4096 ? 4096 : blocks);
+  int64_t blocks = (2 * nsamp + 15) / 16;
+  blocks = blocks < 1 ? 1 : (blocks > 256 ? 256 : blocks);
   int rc2 = RTKV_OK;
   switch (kv->dtype) {
     case RTKV_F16: rc2 = launch_gq_vote<RTKV_F16>(a, (unsigned)blocks, st); break;
@@ -668,6 +886,8 @@ int rtkv_gq_pack(const rtkv_kv_desc* kv, const int32_t* kept_index_dev, const ui
   RTKV_REQUIRE(g->n_outlier == 0 || (outlier_idx_dev && raw_dev), "gq: null outlier index or raw-value buffer");
   for (int c = 0; c < 3; ++c) RTKV_REQUIRE(bits[c] == 2 || bits[c] == 4 || bits[c] == 8, "gq: class widths 2, 4 or 8 bits");
   RTKV_REQUIRE(row_capacity >= 1, "gq: row_capacity >= 1");
+  RTKV_REQUIRE(row_capacity * 2 * kv->H * (g->n_outlier > 2 ? g->n_outlier : 2) < ((int64_t)1 << 31),
+               "gq: meta / raw-value indices beyond 2^31 elements");
   GqArgs a = gq_args(kv, kept_index_dev, labels_dev, stats_dev, g);
   for (int c = 0; c < 3; ++c) a.bits[c] = bits[c];
   a.row_cap = row_capacity;
@@ -680,6 +900,13 @@ int rtkv_gq_pack(const rtkv_kv_desc* kv, const int32_t* kept_index_dev, const ui
   a.raw = raw_dev;
   const int64_t tasks = 2 * row_capacity;  // (row, tensor); a wave keeps one tensor's outlier masks
   int64_t blocks = (tasks + 15) / 16;      // ~4 rows per wave
+  {
+    static const int64_t cap = [] {
+      const char* e = std::getenv("RTKV_GQ_PACK_WGS");  // tuning knob
+      return e ? (int64_t)std::atoll(e) : (int64_t)8192;
+    }();
+    blocks = blocks > cap ? cap : blocks;
+  }
   blocks = blocks < 1 ? 1 : (blocks > 8192 ? 8192 : blocks);
   hipStream_t st = (hipStream_t)stream;
   switch (kv->dtype) {

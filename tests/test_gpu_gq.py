@@ -190,3 +190,83 @@ def test_gq_reconstruction_error_at_cfg5_shape(dtype):
           f"{c.nbytes() / max(c.rows, 1):.0f}")
     assert res["K"][1] < 0.5 * res["K"][0]   # the outlier channels no longer set every channel's step
     assert res["V"][1] < res["V"][0]         # per-head groups alone already narrow the range
+
+
+def _nan_mask(a, dtype):
+    """NaN positions of host storage arrays (float32 values, or fp16 / bf16 bit patterns as uint16)."""
+    if dtype == "float32":
+        return np.isnan(a)
+    a = a.astype(np.uint32)
+    if dtype == "float16":
+        return ((a & 0x7C00) == 0x7C00) & ((a & 0x3FF) != 0)
+    return ((a & 0x7F80) == 0x7F80) & ((a & 0x7F) != 0)
+
+
+def _same_nan_aware(got, ref, dtype):
+    """Bit-identical except that a NaN matches any NaN: a NaN's sign and payload from an invalid operation
+    (0·inf, inf/inf) are the platform's (x86 gives the negative default NaN, gfx950 the positive one)."""
+    ng, nr = _nan_mask(got, dtype), _nan_mask(ref, dtype)
+    if not np.array_equal(ng, nr):
+        return False
+    g = got.view(np.uint32) if dtype == "float32" else got
+    r = ref.view(np.uint32) if dtype == "float32" else ref
+    return np.array_equal(g[~ng], r[~nr])
+
+
+@pytest.mark.parametrize("dtype", ["float32", "float16", "bfloat16"])
+def test_gq_edge_values_match_oracle(dtype):
+    """Rows the fast path must not mistreat: all-zero rows, a NaN element (ignored by the statistics, code 0),
+    +inf (scale inf), a constant head (max == min: scale 1, zero-point 0), values so small that the fast
+    division's gate sends the row to the IEEE division (fp32 / bf16: scales below 2^-100 / 2^-62; fp16:
+    subnormals), a range that overflows to inf, and the injected outlier channels — codes, scale/zero-points
+    and raw values byte for byte against the oracle, the unpacked rows NaN-aware (inf/inf and 0·inf give
+    the platform's default NaN)."""
+    import rtkv
+    S, H = 3000, 8
+    F = H * 128
+    K, V, W = _inputs(4242, S, H, "float32")
+    K, V = K.copy(), V.copy()
+    tiny = 1e-30 if dtype != "float16" else 1e-6
+    huge = 3e38 if dtype != "float16" else 6e4
+    for x, salt in ((K, 0), (V, 5)):
+        for tok in range(0, S):
+            p = (tok + salt) % 11
+            row = x[0, tok]
+            if p == 0:
+                row[:] = 0.0
+            elif p == 1:
+                row[(tok * 13) % F] = np.nan
+            elif p == 2:
+                row[(tok * 29) % F] = np.inf
+            elif p == 3:
+                row[128:256] = 0.5
+            elif p == 4:
+                row *= tiny
+            elif p == 5:
+                row[(tok * 7) % 128] = huge
+                row[128 + (tok * 11) % 128] = -huge
+                row[(tok * 7) % 128 + 256] = huge
+                row[(tok * 5) % 128 + 256] = -huge
+            elif p == 6:
+                row[3] = np.nan  # on an injected outlier channel of K: its raw value stays NaN, bit for bit
+    K, V = synth.cast(K, dtype), synth.cast(V, dtype)
+    gqc = rtkv.GroupQuantConfig(n_outlier=4, n_vote=4, vote_stride=3, min_votes_pm=250)
+    comp, k, v, info = _layer(K, V, synth.cast(W, dtype), dtype, 0.7, gqc)
+    c = info["group_quant"]
+    torch.cuda.synchronize()
+    p = info["packed"]
+    kept = p["kept_index"][0].cpu().numpy().astype(np.int32)
+    labels = p["labels"][0].cpu().numpy()
+    ro = p["row_offset"][0].cpu().numpy()
+    o = _oracle(K, V, dtype, gqc, kept, labels, ro, (2, 4, 8))
+    assert np.unique(kept % 11).size == 11  # every pattern is among the kept rows
+    nb = o[0]["codes"].size
+    for t, (codes, ref) in enumerate(((c.codes_k, o[0]), (c.codes_v, o[1]))):
+        assert np.array_equal(c.outlier_idx[t].cpu().numpy(), ref["idx"]), f"tensor {t} outlier channels"
+        assert np.array_equal(codes[:nb].cpu().numpy(), ref["codes"]), f"tensor {t} codes"
+        assert _same_nan_aware(_host(c.meta[:, t]), ref["meta"], dtype), f"tensor {t} scale/zero-point"
+        got_raw, ref_raw = _host(c.raw[:, t]), ref["raw"]
+        assert np.array_equal(got_raw.view(np.uint32) if dtype == "float32" else got_raw,
+                              ref_raw.view(np.uint32) if dtype == "float32" else ref_raw), f"tensor {t} raw values"
+    kq, vq = c.dequantize()
+    assert _same_nan_aware(_host(kq[0]), o[0]["deq"], dtype) and _same_nan_aware(_host(vq[0]), o[1]["deq"], dtype)
