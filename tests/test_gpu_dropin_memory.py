@@ -5,6 +5,7 @@ unified_compressor.py:170).  rtkv sizes them from the early statistics (rtkv_com
 _finish), so a layer's K'/V' hold 2·B·S'·F elements, its packed codes exactly their bytes, and the
 compressor's layer_states keep only per-token buffers and the packed codes: once the caller drops K'/V'
 nothing pins them, and reset_compression_state() releases the rest."""
+import numpy as np
 import pytest
 import torch
 
@@ -156,3 +157,59 @@ def test_processing_time_is_the_callers_wall_time(strict):
     # the calls are the whole loop but for the last layer's K4 tail: most of the wall time is inside them
     assert total >= 0.5 * wall, (total, wall)
     assert all(comp.layer_states[l]["device_processing_time"] > 0 for l in range(layers))
+
+
+def test_device_span_does_not_depend_on_the_row_order():
+    """The layer's device span (rtkv_layer_times: K1's first block to the K4 end stamp, the source of
+    device_processing_time) against HIP events on the stream, on a layer whose 8-bit rows are the first kept
+    rows and on one whose 8-bit rows are the last: only the waves of K4's last 2048 row tasks stamp the end
+    (quant_impl.h kStampWindow), so if earlier, longer tasks finished after them the span would be short
+    when the heavy rows come first.  Through the drop-in's own begin / finish calls: the begin
+    call records the first event right before K1 (start_event), the second is recorded after K4 is enqueued,
+    so only K1, K2, the host's reaction to the early statistics and K4 lie between them.  Measured on MI355X:
+    events − stamps = 17.5 us in both orders (the events' own start / end latency,
+    profiles/r06v_span_vs_events.log) — the stamps lose nothing to the row order."""
+    import rtkv
+    from rtkv import _lib as L
+    from rtkv.engine import EarlyStatsBuffer, compress_layer_begin
+    S, F = 16384, 4096
+    cfg = rtkv.CompressionConfig(alpha=0.8, beta=0.1, gamma=0.1, theta_h=0.4, theta_m=0.25, num_hidden_layers=1,
+                                 layer_weights=[1.0], high_precision_bits=8, medium_precision_bits=4,
+                                 low_precision_bits=2)
+    g = torch.Generator(device="cuda").manual_seed(21)
+    P = rtkv.prompt_length(S)
+    K = torch.randn(1, S, F, device="cuda", generator=g)
+    V = torch.randn(1, S, F, device="cuda", generator=g)
+    W0 = torch.rand(1, 32, S, P, device="cuda", generator=g)
+    params = rtkv.params_from_config(cfg, 0, P, 0.6, L.EMIT_DEQUANT | L.EMIT_PACKED)
+    ws = rtkv.Workspace("cuda")
+    early = EarlyStatsBuffer()
+    med = {}
+    for order in ("high_first", "low_first"):
+        ramp = torch.linspace(1.0, 0.01, S, device="cuda")  # early tokens most important
+        if order == "low_first":
+            ramp = ramp.flip(0)
+        W = W0 * ramp.view(1, 1, S, 1)
+        gaps = []
+        for it in range(10):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            bufs = rtkv.LayerBuffers(1, S, F, K.dtype, "cuda", (2, 4, 8), outputs=False)
+            e0.record()  # (creates the event and marks it recorded for torch; begin re-records it before K1)
+            pend = compress_layer_begin(K, V, W, params, bufs, ws, early, start_event=e0.cuda_event)
+            pend.stats()
+            pend.finish()
+            e1.record()
+            torch.cuda.synchronize()
+            ev, dev = e0.elapsed_time(e1) * 1e3, pend.device_seconds() * 1e6
+            if it >= 2:  # (warm-up: the first calls' allocations)
+                gaps.append((round(ev, 2), round(dev, 2)))
+        print(f"device span vs events ({order}), us:", gaps)
+        labels = bufs.labels[0].cpu().numpy()
+        kept = bufs.kept_index[0].cpu().numpy()[: pend.stats().max_kept]
+        hi = 0 if order == "high_first" else len(kept) - 64
+        assert (labels[kept[hi:hi + 64]] == 2).all()  # the 8-bit (high-precision) rows are first / last
+        for ev, dev in gaps:
+            assert 0 < dev <= ev + 2.0, gaps  # the stamps lie inside the events
+        med[order] = float(np.median([ev - dev for ev, dev in gaps]))
+        assert med[order] <= 30.0, med
+    assert abs(med["high_first"] - med["low_first"]) <= 4.0, med  # no order-dependent loss of K4's tail

@@ -270,3 +270,44 @@ def test_gq_edge_values_match_oracle(dtype):
                               ref_raw.view(np.uint32) if dtype == "float32" else ref_raw), f"tensor {t} raw values"
     kq, vq = c.dequantize()
     assert _same_nan_aware(_host(kq[0]), o[0]["deq"], dtype) and _same_nan_aware(_host(vq[0]), o[1]["deq"], dtype)
+
+
+@pytest.mark.parametrize("dtype", ["float32", "float16"])
+def test_gq_vote_ties_match_oracle(dtype):
+    """The vote's composite keys under ties: values on a coarse grid (exact |x| ties, broken by the lower
+    channel) and, in fp32, near-ties inside one 2^7-ulp bucket of the truncated key ordered AGAINST the
+    channel order (x·(1 + j·2^-21) rising with j over 16 channels of a head), so the truncated order differs
+    from the exact one exactly where the kernel must detect it and redo the chunk with exact keys.  Votes,
+    outlier channels and codes byte for byte against the oracle."""
+    import rtkv
+    S, H = 2048, 8
+    F = H * 128
+    K, V, W = _inputs(99, S, H, "float32")
+    K = np.round(K * 4.0) / 4.0
+    V = np.round(V * 4.0) / 4.0
+    for tok in range(0, S, 3):
+        h = tok % H
+        base = np.float32(3.0 + (tok % 7))
+        for j in range(16):  # channels 16..31 of head h: |x| rising with the channel, within a 2^-16 bucket
+            K[0, tok, h * 128 + 16 + j] = base * np.float32(1.0 + j * 2.0 ** -21)
+            V[0, tok, h * 128 + 40 + j] = -base * np.float32(1.0 + (15 - j) * 2.0 ** -21)
+    K, V = synth.cast(K.astype(np.float32), dtype), synth.cast(V.astype(np.float32), dtype)
+    gqc = rtkv.GroupQuantConfig(n_outlier=4, n_vote=6, vote_stride=1, min_votes_pm=100)
+    comp, k, v, info = _layer(K, V, synth.cast(W, dtype), dtype, 0.7, gqc)
+    c = info["group_quant"]
+    torch.cuda.synchronize()
+    p = info["packed"]
+    kept = p["kept_index"][0].cpu().numpy().astype(np.int32)
+    labels = p["labels"][0].cpu().numpy()
+    ro = p["row_offset"][0].cpu().numpy()
+    o = _oracle(K, V, dtype, gqc, kept, labels, ro, (2, 4, 8))
+    nb = o[0]["codes"].size
+    for t, (codes, ref) in enumerate(((c.codes_k, o[0]), (c.codes_v, o[1]))):
+        assert np.array_equal(c.outlier_idx[t].cpu().numpy(), ref["idx"]), f"tensor {t} outlier channels"
+        assert np.array_equal(codes[:nb].cpu().numpy(), ref["codes"]), f"tensor {t} codes"
+    # the votes themselves (the workspace of the last gq call) against the oracle's
+    x = (K[0], V[0])
+    for t in range(2):
+        ref_votes = orc.gq_votes(x[t], ODT[dtype], H, 128, kept, gqc.n_vote, gqc.vote_stride)
+        got = c._votes[: 2 * F * 4].view(torch.int32).view(2, F)[t].cpu().numpy().astype(np.uint32)
+        assert np.array_equal(got, ref_votes), f"tensor {t} votes"
