@@ -573,9 +573,12 @@ int rtkv_decode_attention_packed(const uint8_t* packed_k_dev, const uint8_t* pac
  * the mode and the kernels match it byte for byte.  B = 1, head_dim 128 (one group per head), K/V rows
  * [S, H·128] with contiguous heads, H a multiple of 4, class widths 2/4/8 bits.
  *   1. rtkv_gq_outlier_channels: every vote_stride-th kept row votes, per head, for its n_vote channels of
- *      largest |x| (a wave arg-max by shuffles); the n_outlier channels with the most votes (at least
- *      max(1, ceil(samples·min_votes_pm/1000))) are the layer's outlier channels of each head and tensor:
- *      outlier_idx[2][H][n_outlier] (channel within the head, -1 = unused slot).
+ *      largest |x| (ties: the lower channel; DPP row maxima over keys unique within the head); the
+ *      n_outlier channels with the most votes (at least max(1, ceil(samples·min_votes_pm/1000))) are the
+ *      layer's outlier channels of each head and tensor: outlier_idx[2][H][n_outlier] (channel within the
+ *      head, -1 = unused slot).  One launch (the selection runs in the vote grid's last workgroup);
+ *      workspace: rtkv_gq_workspace_size(H, D) bytes (the votes and a done count, zeroed by the call);
+ *      row_capacity < 2^25.
  *   2. rtkv_gq_pack: per (kept row, tensor, head) the reference's per-token formulas (dynamic_quantization.py
  *      :62-126, each op rounded to the dtype) over the head's non-outlier channels: codes of the row's class
  *      width for every channel (outlier channels and NaN: code 0) at codes + row_offset[r] (the per-token

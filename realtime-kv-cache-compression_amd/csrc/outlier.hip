@@ -10,18 +10,19 @@
 //
 // The scheme (D = 128: one group per head):
 //   1 vote    every vote_stride-th kept row votes, per head, for its n_vote channels of largest |x| (a
-//             wave per (sampled row, tensor), a head on each 16-lane DPP row: n_vote rounds of a row
-//             arg-max — lane-local best, four row_ror max steps, the lowest lane by ballot — each vote an
-//             LDS atomic; one global atomic per channel and workgroup at the end).
+//             wave per (sampled row, tensor), a head on each 16-lane DPP row: n_vote rounds of a row maximum
+//             over keys unique within the head, four row_ror max steps each; votes to LDS counters, one
+//             global atomic per nonzero channel and workgroup at the end).
 //   2 select  per (tensor, head) the n_outlier channels with the most votes (at least min_votes): the
 //             layer's outlier channels, fixed for every row (KVQuant-style dense-and-sparse split with a
-//             per-layer channel list instead of per-row coordinates).
+//             per-layer channel list instead of per-row coordinates) — in the vote grid's last workgroup.
 //   3 pack    per (kept row, tensor, head): the reference's per-token formulas (dynamic_quantization.py
 //             :62-126, each op rounded to the dtype) over the head's non-outlier channels, codes of the
 //             row's class width (2/4/8 bits) for every channel (outliers: code 0) in the per-token
 //             layout's row slots (the same row_offset table), {scale, zero_point} per head in the
 //             dtype, the outlier channels' raw values beside them.  A head's 16 chunks of 8 channels sit
-//             on 16 consecutive lanes, so its min/max is a 4-step xor butterfly inside a DPP row.
+//             on 16 consecutive lanes (a DPP row): one transposed row reduction per 8 chunks leaves each
+//             lane one head's statistics, whose parameters it computes once and broadcasts (row_newbcast).
 // Bytes per kept row and tensor: F·w/8 codes + 2·H·e meta + H·n_outlier·e raw values.
 #include <cstring>
 
