@@ -60,19 +60,6 @@ __device__ __forceinline__ int gq_rows(const GqArgs& a) {
   return (int)(n < 0 ? 0 : (n < a.row_cap ? n : a.row_cap));
 }
 
-// two consecutive elements (2l, 2l+1) of a row as fp32
-template <int DT> __device__ __forceinline__ void load2(const typename Dt<DT>::S* p, float& x0, float& x1) {
-  if constexpr (DT == RTKV_F32) {
-    const float2 v = *reinterpret_cast<const float2*>(p);
-    x0 = v.x;
-    x1 = v.y;
-  } else {
-    const uint32_t w = *reinterpret_cast<const uint32_t*>(p);
-    x0 = Dt<DT>::load((uint16_t)(w & 0xffffu));
-    x1 = Dt<DT>::load((uint16_t)(w >> 16));
-  }
-}
-
 // ---- DPP inside a 16-lane row (a head's 16 chunks of one pack chunk index): lane j ↔ j^8 (row_ror:8),
 // j ↔ j^7 (row_half_mirror), j ↔ j^2 / j^1 (quad_perm), and lane n broadcast to its row (row_newbcast:n)
 constexpr int kDppRor8 = 0x128, kDppHalfMirror = 0x141, kDppXor2 = 0x4E, kDppXor1 = 0xB1, kDppRowBcast = 0x150;

@@ -377,14 +377,14 @@ template <> struct Frag32<RTKV_BF16> {
 // steps per 16 rows), and every key fragment read from LDS serves 32 query rows instead of 16.
 // k order: k-step s takes the 16-byte chunk 2s + h of the row in lane half h, for A and B alike (the
 // dot product is the same sum), so a query load instruction reads 32 contiguous bytes of each of 32 rows.
-// Two waves per SIMD (256 VGPRs): the wave keeps QK32_AHEAD query tiles in flight beyond the one it
-// computes, in registers (the loop is unrolled over the tile buffers, no register copies).
+// The wave keeps NB − 1 query tiles in flight beyond the one it computes, in registers (the loop is
+// unrolled over the tile buffers, no register copies).  Without a key bias: four waves per SIMD (128
+// VGPRs) with one tile ahead, 1024 workgroups — head + reduce 41.6 → 39.0 us per cfg3 f16 layer against
+// two waves with two tiles ahead (three waves: 39.5; profiles/r06x_qk_occupancy_ab.txt); with a key bias
+// the 128-register form spills (48–89 VGPRs), so that variant keeps two waves per SIMD, two tiles ahead.
 // KB: a key bias (padding), kept in LDS as kb[p]·scale·log2(e), added to the row's −lse·log2(e).
-#ifndef QK32_WPE
-#define QK32_WPE 2
-#endif
 template <int DT, bool KB, int NTILE, int NB>
-__global__ __launch_bounds__(256, QK32_WPE) void qk_head32_kernel(QKArgs g, float* __restrict__ part) {
+__global__ __launch_bounds__(256, KB ? 2 : 4) void qk_head32_kernel(QKArgs g, float* __restrict__ part) {
   using FT = typename Frag32<DT>::T;
   using S_ = typename Dt<DT>::S;
   constexpr int RB = 256, CH = 16, PT = 128, NT = 4, KS = 8;  // NB query tile buffers (NB - 1 ahead)
@@ -587,10 +587,10 @@ static int launch_qk_head(const QKArgs& a, float* part, hipStream_t st, int* npa
 
 template <int DT, int NTILE>
 static void launch_qk_head32_n(const QKArgs& a, float* part, hipStream_t st, dim3 grid, size_t lds) {
-  // 3 tile buffers (2 tiles ahead): 4 buffers measured 43.6 against 42.6 us per cfg3 f16 layer
-  // (profiles/r05_qk32_ab.json)
+  // key bias: 3 tile buffers (2 tiles ahead) at two waves per SIMD — 4 buffers measured 43.6 against 42.6 us
+  // per cfg3 f16 layer (profiles/r05_qk32_ab.json); none: 2 buffers at four waves per SIMD (above)
   if (a.q.kbias_dev) hipLaunchKernelGGL((qk_head32_kernel<DT, true, NTILE, 3>), grid, dim3(256), lds, st, a, part);
-  else hipLaunchKernelGGL((qk_head32_kernel<DT, false, NTILE, 3>), grid, dim3(256), lds, st, a, part);
+  else hipLaunchKernelGGL((qk_head32_kernel<DT, false, NTILE, 2>), grid, dim3(256), lds, st, a, part);
 }
 
 template <int DT>
@@ -598,11 +598,12 @@ static int launch_qk_head32(const QKArgs& a, float* part, hipStream_t st, int* n
   const size_t lds = (size_t)128 * 256 + (a.q.kbias_dev ? 128 * sizeof(float) : 0);
   const int64_t S = a.q.S;
   // 32-row tiles per wave (8, 4, 2 or 1): the most that still gives about RTKV_QK32_WGS workgroups
-  // (default 512: two per CU, the occupancy the 2-wave register budget allows)
-  static const int target = [] {
+  // (default: four per CU without a key bias, two with one — the occupancy each variant's registers allow)
+  static const int env_target = [] {
     const char* e = getenv("RTKV_QK32_WGS");
-    return e ? atoi(e) : 512;
+    return e ? atoi(e) : 0;
   }();
+  const int target = env_target > 0 ? env_target : (a.q.kbias_dev ? 512 : 1024);
   int nt = 8;
   while (nt > 1 && (S + 128 * nt - 1) / (128 * nt) * a.q.H * a.q.B < target) nt /= 2;
   const dim3 grid((unsigned)((S + 128 * nt - 1) / (128 * nt)), (unsigned)a.q.H, (unsigned)a.q.B);
