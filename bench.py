@@ -560,6 +560,33 @@ def gq_leg(args, job, steps, warmup):
             tot += sum(a.elapsed_time(z) for a, z in ev)
             n += args.layers
     us = tot / n * 1e3
+    # the same layers with the extension on a side stream (what the drop-in does): whole-step time against
+    # the step without it, both between events on the main stream (the side stream joined at the end)
+    side = torch.cuda.Stream(job.device)
+    step_ms = {}
+    for mode in ("without", "side_stream", "without", "side_stream"):
+        for it in range(warmup + steps):
+            a0, a1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a0.record()
+            slot_ev = {}  # a buffer slot is not reused on the main stream before the side stream has read it
+            for l in range(args.layers):
+                if l % job.slots in slot_ev:
+                    torch.cuda.current_stream(job.device).wait_event(slot_ev.pop(l % job.slots))
+                job._step_one(l)
+                if mode == "side_stream":
+                    K, V = job.inputs[l % job.in_slots][:2]
+                    b = job.bufs[l % job.slots]
+                    Sp, pk = acct[l]
+                    rtkv.gq_compress(K, V, b.kept_index[0], b.labels[0], b.row_offset[0], b.stats, Sp, pk, job.bits,
+                                     cfg, stream=side)
+                    slot_ev[l % job.slots] = torch.cuda.Event()
+                    slot_ev[l % job.slots].record(side)
+            torch.cuda.current_stream(job.device).wait_stream(side)
+            a1.record()
+            torch.cuda.synchronize(job.device)
+            if it >= warmup:
+                step_ms.setdefault(mode, []).append(a0.elapsed_time(a1))
+    med = {m: sorted(v)[len(v) // 2] for m, v in step_ms.items()}
     e, H = job.elem(), job.F // 128
     nb = 0
     for Sp, pk in acct:
@@ -580,7 +607,12 @@ def gq_leg(args, job, steps, warmup):
                      "gq": ((gq[0].float() - src) ** 2).mean().item()}
     gbs = nb / (us / 1e6) / 1e9
     return {"us_per_layer": round(us, 2), "algorithmic_bytes_per_layer": int(nb), "GBs": round(gbs, 1),
-            "hbm_frac": round(gbs / 8000.0, 4), "config": vars(cfg), "reconstruction_mse_last_layer": mse,
+            "hbm_frac": round(gbs / 8000.0, 4), "config": vars(cfg),
+            "side_stream": {"step_ms_without": round(med["without"], 4), "step_ms_with": round(med["side_stream"], 4),
+                            "overhead_us_per_layer": round((med["side_stream"] - med["without"]) * 1e3 / args.layers, 2),
+                            "note": "the drop-in's mode: gq after each layer on a side stream, overlapping the next "
+                                    "layers; medians of the steps, the side stream joined before the end event"},
+            "reconstruction_mse_last_layer": mse,
             "note": "synthetic K/V ~ N(0,1) carry no outlier channels: the gq MSE gain here comes from the per-head "
                     "groups alone (tests/test_gpu_gq.py measures it with injected key outliers at the 13B shape)",
             "path": "rtkv.gq_compress after each layer's rtkv_compress_layer (events around the gq launches only)"}

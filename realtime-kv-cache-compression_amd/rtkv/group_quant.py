@@ -94,6 +94,21 @@ class GroupQuantKVCache:
         self._p = cfg.params()
         self._b3 = (ctypes.c_int32 * 3)(*self.bits)
 
+    _ready = None  # set when the cache was produced on a side stream (gq_compress(stream=...))
+
+    def wait(self):
+        """Make the current stream wait for the side stream that produced the cache (no-op otherwise); its
+        tensors are then also recorded on the current stream, so the allocator keeps them until the
+        current stream's work on them is done."""
+        if self._ready is not None:
+            cur = torch.cuda.current_stream(self.device)
+            cur.wait_event(self._ready)
+            for t in (self.codes_k, self.codes_v, self.meta, self.raw, self.outlier_idx, self.kept_index,
+                      self.labels, self.row_offset, self.stats):
+                t.record_stream(cur)
+            self._ready = None
+        return self
+
     def _common(self):
         return (ctypes.byref(self._kd), self.kept_index.data_ptr(), self.labels.data_ptr(), self.stats.data_ptr(),
                 self._b3, ctypes.byref(self._p), self.outlier_idx.data_ptr(), self.row_offset.data_ptr())
@@ -109,6 +124,7 @@ class GroupQuantKVCache:
 
     def dequantize(self):
         """(K', V') [1, rows, F] decoded from the format (rtkv_gq_unpack)."""
+        self.wait()
         outs = []
         for which, codes in ((0, self.codes_k), (1, self.codes_v)):
             out = torch.empty(1, self.rows, self.F, dtype=self.dtype, device=self.device)
@@ -125,6 +141,7 @@ class GroupQuantKVCache:
         (rtkv_gq_decode_attention): out [1, Hq, 128] fp32."""
         if q.dim() != 3 or q.shape[0] != 1 or q.shape[2] != GQ_D or q.dtype != self.dtype:
             raise ValueError("gq attend: q must be [1, Hq, 128] in the K/V dtype")
+        self.wait()
         q = q.contiguous()
         Hq = q.shape[1]
         out = torch.empty(1, Hq, GQ_D, dtype=torch.float32, device=self.device)
@@ -141,13 +158,29 @@ class GroupQuantKVCache:
 
 def gq_compress(K: torch.Tensor, V: torch.Tensor, kept_index: torch.Tensor, labels: torch.Tensor,
                 row_offset: torch.Tensor, stats: torch.Tensor, rows: int, codes_bytes: int, bits,
-                cfg: Optional[GroupQuantConfig] = None) -> GroupQuantKVCache:
+                cfg: Optional[GroupQuantConfig] = None,
+                stream: Optional[torch.cuda.Stream] = None) -> GroupQuantKVCache:
     """Outlier channels (rtkv_gq_outlier_channels) and the pack (rtkv_gq_pack) of a compressed layer's kept
     rows, stream-ordered after the layer: K, V [1, S, H·128] (the layer's inputs), kept_index / labels /
     row_offset / stats its per-token outputs (LayerBuffers), rows = S' and codes_bytes = the layer's packed
-    bytes per tensor (its published statistics)."""
+    bytes per tensor (its published statistics).
+
+    stream: run the launches on this side stream instead (after everything enqueued on the current stream
+    so far), so the extension overlaps what the caller enqueues next — the next layer's selection leaves
+    most CUs idle for ~20 us.  The inputs are recorded on the side stream (the allocator keeps them until
+    it is done); the cache's consumers (dequantize, attend) wait for it, direct reads of its tensors need
+    cache.wait() (or a device sync) first."""
     cfg = cfg or GroupQuantConfig()
     L.require_device(K, V)
+    if stream is not None:
+        stream.wait_stream(torch.cuda.current_stream(K.device))
+        for t in (K, V, kept_index, labels, row_offset, stats):
+            t.record_stream(stream)
+        with torch.cuda.stream(stream):
+            c = gq_compress(K, V, kept_index, labels, row_offset, stats, rows, codes_bytes, bits, cfg)
+            c._ready = torch.cuda.Event()
+            c._ready.record(stream)
+        return c
     c = GroupQuantKVCache(K, V, kept_index, labels, row_offset, stats, rows, codes_bytes, bits, cfg)
     if c.rows == 0:
         return c

@@ -115,6 +115,7 @@ class RealTimePrefillCompressor:
         self._packable: Dict[tuple, bool] = {}  # (dtype, bits, emit_packed) → whether the codes are emitted
         self.strict = (os.environ.get("RTKV_STRICT", "1") != "0") if strict is None else bool(strict)
         self.group_quant = group_quant
+        self._gq_streams = {}  # device -> the extension's side stream
 
     # ------------------------------------------------------------------ reference API
     def identify_prompt_tokens(self, input_ids: torch.Tensor, special_tokens: Optional[List[int]] = None):
@@ -283,11 +284,16 @@ class RealTimePrefillCompressor:
                 "dtype": K.dtype,
                 "feature_dim": F,
             })
-        if gq:  # the extension's group-wise pack of the same kept rows, stream-ordered after the layer
+        if gq:  # the extension's group-wise pack of the same kept rows, after the layer on a side stream: it
+            # overlaps the caller's next work (the next layer's selection leaves most CUs idle) instead of
+            # sitting on the path to the next layer; the cache's consumers wait for it
             from .group_quant import gq_compress
+            side = self._gq_streams.get(K.device)
+            if side is None:
+                side = self._gq_streams[K.device] = torch.cuda.Stream(K.device)
             compression_info["group_quant"] = gq_compress(
                 K, V, bufs.kept_index[0], bufs.labels[0], bufs.row_offset[0], bufs.stats, Sp, st.total_packed_bytes,
-                bits, self.group_quant)
+                bits, self.group_quant, stream=side)
         res.k_out = res.v_out = None  # the caller owns K'/V'; nothing kept here pins them
         self.layer_states[layer_idx] = compression_info
         compression_info["processing_time"] = time.perf_counter() - start_time
