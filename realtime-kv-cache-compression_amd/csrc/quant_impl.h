@@ -521,9 +521,13 @@ constexpr int kStampWindow = 2048;
 // chunks of 8 (F a multiple of 512), so no lane is idle and packed rows stay 16-byte aligned.
 // PKW > 0 (compile time): packed codes + scale/zero-point only (no dequantized K'/V': the decode and packed
 // consumers' mode), the dequantization path compiled out, at a launch bound of PKW waves per SIMD.
-template <int DT, int NCH, bool CONTIG, bool FULL, int PKW = 0>
+// PAIR (packed-only 2-byte rows): one task = a kept row's K AND V rows — one index / class / offset round
+// trip for both, and both rows' loads in flight together (twice a task's bytes per wave, half the waves).
+template <int DT, int NCH, bool CONTIG, bool FULL, int PKW = 0, bool PAIR = false>
 __global__ __launch_bounds__(256, PKW ? PKW : ((DT == RTKV_F32 && NCH == 8 && FULL && CONTIG) ? 4 : 2)) void quant_rows_kernel(QuantArgs a) {
   constexpr bool PK_ONLY = PKW > 0;
+  static_assert(!PAIR || PK_ONLY, "the paired task is the packed-only kernel's");
+  constexpr int TM = PAIR ? 1 : 2;  // tasks per kept row
   using S_ = typename Dt<DT>::S;
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -543,11 +547,11 @@ __global__ __launch_bounds__(256, PKW ? PKW : ((DT == RTKV_F32 && NCH == 8 && FU
   int64_t osb = 0;
   int tasks;
   if (one_row) {
-    tasks = 2 * (a.kept_index ? (cap < S ? cap : S) : S);
+    tasks = TM * (a.kept_index ? (cap < S ? cap : S) : S);
   } else {
     R = a.kept_index ? (int)a.stats->max_kept : S;
     if (R > cap) R = cap;
-    tasks = 2 * B * R;
+    tasks = TM * B * R;
     osb = a.out.o_stride_b >= 0 ? a.out.o_stride_b : (int64_t)R * a.out.o_stride_s;
   }
   const rtkv_batch_stats* bst = a.stats ? reinterpret_cast<const rtkv_batch_stats*>(a.stats + 1) : nullptr;
@@ -577,8 +581,8 @@ __global__ __launch_bounds__(256, PKW ? PKW : ((DT == RTKV_F32 && NCH == 8 && FU
   }
   bool wrote = false;
   for (int t = blockIdx.x * (blockDim.x >> 6) + wave; t < tasks; t += nw) {
-    const int which = t & 1;
-    const int rr = t >> 1;
+    const int which0 = PAIR ? 0 : (t & 1);
+    const int rr = PAIR ? t : (t >> 1);
     int b, r, kept_b, i, lab;
     int64_t roff = -1;  // packed byte offset of the row, fetched with the index when B = 1
     if (one_row) {
@@ -607,39 +611,59 @@ __global__ __launch_bounds__(256, PKW ? PKW : ((DT == RTKV_F32 && NCH == 8 && FU
     // exchange carries kept rows only), their zero dequantized rows by the pad owner alone
     if (shard && r < kept_b && (i < row0 || i >= row1)) continue;
     const int rloc = a.shard_ranges ? r - (int)a.shard_ranges[((int64_t)b * (a.shard_nranks + 1) + a.shard_rank) * 2] : r;
-    S_* orow = emit_deq ? static_cast<S_*>(which ? a.out.v_out_dev : a.out.k_out_dev) + b * osb +
-                              (int64_t)rloc * a.out.o_stride_s
-                        : nullptr;
-    const int64_t sz_idx = ((int64_t)b * cap + r) * 4 + which * 2;
-    if (r >= kept_b || lab > 2) {  // zero padding row (selective_propagation.py:214-222)
+    // (the row lambdas are force-inlined: called twice in the paired kernel, an outlined call took the
+    // row arrays through 816 B of scratch per lane — 268 against 60 us)
+    auto zero_row = [&](int which) __attribute__((always_inline)) {  // zero padding row (selective_propagation.py:214-222)
       if (emit_deq && (!shard || a.pad_owner)) {
+        S_* orow = static_cast<S_*>(which ? a.out.v_out_dev : a.out.k_out_dev) + b * osb + (int64_t)rloc * a.out.o_stride_s;
         const Chunk<DT> z = f32_to_chunk<DT>({0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f});
 #pragma unroll
         for (int k = 0; k < NCH; ++k)
           if (valid(k)) *reinterpret_cast<Chunk<DT>*>(orow + out_off[k]) = z;
       }
-      if (a.out.scale_zp_dev && lane < 2) a.out.scale_zp_dev[sz_idx + lane] = 0.f;
+      if (a.out.scale_zp_dev && lane < 2) a.out.scale_zp_dev[((int64_t)b * cap + r) * 4 + which * 2 + lane] = 0.f;
+    };
+    if (r >= kept_b || lab > 2) {
+      zero_row(which0);
+      if constexpr (PAIR) zero_row(1);
       continue;
     }
     const int bits = lab == 0 ? a.bits[0] : (lab == 1 ? a.bits[1] : a.bits[2]);
     const int w = field_width(DT, bits);
-    const S_* src = static_cast<const S_*>(which ? a.kv.v_dev : a.kv.k_dev) + b * a.kv.stride_b +
-                    (int64_t)(i - row0) * a.kv.stride_s;
-    // ---- load the whole row once (all chunks in flight), min/max
-    Chunk<DT> raw[NCH];
+    // ---- load the whole row(s) once (all chunks in flight), min/max
+    auto load_row = [&](int which, Chunk<DT> (&raw)[NCH]) __attribute__((always_inline)) {
+      const S_* src = static_cast<const S_*>(which ? a.kv.v_dev : a.kv.k_dev) + b * a.kv.stride_b +
+                      (int64_t)(i - row0) * a.kv.stride_s;
 #pragma unroll
-    for (int k = 0; k < NCH; ++k)
-      if (valid(k)) raw[k] = load_chunk_nt<DT>(src + in_off[k]);
-    float mn, mx, anz;
-    bool row_nan;
-    row_minmax<DT, NCH, FULL>(raw, nch, lane, mn, mx, anz, row_nan);
-    const RowParams rp = row_params<DT>(mn, mx, bits, anz);
-    if (a.out.scale_zp_dev && lane < 2) a.out.scale_zp_dev[sz_idx + lane] = lane == 0 ? rp.scale : rp.zp;
-    if (emit_pk && !one_row) roff = a.out.row_offset_dev[(int64_t)b * cap + r];
-    uint8_t* pk = emit_pk ? (which ? a.out.packed_v_dev : a.out.packed_k_dev) + roff : nullptr;
-    emit_row<DT, NCH, CONTIG, FULL, PK_ONLY>(raw, rp, row_nan, w, orow, out_off, pk, nch, lane, emit_deq, emit_pk,
-                                             stage);
-    wrote |= t >= (one_row ? 2 * kept_b : tasks) - kStampWindow;  // one of the last tasks
+      for (int k = 0; k < NCH; ++k)
+        if (valid(k)) raw[k] = load_chunk_nt<DT>(src + in_off[k]);
+    };
+    auto quant_row = [&](int which, Chunk<DT> (&raw)[NCH]) __attribute__((always_inline)) {
+      S_* orow = emit_deq ? static_cast<S_*>(which ? a.out.v_out_dev : a.out.k_out_dev) + b * osb +
+                                (int64_t)rloc * a.out.o_stride_s
+                          : nullptr;
+      float mn, mx, anz;
+      bool row_nan;
+      row_minmax<DT, NCH, FULL>(raw, nch, lane, mn, mx, anz, row_nan);
+      const RowParams rp = row_params<DT>(mn, mx, bits, anz);
+      if (a.out.scale_zp_dev && lane < 2)
+        a.out.scale_zp_dev[((int64_t)b * cap + r) * 4 + which * 2 + lane] = lane == 0 ? rp.scale : rp.zp;
+      if (emit_pk && !one_row) roff = a.out.row_offset_dev[(int64_t)b * cap + r];
+      uint8_t* pk = emit_pk ? (which ? a.out.packed_v_dev : a.out.packed_k_dev) + roff : nullptr;
+      emit_row<DT, NCH, CONTIG, FULL, PK_ONLY>(raw, rp, row_nan, w, orow, out_off, pk, nch, lane, emit_deq, emit_pk,
+                                               stage);
+    };
+    Chunk<DT> raw[NCH];
+    load_row(which0, raw);
+    if constexpr (PAIR) {
+      Chunk<DT> raw_v[NCH];
+      load_row(1, raw_v);
+      quant_row(0, raw);
+      quant_row(1, raw_v);
+    } else {
+      quant_row(which0, raw);
+    }
+    wrote |= t >= (one_row ? TM * kept_b : tasks) - kStampWindow / (3 - TM);  // one of the last tasks
   }
   stamp_end(a.t_end, wrote);
 }
@@ -828,14 +852,26 @@ static int launch_quant_vec(const QuantArgs& a, int64_t nch, dim3 grid, hipStrea
     const char* e = getenv("RTKV_K4_PK_WAVES");
     return e ? atoi(e) : 4;
   }();
+  // RTKV_K4_PK_PAIR (A/B knob): 3 or 4 = a task is a kept row's K and V rows (half the waves), at that
+  // many waves per SIMD; 0 = one row per task
+  static const int pk_pair = [] {
+    const char* e = getenv("RTKV_K4_PK_PAIR");
+    return e ? atoi(e) : 3;
+  }();
   if (!a.out.k_out_dev && a.out.packed_k_dev && pk_waves > 0 && DT != RTKV_F32) {
-#define RTKV_QP(N, WV)                                                                             \
-    if (nch == (int64_t)N * 64 && pk_waves == WV) {                                                \
-      hipLaunchKernelGGL((quant_rows_kernel<DT, N, CONTIG, true, WV>), grid, dim3(256), 0, st, a); \
-      RTKV_HIP_CHECK(hipGetLastError());                                                           \
-      return RTKV_OK;                                                                              \
+    const dim3 pgrid((grid.x + 1) / 2);  // half the tasks (grid = one wave per single-row task)
+#define RTKV_QP(N, WV)                                                                                   \
+    if (nch == (int64_t)N * 64 && pk_waves == WV) {                                                      \
+      if (pk_pair == 3)                                                                                  \
+        hipLaunchKernelGGL((quant_rows_kernel<DT, N, CONTIG, true, 3, true>), pgrid, dim3(256), 0, st, a); \
+      else if (pk_pair)                                                                                  \
+        hipLaunchKernelGGL((quant_rows_kernel<DT, N, CONTIG, true, 4, true>), pgrid, dim3(256), 0, st, a); \
+      else                                                                                               \
+        hipLaunchKernelGGL((quant_rows_kernel<DT, N, CONTIG, true, WV>), grid, dim3(256), 0, st, a);     \
+      RTKV_HIP_CHECK(hipGetLastError());                                                                 \
+      return RTKV_OK;                                                                                    \
     }
-    RTKV_QP(8, 4) RTKV_QP(10, 4) RTKV_QP(8, 5)
+    RTKV_QP(8, 4) RTKV_QP(10, 4)
 #undef RTKV_QP
   }
 #define RTKV_Q(N)                                                                              \

@@ -556,6 +556,35 @@ def test_packed_only_mode_matches_dual_output(dtype):
         assert torch.equal(a, b)
 
 
+@pytest.mark.parametrize("B,S,dtype", [(1, 16384, "float16"), (1, 4096, "bfloat16"), (2, 3000, "float16")])
+def test_packed_only_selection_matches_dual_output(B, S, dtype):
+    """With a binding selection (dropped tokens, three classes; B = 2: padding rows past a batch row's
+    kept count) the packed-only launch — for 2-byte rows the paired kernel, one task per kept row's K
+    and V rows — writes the same codes, scale/zp and row offsets as the dual-output launch."""
+    import rtkv
+    from rtkv import _lib as L
+    H = 32
+    F = H * 128
+    cfg = config(COVERAGE, 8)
+    P = rtkv.prompt_length(S)
+    K, V = synth.kv(77 + S, B, S, F, dtype)
+    W = synth.attention_slice(77 + S, B, H, S, P, dtype)
+    Kd, Vd, Wd = dev(K, dtype), dev(V, dtype), dev(W, dtype)
+    got = []
+    for flags, deq in ((L.EMIT_DEQUANT | L.EMIT_PACKED, True), (L.EMIT_PACKED, False)):
+        p = rtkv.params_from_config(cfg, 2, P, 0.6, flags)
+        bufs = rtkv.LayerBuffers(B, S, F, TD[dtype], "cuda", (2, 4, 8), emit_dequant=deq, emit_packed=True)
+        res = rtkv.compress_layer(Kd, Vd, Wd, p, bufs, rtkv.Workspace("cuda"))
+        st = res.stats()
+        n = st.total_packed_bytes
+        got.append((bufs.packed_k[:n].clone(), bufs.packed_v[:n].clone(),
+                    bufs.scale_zp[:, :st.max_kept].clone().view(torch.int32), st.max_kept, n))
+    assert got[0][3:] == got[1][3:]
+    assert got[0][3] < S  # the selection dropped tokens
+    for a, b in zip(got[0][:3], got[1][:3]):
+        assert torch.equal(a, b)
+
+
 # ----------------------------------------------------------------------------- full-size properties
 @pytest.mark.parametrize("S,dtype,ratio,H", [(16384, "float16", 0.6, 32), (65536, "float16", 0.4, 32),
                                              (32768, "bfloat16", 0.8, 32),
