@@ -856,7 +856,7 @@ static int launch_quant_vec(const QuantArgs& a, int64_t nch, dim3 grid, hipStrea
   // many waves per SIMD; 0 = one row per task
   static const int pk_pair = [] {
     const char* e = getenv("RTKV_K4_PK_PAIR");
-    return e ? atoi(e) : 3;
+    return e ? atoi(e) : 0;
   }();
   if (!a.out.k_out_dev && a.out.packed_k_dev && pk_waves > 0 && DT != RTKV_F32) {
     const dim3 pgrid((grid.x + 1) / 2);  // half the tasks (grid = one wave per single-row task)
